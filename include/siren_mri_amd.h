@@ -1,0 +1,110 @@
+/*
+ * siren_mri_amd.h — C ABI of the MI355X (gfx950) SIREN SineLayer-stack library.
+ *
+ * The reference (jonbmartin/siren_mri) has no native ABI: its hot path is the Python
+ * module stack modules.SingleBVPNet -> FCBlock -> MetaSequential(BatchLinear, Sine)
+ * (modules.py:11-170) driven by training.train (training.py:19-146). This header is the
+ * boundary the build puts underneath that Python API. Each entry point states which
+ * reference interface it replaces.
+ *
+ * Conventions
+ *  - Plain pointers to DEVICE memory (allocated by the caller, e.g. the PyTorch caching
+ *    allocator); sizes in elements unless a name says bytes.
+ *  - Row-major, contiguous tensors. "rows" = coordinates (batch * points).
+ *  - Every call is asynchronous on `stream` (a hipStream_t passed as void*); no call
+ *    allocates, frees or synchronises, so every call can be captured into a hipGraph.
+ *  - Return value: 0 on success, a negative SIREN_E* code otherwise; the message is
+ *    available from siren_last_error() (thread-local). No C++ exception crosses the ABI.
+ */
+#ifndef SIREN_MRI_AMD_H
+#define SIREN_MRI_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SIREN_MAX_LAYERS 16
+
+/* Arithmetic modes of the layer stack. */
+#define SIREN_PREC_F32  0 /* fp32 operands, exact-fp32 MFMA (v_mfma_f32_32x32x2_f32), libm sin/cos  */
+#define SIREN_PREC_BF16 1 /* bf16 operands, fp32 accumulate, 16-bit phase storage, v_sin/v_cos     */
+
+/* Error codes. */
+#define SIREN_OK 0
+#define SIREN_EINVAL -1   /* unsupported shape / argument                       */
+#define SIREN_ELAUNCH -2  /* a HIP launch failed (hipGetLastError)             */
+#define SIREN_ENOSPACE -3 /* workspace or saved buffer too small               */
+
+/*
+ * Description of one SIREN MLP (an FCBlock with nonlinearity='sine').
+ * Replaces modules.FCBlock.__init__/forward (modules.py:45-97) and the param routing of
+ * torchmeta MetaSequential/get_subdict (torchmeta/modules/container.py:9-19, utils.py:4-11).
+ *
+ *   dims[0]           in_features (coords, or 2m Fourier features)
+ *   dims[1..L-1]      hidden widths (multiples of 32; the MFMA layers need multiples of 32)
+ *   dims[L]           out_features
+ *   layer l computes  z = x_l W_l^T + b_l  (modules.py:25-26), then
+ *                     h = sin(w0 * z)      (modules.py:38) for every layer except the last
+ *                     one when outermost_linear != 0 (modules.py:78-79).
+ *   weights_batched   0: weight[l] is [dims[l+1], dims[l]], shared by all rows
+ *                     1: weight[l] is [batch, dims[l+1], dims[l]] (hypernetwork output,
+ *                        meta_modules.py:42-54); bias[l] is then [batch, dims[l+1]]
+ *   rows_per_batch    points per batch element; x is [batch * rows_per_batch, dims[0]]
+ */
+typedef struct siren_mlp_desc {
+  int32_t num_layers;
+  int32_t dims[SIREN_MAX_LAYERS + 1];
+  int32_t outermost_linear;
+  int32_t prec;
+  int32_t weights_batched;
+  float w0;
+  int64_t batch;
+  int64_t rows_per_batch;
+  const float* weight[SIREN_MAX_LAYERS];
+  const float* bias[SIREN_MAX_LAYERS];
+} siren_mlp_desc;
+
+/* Validates a descriptor; returns SIREN_OK or SIREN_EINVAL (message in siren_last_error). */
+int siren_mlp_check(const siren_mlp_desc* d);
+
+/* Bytes of the per-call "saved" buffer (the activations kept between forward and
+ * backward: one phase tensor per sine layer). */
+int64_t siren_mlp_saved_bytes(const siren_mlp_desc* d);
+
+/* Bytes of scratch workspace a forward or backward call needs. */
+int64_t siren_mlp_workspace_bytes(const siren_mlp_desc* d);
+
+/*
+ * Forward pass: y[rows, dims[L]] = FCBlock(x).
+ * Replaces SingleBVPNet.forward -> FCBlock.forward (modules.py:146-164, 92-97) and the
+ * per-layer BatchLinear.forward + Sine.forward (modules.py:16-27, 35-38).
+ * `saved` may be NULL (inference: nothing is kept for backward).
+ */
+int siren_mlp_forward(const siren_mlp_desc* d, const float* x, float* y, void* saved,
+                      int64_t saved_bytes, void* workspace, int64_t workspace_bytes,
+                      void* stream);
+
+/*
+ * Backward pass from dy = dL/dy. Writes (overwrites) dweight[l], dbias[l] (same shapes as
+ * weight[l], bias[l]) and, if dx != NULL, dx = dL/dx [rows, dims[0]].
+ * Replaces the autograd MmBackward/AddBackward/MulBackward/SinBackward chain that
+ * training.py:91 (train_loss.backward()) runs through the reference modules.
+ */
+int siren_mlp_backward(const siren_mlp_desc* d, const float* x, const float* dy,
+                       const void* saved, int64_t saved_bytes, void* workspace,
+                       int64_t workspace_bytes, float* const* dweight, float* const* dbias,
+                       float* dx, void* stream);
+
+/* Thread-local message of the last failing call ("" if none). */
+const char* siren_last_error(void);
+
+/* Library build string (architecture, HIP version). */
+const char* siren_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SIREN_MRI_AMD_H */

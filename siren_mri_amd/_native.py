@@ -1,0 +1,165 @@
+"""ctypes binding of the C ABI in include/siren_mri_amd.h (libsiren_mri_amd.so).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc --offload-arch=gfx950) and
+loaded lazily at the first kernel call, after ``torch`` so that the kernels register with the
+HIP runtime PyTorch already holds. There is deliberately NO fallback: if the library or a GPU
+is missing, every SIREN kernel entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+MAX_LAYERS = 16
+PREC_F32 = 0
+PREC_BF16 = 1
+PRECISIONS = {"fp32": PREC_F32, "f32": PREC_F32, "float32": PREC_F32,
+              "bf16": PREC_BF16, "bfloat16": PREC_BF16}
+
+LIB_NAME = "libsiren_mri_amd.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+# Every symbol include/siren_mri_amd.h declares (checked by tests/test_native_abi.py).
+EXPORTED_SYMBOLS = (
+    "siren_mlp_check",
+    "siren_mlp_saved_bytes",
+    "siren_mlp_workspace_bytes",
+    "siren_mlp_forward",
+    "siren_mlp_backward",
+    "siren_last_error",
+    "siren_version",
+)
+
+
+class SirenMLPDesc(ctypes.Structure):
+    """Mirror of ``siren_mlp_desc`` (include/siren_mri_amd.h)."""
+
+    _fields_ = [
+        ("num_layers", ctypes.c_int32),
+        ("dims", ctypes.c_int32 * (MAX_LAYERS + 1)),
+        ("outermost_linear", ctypes.c_int32),
+        ("prec", ctypes.c_int32),
+        ("weights_batched", ctypes.c_int32),
+        ("w0", ctypes.c_float),
+        ("batch", ctypes.c_int64),
+        ("rows_per_batch", ctypes.c_int64),
+        ("weight", ctypes.c_void_p * MAX_LAYERS),
+        ("bias", ctypes.c_void_p * MAX_LAYERS),
+    ]
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def _declare(lib):
+    P = ctypes.POINTER(SirenMLPDesc)
+    vp = ctypes.c_void_p
+    i64 = ctypes.c_int64
+    lib.siren_mlp_check.argtypes = [P]
+    lib.siren_mlp_check.restype = ctypes.c_int
+    lib.siren_mlp_saved_bytes.argtypes = [P]
+    lib.siren_mlp_saved_bytes.restype = i64
+    lib.siren_mlp_workspace_bytes.argtypes = [P]
+    lib.siren_mlp_workspace_bytes.restype = i64
+    lib.siren_mlp_forward.argtypes = [P, vp, vp, vp, i64, vp, i64, vp]
+    lib.siren_mlp_forward.restype = ctypes.c_int
+    lib.siren_mlp_backward.argtypes = [P, vp, vp, vp, i64, vp, i64,
+                                       ctypes.POINTER(vp), ctypes.POINTER(vp), vp, vp]
+    lib.siren_mlp_backward.restype = ctypes.c_int
+    lib.siren_last_error.argtypes = []
+    lib.siren_last_error.restype = ctypes.c_char_p
+    lib.siren_version.argtypes = []
+    lib.siren_version.restype = ctypes.c_char_p
+
+
+def load_library(path: str | None = None):
+    """Load (once) and return the native library. Raises if it is missing."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise NativeError(
+                f"siren_mri_amd: native library {p} not found. Build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950).")
+        lib = ctypes.CDLL(p)
+        _declare(lib)
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def lib():
+    return _lib if _lib is not None else load_library()
+
+
+def last_error() -> str:
+    return lib().siren_last_error().decode(errors="replace")
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise NativeError(f"siren_mri_amd.{what} failed ({rc}): {last_error()}")
+
+
+def precision_code(precision) -> int:
+    if isinstance(precision, int):
+        return precision
+    try:
+        return PRECISIONS[str(precision).lower()]
+    except KeyError:
+        raise ValueError(f"unknown precision {precision!r}; use 'fp32' or 'bf16'") from None
+
+
+def stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def make_desc(dims, weights, biases, *, w0: float, prec: int, outermost_linear: bool,
+              weights_batched: bool, batch: int, rows_per_batch: int) -> SirenMLPDesc:
+    L = len(dims) - 1
+    if not 2 <= L <= MAX_LAYERS:
+        raise ValueError(f"siren_mri_amd: {L} linear layers outside [2, {MAX_LAYERS}]")
+    d = SirenMLPDesc()
+    d.num_layers = L
+    for i, v in enumerate(dims):
+        d.dims[i] = int(v)
+    d.outermost_linear = 1 if outermost_linear else 0
+    d.prec = int(prec)
+    d.weights_batched = 1 if weights_batched else 0
+    d.w0 = float(w0)
+    d.batch = int(batch)
+    d.rows_per_batch = int(rows_per_batch)
+    for l in range(L):
+        d.weight[l] = weights[l].data_ptr()
+        d.bias[l] = biases[l].data_ptr()
+    return d
+
+
+def describe_only(dims, *, prec: int, outermost_linear: bool = True, weights_batched: bool = False,
+                  batch: int = 1, rows_per_batch: int = 1, w0: float = 30.0):
+    """Descriptor with fake (aligned, non-null) pointers — for size queries and validation."""
+    L = len(dims) - 1
+    d = SirenMLPDesc()
+    d.num_layers = L
+    for i, v in enumerate(dims):
+        d.dims[i] = int(v)
+    d.outermost_linear = 1 if outermost_linear else 0
+    d.prec = int(prec)
+    d.weights_batched = 1 if weights_batched else 0
+    d.w0 = float(w0)
+    d.batch = int(batch)
+    d.rows_per_batch = int(rows_per_batch)
+    for l in range(L):
+        d.weight[l] = 256 * (l + 1)
+        d.bias[l] = 256 * (l + 1) + 64
+    return d

@@ -1,0 +1,88 @@
+// siren_common.h — shared device helpers for the gfx950 SIREN kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DEV __device__ __forceinline__
+
+namespace siren {
+
+constexpr float kInv2Pi = 0.15915494309189535f;
+constexpr int kPrecF32 = 0;
+constexpr int kPrecBF16 = 1;
+
+typedef __bf16 bf16;
+typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Per-precision storage policy.
+//  phase_t: what a sine layer keeps of its pre-activation between forward and backward.
+//           F32 : p = w0*(xW^T+b) in radians (bit-faithful to modules.py:26,38).
+//           BF16: p reduced mod 2pi and quantised to 16 bits of a revolution (resolution
+//                 9.6e-5 rad); sin/cos are then single v_sin_f32/v_cos_f32 instructions
+//                 (which take revolutions) and the tensor costs 2 B/element in HBM.
+//  grad_t : storage of dL/dz between backward kernels.
+//  op_t   : MFMA operand element.
+template <int PREC> struct Prec;
+
+template <> struct Prec<kPrecF32> {
+  using phase_t = float;
+  using grad_t = float;
+  using op_t = float;
+  static DEV phase_t enc(float p) { return p; }
+  static DEV float sinp(phase_t v) { return sinf(v); }
+  static DEV float cosp(phase_t v) { return cosf(v); }
+};
+
+template <> struct Prec<kPrecBF16> {
+  using phase_t = uint16_t;
+  using grad_t = bf16;
+  using op_t = bf16;
+  static DEV phase_t enc(float p) {
+    float r = p * kInv2Pi;
+    r = r - floorf(r);
+    return (uint16_t)((uint32_t)__builtin_rintf(r * 65536.0f) & 0xFFFFu);
+  }
+  static DEV float rev(phase_t v) { return (float)v * (1.0f / 65536.0f); }
+  static DEV float sinp(phase_t v) { return __builtin_amdgcn_sinf(rev(v)); }
+  static DEV float cosp(phase_t v) { return __builtin_amdgcn_cosf(rev(v)); }
+};
+
+DEV float to_f32(float v) { return v; }
+DEV float to_f32(bf16 v) { return (float)v; }
+
+template <typename T> DEV T from_f32(float v);
+template <> DEV float from_f32<float>(float v) { return v; }
+template <> DEV bf16 from_f32<bf16>(float v) { return (bf16)v; }
+
+DEV float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// ds_read_b64_tr_b16: lane (4q+p) of each 16-lane group supplies the address of row q,
+// columns 4p..4p+3 of a 4x16 block; lane i of the group receives column i of the 4 rows.
+DEV s16x4 lds_read_tr16(const void* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+}
+
+// Two transposing reads (rows k..k+3 and k+4..k+7 of one 16-column block) -> one 8-element bf16
+// MFMA operand. Whole-vector casts only: per-element bit_casts of the v4i16 result were lowered
+// to a duplicating v_perm by hipcc 7.2 (wrong operands, no diagnostic).
+DEV bf16x8 lds_read_tr16_pair(const void* lo_ptr, const void* hi_ptr) {
+  const s16x4 lo = lds_read_tr16(lo_ptr);
+  const s16x4 hi = lds_read_tr16(hi_ptr);
+  const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+}  // namespace siren

@@ -1,0 +1,498 @@
+// siren_runtime.hip — host-side orchestration of the SIREN layer stack behind the C ABI
+// declared in include/siren_mri_amd.h. One call launches every kernel of a forward or a
+// backward pass on the caller's stream; nothing here allocates, frees or synchronises.
+#include <string>
+#include <cstdio>
+#include <cstring>
+#include <algorithm>
+#include <cstdarg>
+
+#include "../../include/siren_mri_amd.h"
+#include "siren_kernels.hip"
+
+using namespace siren;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+constexpr int kTargetBlocks = 1024;  // ~4 workgroups per CU on 256 CUs
+
+// Effective batching: shared weights collapse every row into one weight set.
+struct Geo {
+  int L;
+  int64_t nb;     // weight sets
+  int64_t rows;   // rows per weight set
+  int64_t total;  // all rows
+  int prec;
+  int64_t phase_sz, grad_sz, op_sz;
+};
+
+Geo geo_of(const siren_mlp_desc* d) {
+  Geo g;
+  g.L = d->num_layers;
+  if (d->weights_batched) {
+    g.nb = d->batch;
+    g.rows = d->rows_per_batch;
+  } else {
+    g.nb = 1;
+    g.rows = d->batch * d->rows_per_batch;
+  }
+  g.total = d->batch * d->rows_per_batch;
+  g.prec = d->prec;
+  g.phase_sz = d->prec == SIREN_PREC_BF16 ? 2 : 4;
+  g.grad_sz = g.phase_sz;
+  g.op_sz = g.phase_sz;
+  return g;
+}
+
+int max_hidden(const siren_mlp_desc* d) {
+  int m = 0;
+  for (int l = 1; l < d->num_layers; ++l) m = std::max(m, d->dims[l]);
+  return m;
+}
+
+// Split-K geometry of the weight-gradient reductions.
+struct Split {
+  int64_t nsplit, rows_per_split;
+};
+Split split_rows(int64_t rows, int64_t blocks_per_split, int64_t nb, int64_t granule) {
+  int64_t want = std::max<int64_t>(1, kTargetBlocks / std::max<int64_t>(1, blocks_per_split * nb));
+  int64_t rps = align_up(cdiv(rows, want), granule);
+  rps = std::max<int64_t>(rps, granule);
+  Split s;
+  s.rows_per_split = rps;
+  s.nsplit = std::max<int64_t>(1, cdiv(rows, rps));
+  return s;
+}
+
+Split tn_split(const Geo& g, int M, int N) {
+  const int64_t tiles = cdiv(M, TN_BM) * cdiv(N, TN_BN);
+  return split_rows(g.rows, tiles, g.nb, 64);
+}
+Split valu_split(const Geo& g) { return split_rows(g.rows, 1, g.nb, 16); }
+
+struct Layout {
+  // saved
+  int64_t saved_off[SIREN_MAX_LAYERS];
+  int64_t saved_bytes;
+  // workspace
+  int64_t w_op_off[SIREN_MAX_LAYERS];
+  int64_t wt_op_off[SIREN_MAX_LAYERS];
+  int64_t pp_off[2];     // phase ping-pong (forward without saved buffer)
+  int64_t dz_off[2];     // dZ ping-pong
+  int64_t part_off;
+  int64_t ws_bytes;
+};
+
+Layout layout_of(const siren_mlp_desc* d) {
+  const Geo g = geo_of(d);
+  Layout lo;
+  memset(&lo, 0, sizeof(lo));
+  int64_t off = 0;
+  for (int l = 0; l + 1 < g.L; ++l) {  // one phase tensor per sine layer 0..L-2
+    lo.saved_off[l] = off;
+    off = align_up(off + g.total * d->dims[l + 1] * g.phase_sz, 256);
+  }
+  lo.saved_bytes = off;
+
+  off = 0;
+  for (int l = 1; l + 1 < g.L; ++l) {
+    const int64_t n = g.nb * (int64_t)d->dims[l + 1] * d->dims[l];
+    if (g.prec == SIREN_PREC_BF16) {
+      lo.w_op_off[l] = off;
+      off = align_up(off + n * g.op_sz, 256);
+    } else {
+      lo.w_op_off[l] = -1;
+    }
+    lo.wt_op_off[l] = off;
+    off = align_up(off + n * g.op_sz, 256);
+  }
+  const int64_t act = g.total * (int64_t)max_hidden(d);
+  for (int k = 0; k < 2; ++k) {
+    lo.pp_off[k] = off;
+    off = align_up(off + act * g.phase_sz, 256);
+  }
+  for (int k = 0; k < 2; ++k) {
+    lo.dz_off[k] = off;
+    off = align_up(off + act * g.grad_sz, 256);
+  }
+  int64_t part = 0;
+  for (int l = 1; l + 1 < g.L; ++l) {
+    const int M = d->dims[l + 1], N = d->dims[l];
+    const Split s = tn_split(g, M, N);
+    part = std::max(part, s.nsplit * g.nb * ((int64_t)M * N + M));
+  }
+  {
+    const Split s = valu_split(g);
+    const int F = d->dims[g.L - 1], O = d->dims[g.L];
+    part = std::max(part, s.nsplit * g.nb * ((int64_t)O * F + O));
+    const int F0 = d->dims[1], C = d->dims[0];
+    part = std::max(part, s.nsplit * g.nb * ((int64_t)F0 * C + F0));
+  }
+  lo.part_off = off;
+  off = align_up(off + part * 4, 256);
+  lo.ws_bytes = off;
+  return lo;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(SIREN_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
+  return SIREN_OK;
+}
+
+inline unsigned grid1d(int64_t work, int64_t cap = 4096) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), cap));
+}
+
+template <int PREC>
+int launch_reduce(const float* part, int64_t nsplit, int64_t nb, int64_t slab, int64_t n_first,
+                  float* out0, float* out1, hipStream_t st) {
+  hipLaunchKernelGGL(reduce_kernel, dim3(grid1d(nb * slab, 2048)), dim3(256), 0, st, part,
+                     (int)nsplit, nb, slab, n_first, out0, out1);
+  return check_launch("reduce");
+}
+
+template <int PREC>
+int prep_weights(const siren_mlp_desc* d, const Geo& g, const Layout& lo, char* ws, hipStream_t st) {
+  for (int l = 1; l + 1 < g.L; ++l) {
+    const int O = d->dims[l + 1], I = d->dims[l];
+    void* wop = lo.w_op_off[l] >= 0 ? ws + lo.w_op_off[l] : nullptr;
+    hipLaunchKernelGGL(prep_weight_kernel<PREC>, dim3(grid1d(g.nb * (int64_t)O * I, 1024)),
+                       dim3(256), 0, st, d->weight[l], wop, (void*)(ws + lo.wt_op_off[l]), g.nb, O, I);
+    int rc = check_launch("prep_weight");
+    if (rc) return rc;
+  }
+  return SIREN_OK;
+}
+
+template <int PREC, int IT, int MAXO>
+void launch_last_fwd(const LastFwdArgs& a, int64_t nb, hipStream_t st) {
+  const unsigned gx = grid1d(a.rows_per_batch * 64, std::max<int64_t>(1, 2048 / nb));
+  hipLaunchKernelGGL((last_fwd_kernel<PREC, IT, MAXO>), dim3(gx, (unsigned)nb), dim3(256), 0, st, a);
+}
+
+template <int PREC>
+int dispatch_last_fwd(const LastFwdArgs& a, int64_t nb, hipStream_t st) {
+  const int it = (int)cdiv(a.F, 256);
+  if (a.O <= 2) {
+    if (it == 1) launch_last_fwd<PREC, 1, 2>(a, nb, st);
+    else if (it == 2) launch_last_fwd<PREC, 2, 2>(a, nb, st);
+    else launch_last_fwd<PREC, 4, 2>(a, nb, st);
+  } else {
+    if (it == 1) launch_last_fwd<PREC, 1, 8>(a, nb, st);
+    else if (it == 2) launch_last_fwd<PREC, 2, 8>(a, nb, st);
+    else launch_last_fwd<PREC, 4, 8>(a, nb, st);
+  }
+  return check_launch("last_fwd");
+}
+
+template <int PREC>
+int dispatch_last_bwd(const LastBwdArgs& a, int64_t nsplit, int64_t nb, hipStream_t st) {
+  const int it = (int)cdiv(a.F, 256);
+  dim3 grid((unsigned)nsplit, (unsigned)nb);
+  if (a.O <= 2) {
+    if (it == 1) hipLaunchKernelGGL((last_bwd_kernel<PREC, 1, 2>), grid, dim3(256), 0, st, a);
+    else if (it == 2) hipLaunchKernelGGL((last_bwd_kernel<PREC, 2, 2>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((last_bwd_kernel<PREC, 4, 2>), grid, dim3(256), 0, st, a);
+  } else {
+    if (it == 1) hipLaunchKernelGGL((last_bwd_kernel<PREC, 1, 8>), grid, dim3(256), 0, st, a);
+    else if (it == 2) hipLaunchKernelGGL((last_bwd_kernel<PREC, 2, 8>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((last_bwd_kernel<PREC, 4, 8>), grid, dim3(256), 0, st, a);
+  }
+  return check_launch("last_bwd");
+}
+
+template <int PREC>
+int dispatch_first_bwd(const FirstBwdArgs& a, int64_t nsplit, int64_t nb, hipStream_t st) {
+  const int it = (int)cdiv(a.F, 256);
+  dim3 grid((unsigned)nsplit, (unsigned)nb);
+  if (a.C <= 4) {
+    if (it == 1) hipLaunchKernelGGL((first_bwd_kernel<PREC, 1, 4>), grid, dim3(256), 0, st, a);
+    else if (it == 2) hipLaunchKernelGGL((first_bwd_kernel<PREC, 2, 4>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((first_bwd_kernel<PREC, 4, 4>), grid, dim3(256), 0, st, a);
+  } else if (a.C <= 16) {
+    if (it == 1) hipLaunchKernelGGL((first_bwd_kernel<PREC, 1, 16>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((first_bwd_kernel<PREC, 2, 16>), grid, dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((first_bwd_kernel<PREC, 1, 32>), grid, dim3(256), 0, st, a);
+  }
+  return check_launch("first_bwd");
+}
+
+template <int PREC>
+int forward_impl(const siren_mlp_desc* d, const float* x, float* y, char* saved, char* ws,
+                 hipStream_t st) {
+  const Geo g = geo_of(d);
+  const Layout lo = layout_of(d);
+  int rc = prep_weights<PREC>(d, g, lo, ws, st);
+  if (rc) return rc;
+  auto phase_buf = [&](int l) -> char* {
+    return saved ? saved + lo.saved_off[l] : ws + lo.pp_off[l & 1];
+  };
+  // Layer 0 (VALU).
+  {
+    FirstFwdArgs a;
+    a.x = x;
+    a.W = d->weight[0];
+    a.b = d->bias[0];
+    a.P = phase_buf(0);
+    a.rows_per_batch = g.rows;
+    a.w_bstride = d->weights_batched ? (int64_t)d->dims[1] * d->dims[0] : 0;
+    a.b_bstride = d->weights_batched ? d->dims[1] : 0;
+    a.C = d->dims[0];
+    a.F = d->dims[1];
+    a.w0 = d->w0;
+    const unsigned gx = grid1d(g.rows * (a.F / 4), std::max<int64_t>(1, 4096 / g.nb));
+    hipLaunchKernelGGL(first_fwd_kernel<PREC>, dim3(gx, (unsigned)g.nb), dim3(256), 0, st, a);
+    if ((rc = check_launch("first_fwd"))) return rc;
+  }
+  // Hidden MFMA layers.
+  for (int l = 1; l + 1 < g.L; ++l) {
+    NTArgs a;
+    a.A = phase_buf(l - 1);
+    a.Bt = PREC == kPrecBF16 ? (const void*)(ws + lo.w_op_off[l]) : (const void*)d->weight[l];
+    a.bias = d->bias[l];
+    a.Paux = nullptr;
+    a.C = phase_buf(l);
+    a.rows_per_batch = g.rows;
+    a.bt_bstride = d->weights_batched ? (int64_t)d->dims[l + 1] * d->dims[l] : 0;
+    a.bias_bstride = d->weights_batched ? d->dims[l + 1] : 0;
+    a.K = d->dims[l];
+    a.N = d->dims[l + 1];
+    a.w0 = d->w0;
+    dim3 grid((unsigned)cdiv(g.rows, NT_BM), (unsigned)cdiv(a.N, NT_BN), (unsigned)g.nb);
+    hipLaunchKernelGGL((nt_gemm_kernel<PREC, MODE_FWD>), grid, dim3(256), 0, st, a);
+    if ((rc = check_launch("nt_gemm fwd"))) return rc;
+  }
+  // Output layer (VALU).
+  {
+    const int l = g.L - 1;
+    LastFwdArgs a;
+    a.P = phase_buf(l - 1);
+    a.W = d->weight[l];
+    a.b = d->bias[l];
+    a.y = y;
+    a.rows_per_batch = g.rows;
+    a.w_bstride = d->weights_batched ? (int64_t)d->dims[l + 1] * d->dims[l] : 0;
+    a.b_bstride = d->weights_batched ? d->dims[l + 1] : 0;
+    a.F = d->dims[l];
+    a.O = d->dims[l + 1];
+    a.sine_out = d->outermost_linear ? 0 : 1;
+    a.w0 = d->w0;
+    if ((rc = dispatch_last_fwd<PREC>(a, g.nb, st))) return rc;
+  }
+  return SIREN_OK;
+}
+
+template <int PREC>
+int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, const char* saved,
+                  char* ws, float* const* dW, float* const* db, float* dx, hipStream_t st) {
+  const Geo g = geo_of(d);
+  const Layout lo = layout_of(d);
+  int rc = prep_weights<PREC>(d, g, lo, ws, st);
+  if (rc) return rc;
+  float* part = (float*)(ws + lo.part_off);
+  auto P = [&](int l) -> const void* { return saved + lo.saved_off[l]; };
+  int cur = 0;  // dz ping-pong index holding dZ of the current layer
+  // Output layer: dZ_{L-2}, dW_{L-1}, db_{L-1}.
+  {
+    const int l = g.L - 1;
+    const Split s = valu_split(g);
+    LastBwdArgs a;
+    a.P = P(l - 1);
+    a.W = d->weight[l];
+    a.b = d->bias[l];
+    a.dy = dy;
+    a.dZ = ws + lo.dz_off[cur];
+    a.part = part;
+    a.rows_per_batch = g.rows;
+    a.rows_per_split = s.rows_per_split;
+    a.w_bstride = d->weights_batched ? (int64_t)d->dims[l + 1] * d->dims[l] : 0;
+    a.b_bstride = d->weights_batched ? d->dims[l + 1] : 0;
+    a.F = d->dims[l];
+    a.O = d->dims[l + 1];
+    a.batch = (int)g.nb;
+    a.sine_out = d->outermost_linear ? 0 : 1;
+    a.w0 = d->w0;
+    if ((rc = dispatch_last_bwd<PREC>(a, s.nsplit, g.nb, st))) return rc;
+    if ((rc = launch_reduce<PREC>(part, s.nsplit, g.nb, (int64_t)a.O * a.F + a.O,
+                                  (int64_t)a.O * a.F, dW[l], db[l], st)))
+      return rc;
+  }
+  // Hidden MFMA layers, top to bottom.
+  for (int l = g.L - 2; l >= 1; --l) {
+    const int M = d->dims[l + 1], N = d->dims[l];
+    {
+      const Split s = tn_split(g, M, N);
+      TNArgs a;
+      a.D = ws + lo.dz_off[cur];
+      a.P = P(l - 1);
+      a.part = part;
+      a.rows_per_batch = g.rows;
+      a.rows_per_split = s.rows_per_split;
+      a.M = M;
+      a.N = N;
+      a.batch = (int)g.nb;
+      dim3 grid((unsigned)(cdiv(M, TN_BM) * cdiv(N, TN_BN)), (unsigned)s.nsplit, (unsigned)g.nb);
+      hipLaunchKernelGGL(tn_dw_kernel<PREC>, grid, dim3(256), 0, st, a);
+      if ((rc = check_launch("tn_dw"))) return rc;
+      if ((rc = launch_reduce<PREC>(part, s.nsplit, g.nb, (int64_t)M * N + M, (int64_t)M * N,
+                                    dW[l], db[l], st)))
+        return rc;
+    }
+    {
+      NTArgs a;
+      a.A = ws + lo.dz_off[cur];
+      a.Bt = ws + lo.wt_op_off[l];
+      a.bias = nullptr;
+      a.Paux = P(l - 1);
+      a.C = ws + lo.dz_off[cur ^ 1];
+      a.rows_per_batch = g.rows;
+      a.bt_bstride = d->weights_batched ? (int64_t)M * N : 0;
+      a.bias_bstride = 0;
+      a.K = M;
+      a.N = N;
+      a.w0 = d->w0;
+      dim3 grid((unsigned)cdiv(g.rows, NT_BM), (unsigned)cdiv(N, NT_BN), (unsigned)g.nb);
+      hipLaunchKernelGGL((nt_gemm_kernel<PREC, MODE_DX>), grid, dim3(256), 0, st, a);
+      if ((rc = check_launch("nt_gemm dx"))) return rc;
+      cur ^= 1;
+    }
+  }
+  // First layer.
+  {
+    const Split s = valu_split(g);
+    FirstBwdArgs a;
+    a.dZ = ws + lo.dz_off[cur];
+    a.x = x;
+    a.W = d->weight[0];
+    a.dx = dx;
+    a.part = part;
+    a.rows_per_batch = g.rows;
+    a.rows_per_split = s.rows_per_split;
+    a.w_bstride = d->weights_batched ? (int64_t)d->dims[1] * d->dims[0] : 0;
+    a.F = d->dims[1];
+    a.C = d->dims[0];
+    a.batch = (int)g.nb;
+    if ((rc = dispatch_first_bwd<PREC>(a, s.nsplit, g.nb, st))) return rc;
+    if ((rc = launch_reduce<PREC>(part, s.nsplit, g.nb, (int64_t)a.F * a.C + a.F,
+                                  (int64_t)a.F * a.C, dW[0], db[0], st)))
+      return rc;
+  }
+  return SIREN_OK;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int siren_mlp_check(const siren_mlp_desc* d) {
+  if (!d) return fail(SIREN_EINVAL, "null descriptor");
+  const int L = d->num_layers;
+  if (L < 2 || L > SIREN_MAX_LAYERS)
+    return fail(SIREN_EINVAL, "num_layers=%d outside [2, %d]", L, SIREN_MAX_LAYERS);
+  if (d->prec != SIREN_PREC_F32 && d->prec != SIREN_PREC_BF16)
+    return fail(SIREN_EINVAL, "unknown precision %d", d->prec);
+  if (d->batch < 1 || d->rows_per_batch < 1)
+    return fail(SIREN_EINVAL, "empty input (batch=%lld rows=%lld)", (long long)d->batch,
+                (long long)d->rows_per_batch);
+  if (d->batch > 65535) return fail(SIREN_EINVAL, "batch %lld > 65535", (long long)d->batch);
+  if (d->dims[0] < 1 || d->dims[0] > 32)
+    return fail(SIREN_EINVAL, "in_features=%d unsupported (1..32)", d->dims[0]);
+  if (d->dims[L] < 1 || d->dims[L] > 8)
+    return fail(SIREN_EINVAL, "out_features=%d unsupported (1..8)", d->dims[L]);
+  for (int l = 1; l < L; ++l)
+    if (d->dims[l] < 32 || d->dims[l] % 32 != 0 || d->dims[l] > 1024)
+      return fail(SIREN_EINVAL, "hidden width dims[%d]=%d must be a multiple of 32 in [32, 1024]",
+                  l, d->dims[l]);
+  if (d->dims[0] > 16 && d->dims[1] > 256)
+    return fail(SIREN_EINVAL, "in_features > 16 needs first hidden width <= 256");
+  if (d->dims[0] > 4 && d->dims[1] > 512)
+    return fail(SIREN_EINVAL, "in_features > 4 needs first hidden width <= 512");
+  for (int l = 0; l < L; ++l)
+    if (!d->weight[l] || !d->bias[l]) return fail(SIREN_EINVAL, "layer %d: null weight/bias", l);
+  for (int l = 1; l + 1 < L; ++l)
+    if (!aligned16(d->weight[l])) return fail(SIREN_EINVAL, "layer %d weight not 16-B aligned", l);
+  return SIREN_OK;
+}
+
+int64_t siren_mlp_saved_bytes(const siren_mlp_desc* d) {
+  if (siren_mlp_check(d)) return -1;
+  return layout_of(d).saved_bytes;
+}
+
+int64_t siren_mlp_workspace_bytes(const siren_mlp_desc* d) {
+  if (siren_mlp_check(d)) return -1;
+  return layout_of(d).ws_bytes;
+}
+
+int siren_mlp_forward(const siren_mlp_desc* d, const float* x, float* y, void* saved,
+                      int64_t saved_bytes, void* workspace, int64_t workspace_bytes, void* stream) {
+  int rc = siren_mlp_check(d);
+  if (rc) return rc;
+  const Layout lo = layout_of(d);
+  if (saved && saved_bytes < lo.saved_bytes)
+    return fail(SIREN_ENOSPACE, "saved buffer %lld < %lld bytes", (long long)saved_bytes,
+                (long long)lo.saved_bytes);
+  if (workspace_bytes < lo.ws_bytes || !workspace)
+    return fail(SIREN_ENOSPACE, "workspace %lld < %lld bytes", (long long)workspace_bytes,
+                (long long)lo.ws_bytes);
+  if (!x || !y) return fail(SIREN_EINVAL, "null x or y");
+  hipStream_t st = (hipStream_t)stream;
+  g_err.clear();
+  if (d->prec == SIREN_PREC_BF16)
+    return forward_impl<kPrecBF16>(d, x, y, (char*)saved, (char*)workspace, st);
+  return forward_impl<kPrecF32>(d, x, y, (char*)saved, (char*)workspace, st);
+}
+
+int siren_mlp_backward(const siren_mlp_desc* d, const float* x, const float* dy, const void* saved,
+                       int64_t saved_bytes, void* workspace, int64_t workspace_bytes,
+                       float* const* dweight, float* const* dbias, float* dx, void* stream) {
+  int rc = siren_mlp_check(d);
+  if (rc) return rc;
+  const Layout lo = layout_of(d);
+  if (!saved || saved_bytes < lo.saved_bytes)
+    return fail(SIREN_ENOSPACE, "saved buffer %lld < %lld bytes", (long long)saved_bytes,
+                (long long)lo.saved_bytes);
+  if (workspace_bytes < lo.ws_bytes || !workspace)
+    return fail(SIREN_ENOSPACE, "workspace %lld < %lld bytes", (long long)workspace_bytes,
+                (long long)lo.ws_bytes);
+  if (!x || !dy || !dweight || !dbias) return fail(SIREN_EINVAL, "null argument");
+  for (int l = 0; l < d->num_layers; ++l)
+    if (!dweight[l] || !dbias[l]) return fail(SIREN_EINVAL, "layer %d: null gradient output", l);
+  hipStream_t st = (hipStream_t)stream;
+  g_err.clear();
+  if (d->prec == SIREN_PREC_BF16)
+    return backward_impl<kPrecBF16>(d, x, dy, (const char*)saved, (char*)workspace, dweight, dbias,
+                                    dx, st);
+  return backward_impl<kPrecF32>(d, x, dy, (const char*)saved, (char*)workspace, dweight, dbias, dx,
+                                 st);
+}
+
+const char* siren_last_error(void) { return g_err.c_str(); }
+
+const char* siren_version(void) {
+  static char buf[128];
+  snprintf(buf, sizeof(buf), "siren_mri_amd gfx950 hip %d.%d", HIP_VERSION_MAJOR, HIP_VERSION_MINOR);
+  return buf;
+}
+
+}  // extern "C"

@@ -1,0 +1,114 @@
+"""GPU parity of the native SIREN layer stack (siren_mlp, C ABI siren_mlp_forward/backward)
+against the CPU oracle (oracle/siren_oracle.py, a restatement of modules.py:11-97).
+
+Tolerances (norm-relative, ||a-b||/||b||, per SURVEY.md §7 'Parity tolerances'):
+  fp32 mode : forward <= 1e-5 (north_star), gradients <= 1e-4 (fp32 reduction order over up
+              to 2^18 rows differs from the CPU's)
+  bf16 mode : forward <= 3e-2, gradients <= 5e-2 (bf16 operands, fp32 accumulation)
+The reference is the oracle evaluated in float64 on the same fp32 parameters.
+"""
+import pytest
+import torch
+
+from oracle import siren_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+def _ref(x, params, w0=30.0, outermost_linear=True, loss_w=None):
+    ps = [(W.double().clone().requires_grad_(True), b.double().clone().requires_grad_(True))
+          for W, b in params]
+    xx = x.double().clone().requires_grad_(True)
+    y = orc.siren_forward(xx, ps, w0, outermost_linear)
+    lw = loss_w.double() if loss_w is not None else torch.ones_like(y)
+    (y * lw).sum().backward()
+    return y.detach(), [(W.grad, b.grad) for W, b in ps], xx.grad
+
+
+def _run(x, params, precision, w0=30.0, outermost_linear=True, loss_w=None):
+    from siren_mri_amd.ops import siren_mlp
+    ws = [W.to(DEV).requires_grad_(True) for W, _ in params]
+    bs = [b.to(DEV).requires_grad_(True) for _, b in params]
+    xd = x.to(DEV).requires_grad_(True)
+    y = siren_mlp(xd, ws, bs, w0=w0, precision=precision, outermost_linear=outermost_linear)
+    lw = loss_w.to(DEV) if loss_w is not None else torch.ones_like(y)
+    (y * lw).sum().backward()
+    torch.cuda.synchronize()
+    return y.detach().cpu(), [(w.grad.cpu(), b.grad.cpu()) for w, b in zip(ws, bs)], xd.grad.cpu()
+
+
+TOL = {"fp32": (1e-5, 1e-4), "bf16": (3e-2, 5e-2)}
+
+
+def _check(x, params, precision, **kw):
+    torch.manual_seed(123)
+    y_ref, g_ref, dx_ref = _ref(x, params, **kw)
+    y, g, dx = _run(x, params, precision, **kw)
+    ty, tg = TOL[precision]
+    ey = orc.norm_rel(y, y_ref)
+    assert ey <= ty, f"forward norm-rel {ey:.3e} > {ty}"
+    for l, ((dW, db), (rW, rb)) in enumerate(zip(g, g_ref)):
+        eW, eb = orc.norm_rel(dW, rW), orc.norm_rel(db, rb)
+        assert eW <= tg, f"layer {l} dW norm-rel {eW:.3e} > {tg}"
+        assert eb <= tg, f"layer {l} db norm-rel {eb:.3e} > {tg}"
+    edx = orc.norm_rel(dx, dx_ref)
+    assert edx <= tg, f"dx norm-rel {edx:.3e} > {tg}"
+    return ey
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("side,hidden,nh", [(32, 256, 3), (33, 64, 1), (20, 128, 2), (64, 256, 1)])
+def test_plain_siren(precision, side, hidden, nh):
+    dims = orc.siren_dims(2, hidden, nh, 1)
+    params = orc.siren_init(dims, seed=side)
+    x = orc.get_mgrid(side).unsqueeze(0)
+    lw = torch.randn(1, side * side, 1, generator=torch.Generator().manual_seed(5))
+    _check(x, params, precision, loss_w=lw)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_batched_weights_hypernet_shape(precision):
+    # configs 4/5 shape at reduced size: B weight sets, Fourier-feature input (2m = 16), out 2
+    B, N = 3, 300
+    dims = [16, 256, 256, 256, 256, 2]
+    g = torch.Generator().manual_seed(7)
+    params = []
+    for l in range(len(dims) - 1):
+        base = orc.siren_init(dims, seed=l)[l]
+        W = base[0].unsqueeze(0).repeat(B, 1, 1) * (1 + 0.1 * torch.randn(B, 1, 1, generator=g))
+        b = base[1].unsqueeze(0).repeat(B, 1) + 0.01 * torch.randn(B, dims[l + 1], generator=g)
+        params.append((W.contiguous(), b.contiguous()))
+    x = torch.rand(B, N, 16, generator=g) * 2 - 1
+    lw = torch.randn(B, N, 2, generator=g)
+    _check(x, params, precision, loss_w=lw)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_sine_output_layer(precision):
+    dims = [3, 64, 64, 4]
+    params = orc.siren_init(dims, seed=3)
+    x = torch.rand(1, 129, 3, generator=torch.Generator().manual_seed(1)) * 2 - 1
+    _check(x, params, precision, outermost_linear=False)
+
+
+def test_metric_size_fp32_forward():
+    # the metric configuration (512^2, 5x256) forward in fp32 against the fp64 oracle
+    from siren_mri_amd.ops import siren_mlp
+    dims = orc.siren_dims(2, 256, 3, 1)
+    params = orc.siren_init(dims, seed=0)
+    x = orc.get_mgrid(512).unsqueeze(0)
+    with torch.no_grad():
+        y_ref = orc.siren_forward(x.double(), [(W.double(), b.double()) for W, b in params])
+        y = siren_mlp(x.to(DEV), [W.to(DEV) for W, _ in params], [b.to(DEV) for _, b in params],
+                      precision="fp32")
+    assert orc.norm_rel(y.cpu(), y_ref) <= 1e-5
+
+
+def test_cpu_tensor_raises():
+    from siren_mri_amd.ops import siren_mlp
+    dims = orc.siren_dims(2, 64, 1, 1)
+    params = orc.siren_init(dims, seed=0)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        siren_mlp(torch.zeros(1, 4, 2), [W for W, _ in params], [b for _, b in params])
