@@ -1,0 +1,259 @@
+"""Benchmark: SIREN fitting throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision bf16|fp32]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1]'s metric configuration): the train_img.py
+fit — a 512x512 coordinate grid (262,144 coords per GPU per step, full batch) through a
+5x256 SIREN (SingleBVPNet: 2-256-256-256-256-1, w0=30), image_mse + Adam(lr=1e-4). One step =
+forward + loss + backward + (N>1: one RCCL all-reduce of the 198,401 grads) + Adam. Synthetic
+target: a smooth random image (sum of 32 sinusoids). Multi-GPU is weak scaling: every rank owns
+its own 512^2 block of coordinates (a 512 x 512N image), one gradient all-reduce per step.
+
+Prints ONE JSON line on rank 0 with: value (coord-samples/s, whole job), roofline of the
+dominant kernel (HIP events around each of its launches inside the timed region; FLOPs per
+launch = 2*rows*in*out), cpu_baseline (the CPU oracle timed on this host, rank 0, N=1 only),
+and psnr (64^2 cameraman, 500 steps, this path vs the reference's golden trajectory).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK = {"bf16": (2.5e15, "TFLOP/s"), "fp32": (157.3e12, "TFLOP/s")}
+HBM_PEAK = 8.0e12
+KCLASS_NAMES = {1: "nt_gemm_kernel<fwd> (hidden-layer forward GEMM + bias/w0/sin-phase epilogue)",
+                2: "nt_gemm_kernel<dx> (hidden-layer input-gradient GEMM + cos epilogue)",
+                3: "tn_dw_kernel (hidden-layer weight-gradient split-K GEMM)"}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--side", type=int, default=512)
+    p.add_argument("--hidden", type=int, default=256)
+    p.add_argument("--num-hidden-layers", type=int, default=3)
+    p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-psnr", action="store_true")
+    p.add_argument("--cpu-budget-s", type=float, default=20.0)
+    return p.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    return world, rank, torch.device("cuda", local)
+
+
+def build_step(args, dev, rank, world):
+    from siren_mri_amd import dataio, loss_functions, modules
+    from siren_mri_amd.training_ddp import GradAllReducer
+    torch.manual_seed(0)
+    model = modules.SingleBVPNet(type="sine", mode="mlp", hidden_features=args.hidden,
+                                 num_hidden_layers=args.num_hidden_layers, sidelength=(args.side, args.side),
+                                 precision=args.precision).to(dev)
+    coords = dataio.get_mgrid(args.side)[None].to(dev)
+    img = dataio.smooth_random_image(args.side, seed=rank)
+    gt = {"img": torch.from_numpy(img).reshape(1, -1, 1).to(dev)}
+    opt = torch.optim.Adam(lr=1e-4, params=model.parameters())
+    reducer = GradAllReducer(model.parameters(), op="sum") if world > 1 else None
+    model_input = {"coords": coords}
+
+    def step():
+        out = model(model_input)
+        loss = loss_functions.image_mse(None, out, gt, high_freq=False)["img_loss"]
+        loss.backward()
+        if reducer is not None:
+            reducer()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    return step, model
+
+
+def layer_flops(args, kclass):
+    rows = args.side * args.side
+    return 2.0 * rows * args.hidden * args.hidden
+
+
+def timed_region(step, steps, world):
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(args, budget_s):
+    """The CPU oracle (oracle/siren_oracle.py, the reference algorithm on PyTorch-CPU fp32)
+    running the same 512^2 5x256 fit step, timed on this host's cores."""
+    from oracle import siren_oracle as orc
+    torch.manual_seed(0)
+    model = orc.OracleSiren(hidden_features=args.hidden, num_hidden_layers=args.num_hidden_layers, seed=0)
+    coords = orc.get_mgrid(args.side)[None]
+    from siren_mri_amd import dataio
+    gt = {"img": torch.from_numpy(dataio.smooth_random_image(args.side, seed=0)).reshape(1, -1, 1)}
+    opt = torch.optim.Adam(lr=1e-4, params=model.parameters())
+
+    def step():
+        out = model({"coords": coords})
+        loss = orc.image_mse(None, out, gt, high_freq=False)["img_loss"]
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+
+    step()  # warm-up
+    times = []
+    t_start = time.perf_counter()
+    while len(times) < 5 and (time.perf_counter() - t_start) < budget_s:
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return {"value": args.side * args.side / med, "unit": "coord-samples/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle SingleBVPNet restatement (PyTorch-CPU fp32, autograd, Adam), 1 warm-up + "
+                      f"{len(times)} timed full {args.side}x{args.side} steps, median {med:.3f} s/step, "
+                      f"{torch.get_num_threads()} threads on {os.cpu_count()} visible CPUs"}
+
+
+def psnr_check(args, dev):
+    """64^2 cameraman, 3 hidden layers, Adam 1e-4, seed 0: PSNR at steps 0/50/100/200/500 vs the
+    reference's trajectory recorded in tests/golden/psnr_c1.npz (image_mse, high_freq=False)."""
+    from siren_mri_amd import dataio, loss_functions, modules, utils
+    gold = np.load(os.path.join(ROOT, "tests", "golden", "psnr_c1.npz"), allow_pickle=False)
+    steps = list(gold["steps"])
+    img = dataio.Implicit2DWrapper(dataio.Camera(), sidelength=64)[0][1]["img"][None].to(dev)
+    coords = dataio.get_mgrid(64)[None].to(dev)
+    res = {}
+    for prec in (args.precision, "fp32") if args.precision != "fp32" else ("fp32",):
+        torch.manual_seed(0)
+        m = modules.SingleBVPNet(type="sine", hidden_features=256, num_hidden_layers=3, sidelength=(64, 64),
+                                 precision=prec).to(dev)
+        opt = torch.optim.Adam(lr=1e-4, params=m.parameters())
+        vals = []
+        for s in range(max(steps) + 1):
+            out = m({"coords": coords})
+            if s in steps:
+                vals.append(utils.psnr(dataio.lin2img(out["model_out"].detach()).cpu().numpy()[0],
+                                       dataio.lin2img(img).cpu().numpy()[0]))
+            loss = loss_functions.image_mse(None, out, {"img": img}, high_freq=False)["img_loss"]
+            loss.backward()
+            opt.step()
+            opt.zero_grad()
+        res[prec] = [round(v, 3) for v in vals]
+    return {"steps": [int(s) for s in steps], "reference": [round(float(v), 3) for v in gold["nh3_psnr"]],
+            **{f"siren_mri_amd_{k}": v for k, v in res.items()},
+            "config": "64x64 cameraman, SingleBVPNet 3 hidden x 256, Adam 1e-4, seed 0"}
+
+
+def traffic_from_profile(kclass, args):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        key = f"{args.precision}:{args.side}:{args.hidden}:{kclass}"
+        return d.get(key)
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    world, rank, dev = setup_dist(args)
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    from siren_mri_amd import _native
+    _native.load_library()
+
+    step, model = build_step(args, dev, rank, world)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # pick the dominant kernel class from a short untimed probe (3 steps per class)
+    totals = {}
+    for kc in (_native.KCLASS_FWD_GEMM, _native.KCLASS_DX_GEMM, _native.KCLASS_DW_GEMM):
+        with _native.KernelTimer(kc) as t:
+            for _ in range(3):
+                step()
+        totals[kc] = t.total_ms
+    dom = max(totals, key=totals.get)
+
+    with _native.KernelTimer(dom, max_launches=max(64, 8 * args.steps)) as kt:
+        elapsed = timed_region(step, args.steps, world)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+
+    coords_per_rank = args.side * args.side
+    value = world * coords_per_rank * args.steps / elapsed
+    avg_s = kt.avg_ms * 1e-3
+    flops = layer_flops(args, dom)
+    peak, unit = PEAK[args.precision]
+    achieved = flops / avg_s if avg_s > 0 else float("nan")
+    roofline = {"bound": "mfma", "kernel": KCLASS_NAMES[dom], "achieved": round(achieved / 1e12, 2),
+                "peak": round(peak / 1e12, 1), "unit": unit, "frac": round(achieved / peak, 4),
+                "traffic": traffic_from_profile(dom, args),
+                "flops_per_launch": flops, "avg_launch_ms": round(kt.avg_ms, 4), "launches": kt.launches,
+                "kernel_class_ms_per_3_steps": {KCLASS_NAMES[k].split(" ")[0] + f"[{k}]": round(v, 3)
+                                                for k, v in totals.items()}}
+    result = {
+        "metric": "coord-samples/sec/step, 5x256 SIREN on 512^2 grid; PSNR vs ref",
+        "value": value,
+        "unit": "coord-samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.precision,
+        "data": "synthetic (smooth random 512^2 image per rank: 32 sinusoids; coords = get_mgrid(512))",
+        "config": {"workload": f"train_img.py fit step: {args.side}x{args.side} coordinate grid per GPU, "
+                               f"SingleBVPNet 2-{'-'.join([str(args.hidden)] * (args.num_hidden_layers + 1))}-1 "
+                               f"(w0=30), image_mse + Adam(1e-4), full batch",
+                   "coords_per_gpu_step": coords_per_rank, "global_batch": world * coords_per_rank,
+                   "parallelism": f"dp{world} (coordinate-sharded, one gradient all-reduce per step)"},
+        "roofline": roofline,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args, args.cpu_budget_s)
+    if rank == 0 and world == 1 and not args.no_psnr:
+        result["psnr"] = psnr_check(args, dev)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

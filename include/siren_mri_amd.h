@@ -97,6 +97,20 @@ int siren_mlp_backward(const siren_mlp_desc* d, const float* x, const float* dy,
                        int64_t workspace_bytes, float* const* dweight, float* const* dbias,
                        float* dx, void* stream);
 
+/*
+ * Optional per-kernel-class timing, for benchmarks and profiling (not thread-safe; not for use
+ * under hipGraph capture). While enabled, each launch of `kernel_class` is bracketed by a
+ * hipEventRecord pair on the launch's stream (at most `max_launches` launches are recorded).
+ * siren_timing_collect synchronises on the recorded events and returns the summed duration.
+ */
+#define SIREN_KCLASS_NONE 0
+#define SIREN_KCLASS_FWD_GEMM 1 /* hidden-layer forward GEMM + bias/w0/phase epilogue     */
+#define SIREN_KCLASS_DX_GEMM 2  /* hidden-layer input-gradient GEMM + cos-weighted epilogue */
+#define SIREN_KCLASS_DW_GEMM 3  /* hidden-layer weight-gradient split-K GEMM               */
+int siren_timing_enable(int kernel_class, int max_launches);
+int siren_timing_collect(double* total_ms, int64_t* launches);
+void siren_timing_disable(void);
+
 /* Thread-local message of the last failing call ("" if none). */
 const char* siren_last_error(void);
 

@@ -29,9 +29,16 @@ EXPORTED_SYMBOLS = (
     "siren_mlp_workspace_bytes",
     "siren_mlp_forward",
     "siren_mlp_backward",
+    "siren_timing_enable",
+    "siren_timing_collect",
+    "siren_timing_disable",
     "siren_last_error",
     "siren_version",
 )
+
+KCLASS_FWD_GEMM = 1
+KCLASS_DX_GEMM = 2
+KCLASS_DW_GEMM = 3
 
 
 class SirenMLPDesc(ctypes.Structure):
@@ -74,6 +81,12 @@ def _declare(lib):
     lib.siren_mlp_backward.argtypes = [P, vp, vp, vp, i64, vp, i64,
                                        ctypes.POINTER(vp), ctypes.POINTER(vp), vp, vp]
     lib.siren_mlp_backward.restype = ctypes.c_int
+    lib.siren_timing_enable.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.siren_timing_enable.restype = ctypes.c_int
+    lib.siren_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64)]
+    lib.siren_timing_collect.restype = ctypes.c_int
+    lib.siren_timing_disable.argtypes = []
+    lib.siren_timing_disable.restype = None
     lib.siren_last_error.argtypes = []
     lib.siren_last_error.restype = ctypes.c_char_p
     lib.siren_version.argtypes = []
@@ -163,3 +176,33 @@ def describe_only(dims, *, prec: int, outermost_linear: bool = True, weights_bat
         d.weight[l] = 256 * (l + 1)
         d.bias[l] = 256 * (l + 1) + 64
     return d
+
+
+class KernelTimer:
+    """Context manager: HIP-event timing of every launch of one kernel class (see
+    siren_timing_enable in include/siren_mri_amd.h)."""
+
+    def __init__(self, kernel_class: int, max_launches: int = 4096):
+        self.kernel_class = kernel_class
+        self.max_launches = max_launches
+        self.total_ms = 0.0
+        self.launches = 0
+
+    def __enter__(self):
+        check(lib().siren_timing_enable(self.kernel_class, self.max_launches), "siren_timing_enable")
+        return self
+
+    def __exit__(self, *exc):
+        tot = ctypes.c_double(0.0)
+        n = ctypes.c_int64(0)
+        try:
+            check(lib().siren_timing_collect(ctypes.byref(tot), ctypes.byref(n)), "siren_timing_collect")
+        finally:
+            lib().siren_timing_disable()
+        self.total_ms = tot.value
+        self.launches = n.value
+        return False
+
+    @property
+    def avg_ms(self) -> float:
+        return self.total_ms / self.launches if self.launches else float("nan")

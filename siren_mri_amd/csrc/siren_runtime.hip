@@ -8,7 +8,8 @@
 #include <cstdarg>
 
 #include "../../include/siren_mri_amd.h"
-#include "siren_kernels.hip"
+#include "siren_valu.hip"
+#include "siren_gemm.hip"
 
 using namespace siren;
 
@@ -84,7 +85,10 @@ Split tn_split(const Geo& g, int M, int N) {
   const int64_t tiles = cdiv(M, TN_BM) * cdiv(N, TN_BN);
   return split_rows(g.rows, tiles, g.nb, 64);
 }
-Split valu_split(const Geo& g) { return split_rows(g.rows, 1, g.nb, 16); }
+Split valu_split(const Geo& g) { return split_rows(g.rows, 1, g.nb, 64); }
+
+// Distance between consecutive split slabs (all weight sets of one split), padded to float4.
+int64_t split_stride(const Geo& g, int64_t slab) { return align_up(g.nb * slab, 4); }
 
 struct Layout {
   // saved
@@ -97,20 +101,15 @@ struct Layout {
   int64_t dz_off[2];     // dZ ping-pong
   int64_t part_off;
   int64_t ws_bytes;
+  int64_t weights_bytes;  // prepared MFMA weights (front of `saved`, or of the workspace)
 };
 
 Layout layout_of(const siren_mlp_desc* d) {
   const Geo g = geo_of(d);
   Layout lo;
   memset(&lo, 0, sizeof(lo));
+  // saved = [prepared MFMA weights][one phase tensor per sine layer 0..L-2]
   int64_t off = 0;
-  for (int l = 0; l + 1 < g.L; ++l) {  // one phase tensor per sine layer 0..L-2
-    lo.saved_off[l] = off;
-    off = align_up(off + g.total * d->dims[l + 1] * g.phase_sz, 256);
-  }
-  lo.saved_bytes = off;
-
-  off = 0;
   for (int l = 1; l + 1 < g.L; ++l) {
     const int64_t n = g.nb * (int64_t)d->dims[l + 1] * d->dims[l];
     if (g.prec == SIREN_PREC_BF16) {
@@ -122,6 +121,15 @@ Layout layout_of(const siren_mlp_desc* d) {
     lo.wt_op_off[l] = off;
     off = align_up(off + n * g.op_sz, 256);
   }
+  lo.weights_bytes = off;
+  for (int l = 0; l + 1 < g.L; ++l) {
+    lo.saved_off[l] = off;
+    off = align_up(off + g.total * d->dims[l + 1] * g.phase_sz, 256);
+  }
+  lo.saved_bytes = off;
+
+  // workspace = [prepared weights when no saved buffer][phase ping-pong][dZ ping-pong][partials]
+  off = align_up(lo.weights_bytes, 256);
   const int64_t act = g.total * (int64_t)max_hidden(d);
   for (int k = 0; k < 2; ++k) {
     lo.pp_off[k] = off;
@@ -135,14 +143,14 @@ Layout layout_of(const siren_mlp_desc* d) {
   for (int l = 1; l + 1 < g.L; ++l) {
     const int M = d->dims[l + 1], N = d->dims[l];
     const Split s = tn_split(g, M, N);
-    part = std::max(part, s.nsplit * g.nb * ((int64_t)M * N + M));
+    part = std::max(part, s.nsplit * split_stride(g, (int64_t)M * N + M));
   }
   {
     const Split s = valu_split(g);
     const int F = d->dims[g.L - 1], O = d->dims[g.L];
-    part = std::max(part, s.nsplit * g.nb * ((int64_t)O * F + O));
+    part = std::max(part, s.nsplit * split_stride(g, (int64_t)O * F + O));
     const int F0 = d->dims[1], C = d->dims[0];
-    part = std::max(part, s.nsplit * g.nb * ((int64_t)F0 * C + F0));
+    part = std::max(part, s.nsplit * split_stride(g, (int64_t)F0 * C + F0));
   }
   lo.part_off = off;
   off = align_up(off + part * 4, 256);
@@ -156,34 +164,65 @@ int check_launch(const char* what) {
   return SIREN_OK;
 }
 
+// Optional per-kernel-class timing (bench / profiling only): while enabled, every launch of the
+// selected class is bracketed by a hipEventRecord pair on its own stream.
+struct Timing {
+  int cls = 0;
+  int cap = 0;
+  int used = 0;
+  hipEvent_t* ev = nullptr;
+};
+Timing g_timing;
+
+inline void tmark_begin(int cls, hipStream_t st) {
+  if (g_timing.cls == cls && g_timing.used < g_timing.cap)
+    (void)hipEventRecord(g_timing.ev[2 * g_timing.used], st);
+}
+inline void tmark_end(int cls, hipStream_t st) {
+  if (g_timing.cls == cls && g_timing.used < g_timing.cap) {
+    (void)hipEventRecord(g_timing.ev[2 * g_timing.used + 1], st);
+    ++g_timing.used;
+  }
+}
+
 inline unsigned grid1d(int64_t work, int64_t cap = 4096) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), cap));
 }
 
-template <int PREC>
-int launch_reduce(const float* part, int64_t nsplit, int64_t nb, int64_t slab, int64_t n_first,
-                  float* out0, float* out1, hipStream_t st) {
-  hipLaunchKernelGGL(reduce_kernel, dim3(grid1d(nb * slab, 2048)), dim3(256), 0, st, part,
-                     (int)nsplit, nb, slab, n_first, out0, out1);
+int launch_reduce(const float* part, int64_t nsplit, int64_t sstride, int64_t nb, int64_t slab,
+                  int64_t n_first, float* out0, float* out1, hipStream_t st) {
+  const int64_t total = nb * slab;
+  hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)cdiv(total, 128)), dim3(256), 0, st, part,
+                     (int)nsplit, sstride, (int)total, (int)slab, (int)n_first, out0, out1);
   return check_launch("reduce");
 }
 
+// Convert every MFMA layer's weights (bf16 copy + transpose) into `dst` in one launch.
 template <int PREC>
-int prep_weights(const siren_mlp_desc* d, const Geo& g, const Layout& lo, char* ws, hipStream_t st) {
+int prep_weights(const siren_mlp_desc* d, const Geo& g, const Layout& lo, char* dst, hipStream_t st) {
+  if (g.L < 3) return SIREN_OK;
+  PrepArgs pa;
+  memset(&pa, 0, sizeof(pa));
+  int64_t maxn = 0;
   for (int l = 1; l + 1 < g.L; ++l) {
-    const int O = d->dims[l + 1], I = d->dims[l];
-    void* wop = lo.w_op_off[l] >= 0 ? ws + lo.w_op_off[l] : nullptr;
-    hipLaunchKernelGGL(prep_weight_kernel<PREC>, dim3(grid1d(g.nb * (int64_t)O * I, 1024)),
-                       dim3(256), 0, st, d->weight[l], wop, (void*)(ws + lo.wt_op_off[l]), g.nb, O, I);
-    int rc = check_launch("prep_weight");
-    if (rc) return rc;
+    const int k = l - 1;
+    pa.W[k] = d->weight[l];
+    pa.Wop[k] = lo.w_op_off[l] >= 0 ? dst + lo.w_op_off[l] : nullptr;
+    pa.Wt[k] = dst + lo.wt_op_off[l];
+    pa.O[k] = d->dims[l + 1];
+    pa.I[k] = d->dims[l];
+    maxn = std::max(maxn, (int64_t)pa.O[k] * pa.I[k]);
   }
-  return SIREN_OK;
+  pa.nb = g.nb;
+  hipLaunchKernelGGL(prep_weights_kernel<PREC>, dim3(grid1d(g.nb * maxn, 512), (unsigned)(g.L - 2)),
+                     dim3(256), 0, st, pa);
+  return check_launch("prep_weights");
 }
 
 template <int PREC, int IT, int MAXO>
 void launch_last_fwd(const LastFwdArgs& a, int64_t nb, hipStream_t st) {
-  const unsigned gx = grid1d(a.rows_per_batch * 64, std::max<int64_t>(1, 2048 / nb));
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(a.rows_per_batch, 8),
+                                                                      std::max<int64_t>(1, 4096 / nb)));
   hipLaunchKernelGGL((last_fwd_kernel<PREC, IT, MAXO>), dim3(gx, (unsigned)nb), dim3(256), 0, st, a);
 }
 
@@ -226,13 +265,32 @@ int dispatch_first_bwd(const FirstBwdArgs& a, int64_t nsplit, int64_t nb, hipStr
     if (it == 1) hipLaunchKernelGGL((first_bwd_kernel<PREC, 1, 4>), grid, dim3(256), 0, st, a);
     else if (it == 2) hipLaunchKernelGGL((first_bwd_kernel<PREC, 2, 4>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((first_bwd_kernel<PREC, 4, 4>), grid, dim3(256), 0, st, a);
-  } else if (a.C <= 16) {
+  } else {
     if (it == 1) hipLaunchKernelGGL((first_bwd_kernel<PREC, 1, 16>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((first_bwd_kernel<PREC, 2, 16>), grid, dim3(256), 0, st, a);
-  } else {
-    hipLaunchKernelGGL((first_bwd_kernel<PREC, 1, 32>), grid, dim3(256), 0, st, a);
   }
   return check_launch("first_bwd");
+}
+
+// One hidden-layer GEMM launch (MODE_FWD or MODE_DX). Persistent grid: one 512-thread workgroup
+// per CU (~131 KB LDS each), spread over weight sets and 256-column tiles.
+template <int PREC, int MODE>
+int launch_nt(const NTArgs& a, int64_t nb, int kclass, hipStream_t st) {
+  const int ntn = (int)cdiv(a.N, 256);
+  const int kmax = a.K <= 256 ? 256 : 512;
+  const int bm = PREC == kPrecBF16 ? 64 * 256 / kmax : 32;
+  const int64_t tiles = cdiv(a.rows_per_batch, bm);
+  const int64_t per = std::max<int64_t>(1, 256 / std::max<int64_t>(1, nb * ntn));
+  dim3 grid((unsigned)std::min<int64_t>(tiles, per), (unsigned)nb, (unsigned)ntn);
+  tmark_begin(kclass, st);
+  if constexpr (PREC == kPrecBF16) {
+    if (kmax == 256) hipLaunchKernelGGL((nt_bf16_kernel<MODE, 256>), grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((nt_bf16_kernel<MODE, 512>), grid, dim3(512), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((nt_f32_kernel<MODE>), grid, dim3(512), 0, st, a);
+  }
+  tmark_end(kclass, st);
+  return check_launch(MODE == MODE_FWD ? "nt_gemm fwd" : "nt_gemm dx");
 }
 
 template <int PREC>
@@ -240,7 +298,8 @@ int forward_impl(const siren_mlp_desc* d, const float* x, float* y, char* saved,
                  hipStream_t st) {
   const Geo g = geo_of(d);
   const Layout lo = layout_of(d);
-  int rc = prep_weights<PREC>(d, g, lo, ws, st);
+  char* wbuf = saved ? saved : ws;  // prepared weights live in `saved` so backward reuses them
+  int rc = prep_weights<PREC>(d, g, lo, wbuf, st);
   if (rc) return rc;
   auto phase_buf = [&](int l) -> char* {
     return saved ? saved + lo.saved_off[l] : ws + lo.pp_off[l & 1];
@@ -258,27 +317,28 @@ int forward_impl(const siren_mlp_desc* d, const float* x, float* y, char* saved,
     a.C = d->dims[0];
     a.F = d->dims[1];
     a.w0 = d->w0;
-    const unsigned gx = grid1d(g.rows * (a.F / 4), std::max<int64_t>(1, 4096 / g.nb));
-    hipLaunchKernelGGL(first_fwd_kernel<PREC>, dim3(gx, (unsigned)g.nb), dim3(256), 0, st, a);
+    const unsigned gx = grid1d(g.rows * (a.F / 8), std::max<int64_t>(1, 4096 / g.nb));
+    if (a.C <= 4)
+      hipLaunchKernelGGL((first_fwd_kernel<PREC, 4>), dim3(gx, (unsigned)g.nb), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((first_fwd_kernel<PREC, 16>), dim3(gx, (unsigned)g.nb), dim3(256), 0, st, a);
     if ((rc = check_launch("first_fwd"))) return rc;
   }
   // Hidden MFMA layers.
   for (int l = 1; l + 1 < g.L; ++l) {
     NTArgs a;
     a.A = phase_buf(l - 1);
-    a.Bt = PREC == kPrecBF16 ? (const void*)(ws + lo.w_op_off[l]) : (const void*)d->weight[l];
+    a.W = PREC == kPrecBF16 ? (const void*)(wbuf + lo.w_op_off[l]) : (const void*)d->weight[l];
     a.bias = d->bias[l];
     a.Paux = nullptr;
     a.C = phase_buf(l);
     a.rows_per_batch = g.rows;
-    a.bt_bstride = d->weights_batched ? (int64_t)d->dims[l + 1] * d->dims[l] : 0;
+    a.w_bstride = d->weights_batched ? (int64_t)d->dims[l + 1] * d->dims[l] : 0;
     a.bias_bstride = d->weights_batched ? d->dims[l + 1] : 0;
     a.K = d->dims[l];
     a.N = d->dims[l + 1];
     a.w0 = d->w0;
-    dim3 grid((unsigned)cdiv(g.rows, NT_BM), (unsigned)cdiv(a.N, NT_BN), (unsigned)g.nb);
-    hipLaunchKernelGGL((nt_gemm_kernel<PREC, MODE_FWD>), grid, dim3(256), 0, st, a);
-    if ((rc = check_launch("nt_gemm fwd"))) return rc;
+    if ((rc = launch_nt<PREC, MODE_FWD>(a, g.nb, SIREN_KCLASS_FWD_GEMM, st))) return rc;
   }
   // Output layer (VALU).
   {
@@ -305,8 +365,7 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
                   char* ws, float* const* dW, float* const* db, float* dx, hipStream_t st) {
   const Geo g = geo_of(d);
   const Layout lo = layout_of(d);
-  int rc = prep_weights<PREC>(d, g, lo, ws, st);
-  if (rc) return rc;
+  int rc = SIREN_OK;
   float* part = (float*)(ws + lo.part_off);
   auto P = [&](int l) -> const void* { return saved + lo.saved_off[l]; };
   int cur = 0;  // dz ping-pong index holding dZ of the current layer
@@ -323,16 +382,16 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
     a.part = part;
     a.rows_per_batch = g.rows;
     a.rows_per_split = s.rows_per_split;
-    a.w_bstride = d->weights_batched ? (int64_t)d->dims[l + 1] * d->dims[l] : 0;
-    a.b_bstride = d->weights_batched ? d->dims[l + 1] : 0;
     a.F = d->dims[l];
     a.O = d->dims[l + 1];
-    a.batch = (int)g.nb;
+    a.split_stride = split_stride(g, (int64_t)a.O * a.F + a.O);
+    a.w_bstride = d->weights_batched ? (int64_t)d->dims[l + 1] * d->dims[l] : 0;
+    a.b_bstride = d->weights_batched ? d->dims[l + 1] : 0;
     a.sine_out = d->outermost_linear ? 0 : 1;
     a.w0 = d->w0;
     if ((rc = dispatch_last_bwd<PREC>(a, s.nsplit, g.nb, st))) return rc;
-    if ((rc = launch_reduce<PREC>(part, s.nsplit, g.nb, (int64_t)a.O * a.F + a.O,
-                                  (int64_t)a.O * a.F, dW[l], db[l], st)))
+    if ((rc = launch_reduce(part, s.nsplit, a.split_stride, g.nb, (int64_t)a.O * a.F + a.O,
+                            (int64_t)a.O * a.F, dW[l], db[l], st)))
       return rc;
   }
   // Hidden MFMA layers, top to bottom.
@@ -346,32 +405,32 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
       a.part = part;
       a.rows_per_batch = g.rows;
       a.rows_per_split = s.rows_per_split;
+      a.split_stride = split_stride(g, (int64_t)M * N + M);
       a.M = M;
       a.N = N;
-      a.batch = (int)g.nb;
       dim3 grid((unsigned)(cdiv(M, TN_BM) * cdiv(N, TN_BN)), (unsigned)s.nsplit, (unsigned)g.nb);
+      tmark_begin(SIREN_KCLASS_DW_GEMM, st);
       hipLaunchKernelGGL(tn_dw_kernel<PREC>, grid, dim3(256), 0, st, a);
+      tmark_end(SIREN_KCLASS_DW_GEMM, st);
       if ((rc = check_launch("tn_dw"))) return rc;
-      if ((rc = launch_reduce<PREC>(part, s.nsplit, g.nb, (int64_t)M * N + M, (int64_t)M * N,
-                                    dW[l], db[l], st)))
+      if ((rc = launch_reduce(part, s.nsplit, a.split_stride, g.nb, (int64_t)M * N + M,
+                              (int64_t)M * N, dW[l], db[l], st)))
         return rc;
     }
     {
       NTArgs a;
       a.A = ws + lo.dz_off[cur];
-      a.Bt = ws + lo.wt_op_off[l];
+      a.W = saved + lo.wt_op_off[l];
       a.bias = nullptr;
       a.Paux = P(l - 1);
       a.C = ws + lo.dz_off[cur ^ 1];
       a.rows_per_batch = g.rows;
-      a.bt_bstride = d->weights_batched ? (int64_t)M * N : 0;
+      a.w_bstride = d->weights_batched ? (int64_t)M * N : 0;
       a.bias_bstride = 0;
       a.K = M;
       a.N = N;
       a.w0 = d->w0;
-      dim3 grid((unsigned)cdiv(g.rows, NT_BM), (unsigned)cdiv(N, NT_BN), (unsigned)g.nb);
-      hipLaunchKernelGGL((nt_gemm_kernel<PREC, MODE_DX>), grid, dim3(256), 0, st, a);
-      if ((rc = check_launch("nt_gemm dx"))) return rc;
+      if ((rc = launch_nt<PREC, MODE_DX>(a, g.nb, SIREN_KCLASS_DX_GEMM, st))) return rc;
       cur ^= 1;
     }
   }
@@ -386,13 +445,13 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
     a.part = part;
     a.rows_per_batch = g.rows;
     a.rows_per_split = s.rows_per_split;
-    a.w_bstride = d->weights_batched ? (int64_t)d->dims[1] * d->dims[0] : 0;
     a.F = d->dims[1];
     a.C = d->dims[0];
-    a.batch = (int)g.nb;
+    a.split_stride = split_stride(g, (int64_t)a.F * a.C + a.F);
+    a.w_bstride = d->weights_batched ? (int64_t)d->dims[1] * d->dims[0] : 0;
     if ((rc = dispatch_first_bwd<PREC>(a, s.nsplit, g.nb, st))) return rc;
-    if ((rc = launch_reduce<PREC>(part, s.nsplit, g.nb, (int64_t)a.F * a.C + a.F,
-                                  (int64_t)a.F * a.C, dW[0], db[0], st)))
+    if ((rc = launch_reduce(part, s.nsplit, a.split_stride, g.nb, (int64_t)a.F * a.C + a.F,
+                            (int64_t)a.F * a.C, dW[0], db[0], st)))
       return rc;
   }
   return SIREN_OK;
@@ -415,18 +474,19 @@ int siren_mlp_check(const siren_mlp_desc* d) {
     return fail(SIREN_EINVAL, "empty input (batch=%lld rows=%lld)", (long long)d->batch,
                 (long long)d->rows_per_batch);
   if (d->batch > 65535) return fail(SIREN_EINVAL, "batch %lld > 65535", (long long)d->batch);
-  if (d->dims[0] < 1 || d->dims[0] > 32)
-    return fail(SIREN_EINVAL, "in_features=%d unsupported (1..32)", d->dims[0]);
+  if (d->dims[0] < 1 || d->dims[0] > 16)
+    return fail(SIREN_EINVAL, "in_features=%d unsupported (1..16)", d->dims[0]);
   if (d->dims[L] < 1 || d->dims[L] > 8)
     return fail(SIREN_EINVAL, "out_features=%d unsupported (1..8)", d->dims[L]);
+  const int hmax = d->prec == SIREN_PREC_BF16 ? 512 : 256;
   for (int l = 1; l < L; ++l)
-    if (d->dims[l] < 32 || d->dims[l] % 32 != 0 || d->dims[l] > 1024)
-      return fail(SIREN_EINVAL, "hidden width dims[%d]=%d must be a multiple of 32 in [32, 1024]",
-                  l, d->dims[l]);
-  if (d->dims[0] > 16 && d->dims[1] > 256)
-    return fail(SIREN_EINVAL, "in_features > 16 needs first hidden width <= 256");
+    if (d->dims[l] < 32 || d->dims[l] % 32 != 0 || d->dims[l] > hmax)
+      return fail(SIREN_EINVAL, "hidden width dims[%d]=%d must be a multiple of 32 in [32, %d]",
+                  l, d->dims[l], hmax);
   if (d->dims[0] > 4 && d->dims[1] > 512)
     return fail(SIREN_EINVAL, "in_features > 4 needs first hidden width <= 512");
+  if ((int64_t)d->batch * d->rows_per_batch * (d->dims[1] / 8) >= (int64_t)1 << 31)
+    return fail(SIREN_EINVAL, "too many rows for one call");
   for (int l = 0; l < L; ++l)
     if (!d->weight[l] || !d->bias[l]) return fail(SIREN_EINVAL, "layer %d: null weight/bias", l);
   for (int l = 1; l + 1 < L; ++l)
@@ -488,6 +548,47 @@ int siren_mlp_backward(const siren_mlp_desc* d, const float* x, const float* dy,
 }
 
 const char* siren_last_error(void) { return g_err.c_str(); }
+
+int siren_timing_enable(int kernel_class, int max_launches) {
+  siren_timing_disable();
+  if (kernel_class <= 0 || max_launches <= 0) return SIREN_OK;
+  g_timing.ev = new hipEvent_t[2 * (size_t)max_launches];
+  for (int i = 0; i < 2 * max_launches; ++i) {
+    if (hipEventCreate(&g_timing.ev[i]) != hipSuccess) {
+      for (int k = 0; k < i; ++k) (void)hipEventDestroy(g_timing.ev[k]);
+      delete[] g_timing.ev;
+      g_timing = Timing();
+      return fail(SIREN_ELAUNCH, "hipEventCreate failed");
+    }
+  }
+  g_timing.cls = kernel_class;
+  g_timing.cap = max_launches;
+  g_timing.used = 0;
+  return SIREN_OK;
+}
+
+int siren_timing_collect(double* total_ms, int64_t* launches) {
+  double tot = 0.0;
+  for (int i = 0; i < g_timing.used; ++i) {
+    if (hipEventSynchronize(g_timing.ev[2 * i + 1]) != hipSuccess)
+      return fail(SIREN_ELAUNCH, "hipEventSynchronize failed");
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, g_timing.ev[2 * i], g_timing.ev[2 * i + 1]) != hipSuccess)
+      return fail(SIREN_ELAUNCH, "hipEventElapsedTime failed");
+    tot += ms;
+  }
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = g_timing.used;
+  return SIREN_OK;
+}
+
+void siren_timing_disable(void) {
+  if (g_timing.ev) {
+    for (int i = 0; i < 2 * g_timing.cap; ++i) (void)hipEventDestroy(g_timing.ev[i]);
+    delete[] g_timing.ev;
+  }
+  g_timing = Timing();
+}
 
 const char* siren_version(void) {
   static char buf[128];

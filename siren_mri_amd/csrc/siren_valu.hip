@@ -1,0 +1,515 @@
+// siren_valu.hip — HBM-streaming kernels around the MFMA layers of the SIREN stack (gfx950).
+//
+// The first layer (in_features = 2 coords or 2m Fourier features) and the output layer
+// (out_features 1..8) are far too narrow for MFMA: they are rank-C / rank-O products streamed at
+// HBM speed. Mapping used throughout: a 32-lane half-wave owns one coordinate row and each lane
+// 8 consecutive features (one 16-byte access of a 2-byte phase/grad row), so every row is read
+// or written as 512 contiguous bytes; reductions over features are 5 half-wave shuffles.
+//
+//   first_fwd   P0 = enc(w0 (x W0^T + b0))                                  modules.py:25-26,38
+//   last_fwd    y  = sin(P) W_L^T + b_L   (optionally sin(w0 .))             modules.py:25-26,78
+//   last_bwd    dZ = (g W_L) cos(P) w0 ; partial dW_L = g^T sin(P), db_L = sum g
+//   first_bwd   partial dW0 = dZ^T x, db0 = sum dZ ; dx = dZ W0
+//   reduce      split-K slab reduction (float4 streams, 8 split lanes per column)
+//   prep_weight fp32 W -> op_t W and W^T (once per call)
+#include "siren_common.h"
+
+namespace siren {
+
+struct FirstFwdArgs {
+  const float* x;      // [rows, C]
+  const float* W;      // [nb_w][F, C]
+  const float* b;      // [nb_w][F]
+  void* P;             // [rows, F] phase_t
+  int64_t rows_per_batch;
+  int64_t w_bstride, b_bstride;
+  int C, F;
+  float w0;
+};
+
+struct LastFwdArgs {
+  const void* P;       // [rows, F] phase_t
+  const float* W;      // [nb_w][O, F]
+  const float* b;      // [nb_w][O]
+  float* y;            // [rows, O]
+  int64_t rows_per_batch;
+  int64_t w_bstride, b_bstride;
+  int F, O;
+  int sine_out;        // 1: y = sin(w0 * z) (outermost_linear == False)
+  float w0;
+};
+
+struct LastBwdArgs {
+  const void* P;       // [rows, F] phase_t
+  const float* W;      // [nb_w][O, F]
+  const float* b;      // [nb_w][O]
+  const float* dy;     // [rows, O]
+  void* dZ;            // [rows, F] grad_t
+  float* part;         // split s, batch b slab at part + s*split_stride + b*(O*F + O)
+  int64_t rows_per_batch;
+  int64_t rows_per_split;
+  int64_t split_stride;
+  int64_t w_bstride, b_bstride;
+  int F, O;
+  int sine_out;
+  float w0;
+};
+
+struct FirstBwdArgs {
+  const void* dZ;      // [rows, F] grad_t
+  const float* x;      // [rows, C]
+  const float* W;      // [nb_w][F, C]
+  float* dx;           // [rows, C] or null
+  float* part;         // split s, batch b slab at part + s*split_stride + b*(F*C + F)
+  int64_t rows_per_batch;
+  int64_t rows_per_split;
+  int64_t split_stride;
+  int64_t w_bstride;
+  int F, C;
+};
+
+// 8-element row chunk loads/stores (16 B for 2-byte types, 32 B for fp32).
+DEV void load8(const uint16_t* p, uint16_t (&v)[8]) {
+  const u16x8 t = *(const u16x8*)p;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = t[e];
+}
+DEV void load8(const float* p, float (&v)[8]) {
+  const f32x4 a = ((const f32x4*)p)[0], b = ((const f32x4*)p)[1];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] = a[e];
+    v[e + 4] = b[e];
+  }
+}
+DEV void load8f(const bf16* p, float (&v)[8]) {
+  const bf16x8 t = *(const bf16x8*)p;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = (float)t[e];
+}
+DEV void load8f(const float* p, float (&v)[8]) { load8(p, v); }
+
+DEV void store8(uint16_t* p, const uint16_t (&v)[8]) {
+  u16x8 t;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = v[e];
+  *(u16x8*)p = t;
+}
+DEV void store8(float* p, const float (&v)[8]) {
+  f32x4 a, b;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    a[e] = v[e];
+    b[e] = v[e + 4];
+  }
+  ((f32x4*)p)[0] = a;
+  ((f32x4*)p)[1] = b;
+}
+DEV void store8f(bf16* p, const float (&v)[8]) {
+  bf16x8 t;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = (bf16)v[e];
+  *(bf16x8*)p = t;
+}
+DEV void store8f(float* p, const float (&v)[8]) { store8(p, v); }
+
+// Sum over the 32 lanes of a half-wave (every lane gets the total).
+DEV float half_sum(float v) {
+#pragma unroll
+  for (int off = 16; off >= 1; off >>= 1) v += __shfl_xor(v, off, 32);
+  return v;
+}
+
+// ------------------------------------------------------------------------------------------
+// first_fwd: W0 is staged transposed in LDS ([C][F], then b0) so every thread reads its 8
+// features' weights with two 16-byte LDS reads per input channel; no dependent global loads.
+template <int PREC, int MAXC>
+__global__ __launch_bounds__(256) void first_fwd_kernel(FirstFwdArgs a) {
+  using PT = Prec<PREC>;
+  using phase_t = typename PT::phase_t;
+  __shared__ __attribute__((aligned(16))) float Ws[(MAXC + 1) * 512];
+  const int64_t batch = blockIdx.y;
+  const int F = a.F, C = a.C;
+  const float* W = a.W + batch * a.w_bstride;
+  const float* bias = a.b + batch * a.b_bstride;
+  for (int i = threadIdx.x; i < F * C; i += 256) {
+    const int f = i / C, c = i - f * C;
+    Ws[c * F + f] = W[i];
+  }
+  for (int f = threadIdx.x; f < F; f += 256) Ws[MAXC * F + f] = bias[f];
+  __syncthreads();
+  const uint32_t F8 = (uint32_t)(F >> 3);
+  const uint32_t total = (uint32_t)a.rows_per_batch * F8;
+  for (uint32_t idx = blockIdx.x * 256u + threadIdx.x; idx < total; idx += gridDim.x * 256u) {
+    const uint32_t r = idx / F8;
+    const int f = (int)(idx - r * F8) * 8;
+    const int64_t row = batch * a.rows_per_batch + r;
+    float xv[MAXC];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) xv[c] = (c < C) ? a.x[row * C + c] : 0.f;
+    float z[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) z[e] = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      if (c < C) {
+        const f32x4 w0v = *(const f32x4*)(Ws + c * F + f);
+        const f32x4 w1v = *(const f32x4*)(Ws + c * F + f + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          z[e] = fmaf(xv[c], w0v[e], z[e]);
+          z[e + 4] = fmaf(xv[c], w1v[e], z[e + 4]);
+        }
+      }
+    }
+    const f32x4 b0v = *(const f32x4*)(Ws + MAXC * F + f);
+    const f32x4 b1v = *(const f32x4*)(Ws + MAXC * F + f + 4);
+    phase_t out[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      out[e] = PT::enc(a.w0 * (z[e] + b0v[e]));
+      out[e + 4] = PT::enc(a.w0 * (z[e + 4] + b1v[e]));
+    }
+    store8((phase_t*)a.P + row * F + f, out);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+template <int PREC, int IT, int MAXO>
+__global__ __launch_bounds__(256) void last_fwd_kernel(LastFwdArgs a) {
+  using PT = Prec<PREC>;
+  using phase_t = typename PT::phase_t;
+  const int l32 = threadIdx.x & 31;
+  const int64_t batch = blockIdx.y;
+  const float* W = a.W + batch * a.w_bstride;
+  const float* bias = a.b + batch * a.b_bstride;
+  float w[IT][MAXO][8];
+#pragma unroll
+  for (int it = 0; it < IT; ++it)
+#pragma unroll
+    for (int o = 0; o < MAXO; ++o)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int f = 256 * it + 8 * l32 + e;
+        w[it][o][e] = (o < a.O && f < a.F) ? W[o * a.F + f] : 0.f;
+      }
+  for (int64_t r = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5); r < a.rows_per_batch;
+       r += (int64_t)gridDim.x * 8) {
+    const int64_t row = batch * a.rows_per_batch + r;
+    const phase_t* pr = (const phase_t*)a.P + row * a.F;
+    float acc[MAXO];
+#pragma unroll
+    for (int o = 0; o < MAXO; ++o) acc[o] = 0.f;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int f = 256 * it + 8 * l32;
+      if (f < a.F) {
+        phase_t pv[8];
+        load8(pr + f, pv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float h = PT::sinp(pv[e]);
+#pragma unroll
+          for (int o = 0; o < MAXO; ++o) acc[o] = fmaf(h, w[it][o][e], acc[o]);
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < MAXO; ++o) {
+      if (o < a.O) {
+        float z = half_sum(acc[o]) + bias[o];
+        if (a.sine_out) z = sinf(a.w0 * z);
+        if (l32 == o) a.y[row * a.O + o] = z;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+template <int PREC, int IT, int MAXO>
+__global__ __launch_bounds__(256) void last_bwd_kernel(LastBwdArgs a) {
+  using PT = Prec<PREC>;
+  using phase_t = typename PT::phase_t;
+  using grad_t = typename PT::grad_t;
+  __shared__ float red[8][MAXO * 256 + MAXO];
+  const int l32 = threadIdx.x & 31;
+  const int grp = threadIdx.x >> 5;  // 8 row groups (half-waves) per block
+  const int split = blockIdx.x;
+  const int64_t batch = blockIdx.y;
+  const float* W = a.W + batch * a.w_bstride;
+  const float* bias = a.b + batch * a.b_bstride;
+  const int64_t r_begin = (int64_t)split * a.rows_per_split;
+  int64_t r_end = r_begin + a.rows_per_split;
+  if (r_end > a.rows_per_batch) r_end = a.rows_per_batch;
+  float w[IT][MAXO][8];
+  float dw[IT][MAXO][8];
+  float db[MAXO];
+#pragma unroll
+  for (int it = 0; it < IT; ++it)
+#pragma unroll
+    for (int o = 0; o < MAXO; ++o)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int f = 256 * it + 8 * l32 + e;
+        w[it][o][e] = (o < a.O && f < a.F) ? W[o * a.F + f] : 0.f;
+        dw[it][o][e] = 0.f;
+      }
+#pragma unroll
+  for (int o = 0; o < MAXO; ++o) db[o] = 0.f;
+
+  for (int64_t r = r_begin + grp; r < r_end; r += 8) {
+    const int64_t row = batch * a.rows_per_batch + r;
+    const phase_t* pr = (const phase_t*)a.P + row * a.F;
+    float g[MAXO];
+#pragma unroll
+    for (int o = 0; o < MAXO; ++o) g[o] = (o < a.O) ? a.dy[row * a.O + o] : 0.f;
+    phase_t pv[IT][8];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int f = 256 * it + 8 * l32;
+      if (f < a.F) load8(pr + f, pv[it]);
+    }
+    if (a.sine_out) {
+      float acc[MAXO];
+#pragma unroll
+      for (int o = 0; o < MAXO; ++o) acc[o] = 0.f;
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+        if (256 * it + 8 * l32 < a.F)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float h = PT::sinp(pv[it][e]);
+#pragma unroll
+            for (int o = 0; o < MAXO; ++o) acc[o] = fmaf(h, w[it][o][e], acc[o]);
+          }
+#pragma unroll
+      for (int o = 0; o < MAXO; ++o)
+        if (o < a.O) g[o] = (g[o] * cosf(a.w0 * (half_sum(acc[o]) + bias[o]))) * a.w0;
+    }
+#pragma unroll
+    for (int o = 0; o < MAXO; ++o) db[o] += g[o];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int f = 256 * it + 8 * l32;
+      if (f < a.F) {
+        float dz[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float s = PT::sinp(pv[it][e]), c = PT::cosp(pv[it][e]);
+          float dh = 0.f;
+#pragma unroll
+          for (int o = 0; o < MAXO; ++o) {
+            dh = fmaf(g[o], w[it][o][e], dh);
+            dw[it][o][e] = fmaf(g[o], s, dw[it][o][e]);
+          }
+          dz[e] = (dh * c) * a.w0;
+        }
+        store8f((grad_t*)a.dZ + row * a.F + f, dz);
+      }
+    }
+  }
+  // Reduce the 8 row groups through LDS, 256 features at a time; one slab write per block.
+  float* part = a.part + (int64_t)split * a.split_stride + batch * (int64_t)(a.O * a.F + a.O);
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+#pragma unroll
+    for (int o = 0; o < MAXO; ++o)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[grp][o * 256 + 8 * l32 + e] = dw[it][o][e];
+    if (it == 0 && l32 == 0) {
+#pragma unroll
+      for (int o = 0; o < MAXO; ++o) red[grp][MAXO * 256 + o] = db[o];
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < a.O * 256; idx += 256) {
+      const int o = idx >> 8, f = 256 * it + (idx & 255);
+      if (f < a.F) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += red[k][idx];
+        part[o * a.F + f] = s;
+      }
+    }
+    if (it == 0 && (int)threadIdx.x < a.O) {
+      const int k0 = MAXO * 256 + threadIdx.x;
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += red[k][k0];
+      part[a.O * a.F + threadIdx.x] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// first_bwd: LPR lanes per row, FPL features per lane (C <= 4: 32 x 8; else 64 x 4).
+template <int PREC, int IT, int MAXC>
+__global__ __launch_bounds__(256) void first_bwd_kernel(FirstBwdArgs a) {
+  using PT = Prec<PREC>;
+  using grad_t = typename PT::grad_t;
+  constexpr int FPL = (MAXC <= 4) ? 8 : 4;
+  constexpr int LPR = 256 / FPL;
+  constexpr int GROUPS = 256 / LPR;
+  __shared__ float red[GROUPS][256 * (MAXC + 1)];
+  const int li = threadIdx.x % LPR;
+  const int grp = threadIdx.x / LPR;
+  const int split = blockIdx.x;
+  const int64_t batch = blockIdx.y;
+  const float* W = a.W + batch * a.w_bstride;
+  const int64_t r_begin = (int64_t)split * a.rows_per_split;
+  int64_t r_end = r_begin + a.rows_per_split;
+  if (r_end > a.rows_per_batch) r_end = a.rows_per_batch;
+  float wv[IT][FPL][MAXC];
+  float dw[IT][FPL][MAXC];
+  float db[IT][FPL];
+#pragma unroll
+  for (int it = 0; it < IT; ++it)
+#pragma unroll
+    for (int e = 0; e < FPL; ++e) {
+      const int f = 256 * it + FPL * li + e;
+      db[it][e] = 0.f;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) {
+        wv[it][e][c] = (f < a.F && c < a.C) ? W[f * a.C + c] : 0.f;
+        dw[it][e][c] = 0.f;
+      }
+    }
+  for (int64_t r = r_begin + grp; r < r_end; r += GROUPS) {
+    const int64_t row = batch * a.rows_per_batch + r;
+    float xv[MAXC];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) xv[c] = (c < a.C) ? a.x[row * a.C + c] : 0.f;
+    float dxp[MAXC];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) dxp[c] = 0.f;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int f = 256 * it + FPL * li;
+      if (f < a.F) {
+        float dz[8];
+        if constexpr (FPL == 8) {
+          load8f((const grad_t*)a.dZ + row * a.F + f, dz);
+        } else {
+          const grad_t* src = (const grad_t*)a.dZ + row * a.F + f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dz[e] = to_f32(src[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < FPL; ++e) {
+          db[it][e] += dz[e];
+#pragma unroll
+          for (int c = 0; c < MAXC; ++c) {
+            dw[it][e][c] = fmaf(dz[e], xv[c], dw[it][e][c]);
+            dxp[c] = fmaf(dz[e], wv[it][e][c], dxp[c]);
+          }
+        }
+      }
+    }
+    if (a.dx) {
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) {
+        if (c < a.C) {
+          float s = dxp[c];
+#pragma unroll
+          for (int off = LPR / 2; off >= 1; off >>= 1) s += __shfl_xor(s, off, LPR);
+          if (li == 0) a.dx[row * a.C + c] = s;
+        }
+      }
+    }
+  }
+  float* part = a.part + (int64_t)split * a.split_stride + batch * (int64_t)(a.F * a.C + a.F);
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+#pragma unroll
+    for (int e = 0; e < FPL; ++e) {
+      const int fl = FPL * li + e;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) red[grp][fl * (MAXC + 1) + c] = dw[it][e][c];
+      red[grp][fl * (MAXC + 1) + MAXC] = db[it][e];
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < 256 * (MAXC + 1); idx += 256) {
+      const int fl = idx / (MAXC + 1), c = idx % (MAXC + 1);
+      const int f = 256 * it + fl;
+      if (f >= a.F || (c >= a.C && c != MAXC)) continue;
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < GROUPS; ++k) s += red[k][idx];
+      if (c < a.C) part[f * a.C + c] = s;
+      else part[a.F * a.C + f] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// reduce: out[e] = sum_s part[s * split_stride + e] for e < total (= nb * slab). Element e of
+// batch slab b goes to out0[b*n_first + r] (r < n_first) or out1[b*(slab-n_first) + r-n_first].
+// Block = 32 float4 columns x 8 split lanes; split_stride % 4 == 0.
+__global__ __launch_bounds__(256) void reduce_kernel(const float* part, int nsplit, int64_t split_stride,
+                                                     int total, int slab, int n_first, float* out0,
+                                                     float* out1) {
+  __shared__ f32x4 red[8][32];
+  const int c4 = threadIdx.x & 31, sl = threadIdx.x >> 5;
+  const int base = (blockIdx.x * 32 + c4) * 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (base < total) {
+    int s = sl;
+    for (; s + 24 < nsplit; s += 32) {
+      const f32x4 v0 = *(const f32x4*)(part + (int64_t)s * split_stride + base);
+      const f32x4 v1 = *(const f32x4*)(part + (int64_t)(s + 8) * split_stride + base);
+      const f32x4 v2 = *(const f32x4*)(part + (int64_t)(s + 16) * split_stride + base);
+      const f32x4 v3 = *(const f32x4*)(part + (int64_t)(s + 24) * split_stride + base);
+      acc += (v0 + v1) + (v2 + v3);
+    }
+    for (; s < nsplit; s += 8) acc += *(const f32x4*)(part + (int64_t)s * split_stride + base);
+  }
+  red[sl][c4] = acc;
+  __syncthreads();
+  if (sl == 0 && base < total) {
+    f32x4 t = red[0][c4];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) t += red[k][c4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = base + e;
+      if (idx >= total) break;
+      const int b = idx / slab, r = idx - b * slab;
+      if (r < n_first) out0[(int64_t)b * n_first + r] = t[e];
+      else out1[(int64_t)b * (slab - n_first) + (r - n_first)] = t[e];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Weight preparation for every MFMA layer in one launch (blockIdx.y = layer):
+// W [nb][O][I] fp32 -> Wop [nb][O][I] op_t (bf16 only) and WtOp [nb][I][O] op_t.
+struct PrepArgs {
+  const float* W[16];
+  void* Wop[16];
+  void* Wt[16];
+  int O[16], I[16];
+  int64_t nb;
+};
+
+template <int PREC>
+__global__ __launch_bounds__(256) void prep_weights_kernel(PrepArgs a) {
+  using op_t = typename Prec<PREC>::op_t;
+  const int l = blockIdx.y;
+  const int O = a.O[l], I = a.I[l];
+  const float* W = a.W[l];
+  op_t* Wop = (op_t*)a.Wop[l];
+  op_t* Wt = (op_t*)a.Wt[l];
+  const int64_t per = (int64_t)O * I;
+  const int64_t total = a.nb * per;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+    const int64_t b = idx / per;
+    const int rem = (int)(idx - b * per);
+    const int o = rem / I, i = rem - o * I;
+    const op_t v = from_f32<op_t>(W[idx]);
+    if (Wop) Wop[idx] = v;
+    Wt[b * per + (int64_t)i * O + o] = v;
+  }
+}
+
+}  // namespace siren

@@ -1,0 +1,78 @@
+"""Losses on the SIREN hot path (drop-in for loss_functions.py of jonbmartin/siren_mri).
+
+  image_mse                loss_functions.py:66-101
+  latent_loss              loss_functions.py:275-276
+  hypo_weight_loss         loss_functions.py:279-287
+  image_hypernetwork_loss  loss_functions.py:290-293
+  function_mse             loss_functions.py:326-327
+  gradients_mse            loss_functions.py:330-335
+  laplace_mse              loss_functions.py:350-355
+
+Deliberate deviation (bug 0.2): the reference builds its high-frequency mask
+on a fixed 128x128 grid, so image_mse(high_freq=True) raises for any other image size; here the
+mask applies when the image is 128x128 and the loss is the plain SSE otherwise.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import diff_operators
+from .dataio import lin2img
+from .utils import create_circular_mask_torch
+
+_KSPACE_WEIGHT = 1.0 / (128 * 128)
+_MASKS: dict = {}
+
+
+def _high_freq_mask(device):
+    m = _MASKS.get(device)
+    if m is None:
+        m = 1 - create_circular_mask_torch(129, 129, center=None, radius=20)
+        m = m.to(device)
+        _MASKS[device] = m
+    return m
+
+
+def image_mse(mask, model_output, gt, high_freq=True):
+    """Weighted k-space SSE: sum |m * (pred - gt)|^2 / 128^2 (a sum over the batch)."""
+    pred = lin2img(model_output["model_out"])
+    tgt = lin2img(gt["img"])
+    diff = pred - tgt
+    if high_freq and pred.shape[-2:] == (128, 128):
+        diff = _high_freq_mask(pred.device) * diff
+    loss = (diff.abs() ** 2).sum() * _KSPACE_WEIGHT
+    return {"img_loss": loss}
+
+
+def latent_loss(model_output):
+    return torch.mean(model_output["latent_vec"] ** 2)
+
+
+def hypo_weight_loss(model_output):
+    weight_sum = 0
+    total = 0
+    for w in model_output["hypo_params"].values():
+        weight_sum = weight_sum + torch.sum(w ** 2)
+        total += w.numel()
+    return weight_sum * (1 / total)
+
+
+def image_hypernetwork_loss(mask, kl, fw, model_output, gt):
+    return {"img_loss": image_mse(mask, model_output, gt)["img_loss"],
+            "latent_loss": kl * latent_loss(model_output),
+            "hypo_weight_loss": fw * hypo_weight_loss(model_output)}
+
+
+def function_mse(model_output, gt):
+    return {"func_loss": ((model_output["model_out"] - gt["func"]) ** 2).mean()}
+
+
+def gradients_mse(model_output, gt):
+    """mean_n sum_k (dy/dx_k - gt_k)^2 with the analytic SIREN gradient (config 3)."""
+    g = diff_operators.gradient(model_output["model_out"], model_output["model_in"])
+    return {"gradients_loss": torch.mean((g - gt["gradients"]).pow(2).sum(-1))}
+
+
+def laplace_mse(model_output, gt):
+    lap = diff_operators.laplace(model_output["model_out"], model_output["model_in"])
+    return {"laplace_loss": torch.mean((lap - gt["laplace"]) ** 2)}

@@ -93,7 +93,7 @@ def _flat_params(weights, biases, geo: _Geometry):
 class _SirenMLPFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cfg, x, *params):
-        w0, prec, outermost_linear, n_layers = cfg
+        w0, prec, outermost_linear, n_layers, grad_on = cfg
         weights = list(params[:n_layers])
         biases = list(params[n_layers:])
         _require_device(x)
@@ -106,7 +106,7 @@ class _SirenMLPFunction(torch.autograd.Function):
                                  batch=geo.batch, rows_per_batch=geo.rows)
         L = _native.lib()
         _native.check(L.siren_mlp_check(ctypes.byref(desc)), "siren_mlp_check")
-        need_saved = any(ctx.needs_input_grad)
+        need_saved = grad_on and any(ctx.needs_input_grad)
         saved_bytes = L.siren_mlp_saved_bytes(ctypes.byref(desc)) if need_saved else 0
         ws_bytes = L.siren_mlp_workspace_bytes(ctypes.byref(desc))
         saved = torch.empty(max(saved_bytes, 1), dtype=torch.uint8, device=dev) if need_saved else None
@@ -126,7 +126,7 @@ class _SirenMLPFunction(torch.autograd.Function):
     @staticmethod
     @once_differentiable
     def backward(ctx, dy):
-        w0, prec, outermost_linear, n_layers = ctx.cfg
+        w0, prec, outermost_linear, n_layers, _ = ctx.cfg
         geo = ctx.geo
         tensors = ctx.saved_tensors
         xc = tensors[0]
@@ -168,5 +168,5 @@ def siren_mlp(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence
     n = len(weights)
     if len(biases) != n:
         raise ValueError("siren_mlp: weights and biases differ in length")
-    cfg = (float(w0), prec, bool(outermost_linear), n)
+    cfg = (float(w0), prec, bool(outermost_linear), n, torch.is_grad_enabled())
     return _SirenMLPFunction.apply(cfg, x, *weights, *biases)

@@ -1,0 +1,166 @@
+"""Generic fitting loop (drop-in for training.py:19-146 of jonbmartin/siren_mri).
+
+Same signature and step semantics: optional Fourier-feature transform of the coordinates
+(:61-64), forward, loss dict summed from per-term `.mean()`s with optional schedules (:67-78),
+loss / accumulation_steps, backward, optional clip_grad_norm_ every micro-step (:93-97), Adam
+step + zero_grad every `accumulation_steps` micro-steps or at the last batch (:101-103),
+checkpoints (`model_epoch_%04d.pth`, `model_current.pth`, `model_final.pth`) and loss text files
+with the reference's names.
+
+Deliberate deviations:
+  * batches are moved to the model's device (bug 0.1, training.py:53-66);
+  * the function returns the mean validation loss, or the last training loss when there is no
+    validation loader (bug 0.3, training.py:145);
+  * the per-step loss is kept on the device and read back only at summary steps and at the end
+    (the reference calls .item() every step, a host sync per step);
+  * an existing model_dir is overwritten without an interactive prompt when stdin is not a TTY.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import sys
+import time
+
+import numpy as np
+import torch
+
+from . import utils
+
+
+class _NullWriter:
+    def __getattr__(self, name):
+        return lambda *a, **k: None
+
+
+def make_writer(path):
+    try:
+        from torch.utils.tensorboard import SummaryWriter
+        return SummaryWriter(path)
+    except Exception:  # tensorboard is optional
+        return _NullWriter()
+
+
+def to_device(d, device):
+    return {k: (v.to(device, non_blocking=True) if torch.is_tensor(v) else v) for k, v in d.items()}
+
+
+def model_device(model):
+    for p in model.parameters():
+        return p.device
+    return torch.device("cpu")
+
+
+def prepare_model_dir(model_dir, hyperopt_run=False):
+    if os.path.exists(model_dir):
+        if hyperopt_run or not sys.stdin.isatty():
+            val = "y"
+        else:
+            val = input("The model directory %s exists. Overwrite? (y/n)" % model_dir)
+        if val == "y":
+            shutil.rmtree(model_dir)
+    os.makedirs(model_dir, exist_ok=True)
+    summaries_dir = os.path.join(model_dir, "summaries")
+    checkpoints_dir = os.path.join(model_dir, "checkpoints")
+    utils.cond_mkdir(summaries_dir)
+    utils.cond_mkdir(checkpoints_dir)
+    return summaries_dir, checkpoints_dir
+
+
+def compute_loss(losses, loss_schedules, total_steps, writer):
+    train_loss = 0.0
+    for name, loss in losses.items():
+        single = loss.mean()
+        if loss_schedules is not None and name in loss_schedules:
+            w = loss_schedules[name](total_steps)
+            writer.add_scalar(name + "_weight", w, total_steps)
+            single = single * w
+        train_loss = train_loss + single
+    return train_loss
+
+
+def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_checkpoint, model_dir, loss_fn,
+          summary_fn, val_dataloader=None, double_precision=False, clip_grad=False, use_lbfgs=False,
+          loss_schedules=None, fourier_feat_transformer=None, device=None, hyperopt_run=False,
+          accumulation_steps=1, grad_reducer=None):
+    """Fit `model` (training.py:19-146). `grad_reducer`, if given, is called after each backward
+    (before clipping) — the data-parallel gradient exchange of training_ddp."""
+    optim = torch.optim.Adam(lr=lr, params=model.parameters())
+    dev = model_device(model) if device is None else torch.device(device)
+    summaries_dir, checkpoints_dir = prepare_model_dir(model_dir, hyperopt_run)
+    writer = make_writer(summaries_dir)
+
+    total_steps = 0
+    train_losses_dev = []
+    mean_val_loss = None
+    last_loss = None
+    n_batches = len(train_dataloader)
+    for epoch in range(epochs):
+        if not epoch % epochs_til_checkpoint and epoch:
+            torch.save(model.state_dict(), os.path.join(checkpoints_dir, "model_epoch_%04d.pth" % epoch))
+            np.savetxt(os.path.join(checkpoints_dir, "train_losses_epoch_%04d.txt" % epoch),
+                       np.array([float(t) for t in torch.stack(train_losses_dev).cpu()]) if train_losses_dev else np.array([]))
+        for step, (model_input, gt) in enumerate(train_dataloader):
+            start_time = time.time()
+            model_input = to_device(model_input, dev)
+            gt = to_device(gt, dev)
+            if double_precision:
+                model_input = {k: v.double() for k, v in model_input.items()}
+                gt = {k: v.double() for k, v in gt.items()}
+            if fourier_feat_transformer is not None:
+                model_input["coords"] = fourier_feat_transformer(model_input["coords"])
+
+            model_output = model(model_input)
+            losses = loss_fn(model_output, gt)
+            train_loss = compute_loss(losses, loss_schedules, total_steps, writer)
+            train_losses_dev.append(train_loss.detach().reshape(()))
+            summary_step = not total_steps % steps_til_summary
+            if summary_step:
+                writer.add_scalar("total_train_loss", float(train_loss), total_steps)
+                torch.save(model.state_dict(), os.path.join(checkpoints_dir, "model_current.pth"))
+                summary_fn(model, model_input, gt, model_output, writer, total_steps)
+            del model_output, losses
+
+            train_loss = train_loss / accumulation_steps
+            train_loss.backward()
+            if grad_reducer is not None:
+                grad_reducer()
+            if clip_grad:
+                max_norm = 1.0 if isinstance(clip_grad, bool) else clip_grad
+                torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
+            if (step + 1) % accumulation_steps == 0 or (step + 1 == n_batches):
+                optim.step()
+                optim.zero_grad()
+
+            if summary_step:
+                print("Epoch %d, Total loss %0.6f, iteration time %0.6f"
+                      % (epoch, float(train_loss), time.time() - start_time))
+                if val_dataloader is not None:
+                    mean_val_loss = validate(model, val_dataloader, loss_fn, fourier_feat_transformer, dev)
+                    writer.add_scalar("val_loss", mean_val_loss, total_steps)
+                    print(f"val loss (img_loss_only): {mean_val_loss}")
+            last_loss = train_loss
+            total_steps += 1
+
+    torch.save(model.state_dict(), os.path.join(checkpoints_dir, "model_final.pth"))
+    losses_host = torch.stack(train_losses_dev).cpu().numpy() if train_losses_dev else np.array([])
+    np.savetxt(os.path.join(checkpoints_dir, "train_losses_final.txt"), losses_host)
+    if mean_val_loss is not None:
+        return mean_val_loss
+    return None if last_loss is None else float(last_loss) * accumulation_steps
+
+
+@torch.no_grad()
+def validate(model, val_dataloader, loss_fn, fourier_feat_transformer, dev):
+    """training.py:111-136: mean of the 'img_loss' term over the validation loader."""
+    model.eval()
+    vals = []
+    for model_input, gt in val_dataloader:
+        model_input = to_device(model_input, dev)
+        gt = to_device(gt, dev)
+        if fourier_feat_transformer is not None:
+            model_input["coords"] = fourier_feat_transformer(model_input["coords"])
+        out = model(model_input)
+        vals.append(loss_fn(out, gt)["img_loss"])
+    model.train()
+    return float(torch.mean(torch.stack(vals)))

@@ -254,7 +254,7 @@ def main():
         k = np.fft.fftshift(np.fft.fft2(sl))
         k = k / np.abs(k).max()
         ks.append(np.stack([k.real, k.imag]).astype(np.float32) * 2.0)
-    kspace = torch.from_numpy(np.stack(ks))  # [2,2,128,128]
+    kspace = torch.from_numpy(np.ascontiguousarray(np.stack(ks))).contiguous()  # [2,2,128,128]
     rs = np.random.RandomState(5)
     mask = torch.zeros_like(kspace)
     for b in range(2):

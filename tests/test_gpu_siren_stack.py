@@ -93,6 +93,24 @@ def test_sine_output_layer(precision):
     _check(x, params, precision, outermost_linear=False)
 
 
+def test_wide_hidden_bf16():
+    # 512-wide hidden layers use the K=512 bf16 kernel variant (32-row tiles)
+    dims = orc.siren_dims(2, 512, 1, 1)
+    params = orc.siren_init(dims, seed=9)
+    x = orc.get_mgrid(23).unsqueeze(0)
+    _check(x, params, "bf16")
+
+
+def test_wide_hidden_fp32_rejected():
+    from siren_mri_amd.ops import siren_mlp
+    from siren_mri_amd._native import NativeError
+    dims = orc.siren_dims(2, 512, 1, 1)
+    params = orc.siren_init(dims, seed=9)
+    with pytest.raises(NativeError, match="hidden width"):
+        siren_mlp(torch.zeros(1, 4, 2, device=DEV), [W.to(DEV) for W, _ in params],
+                  [b.to(DEV) for _, b in params], precision="fp32")
+
+
 def test_metric_size_fp32_forward():
     # the metric configuration (512^2, 5x256) forward in fp32 against the fp64 oracle
     from siren_mri_amd.ops import siren_mlp
