@@ -82,13 +82,21 @@ def compute_loss(losses, loss_schedules, total_steps, writer):
 def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_checkpoint, model_dir, loss_fn,
           summary_fn, val_dataloader=None, double_precision=False, clip_grad=False, use_lbfgs=False,
           loss_schedules=None, fourier_feat_transformer=None, device=None, hyperopt_run=False,
-          accumulation_steps=1, grad_reducer=None):
+          accumulation_steps=1, grad_reducer=None, write_outputs=True):
     """Fit `model` (training.py:19-146). `grad_reducer`, if given, is called after each backward
-    (before clipping) — the data-parallel gradient exchange of training_ddp."""
+    (before clipping) — the data-parallel gradient exchange of training_ddp. With
+    write_outputs=False (non-zero data-parallel ranks) nothing is written to disk."""
     optim = torch.optim.Adam(lr=lr, params=model.parameters())
     dev = model_device(model) if device is None else torch.device(device)
-    summaries_dir, checkpoints_dir = prepare_model_dir(model_dir, hyperopt_run)
-    writer = make_writer(summaries_dir)
+    if write_outputs:
+        summaries_dir, checkpoints_dir = prepare_model_dir(model_dir, hyperopt_run)
+        writer = make_writer(summaries_dir)
+    else:
+        checkpoints_dir, writer = None, _NullWriter()
+
+    def save(obj_fn, name):
+        if checkpoints_dir is not None:
+            obj_fn(os.path.join(checkpoints_dir, name))
 
     total_steps = 0
     train_losses_dev = []
@@ -97,9 +105,9 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
     n_batches = len(train_dataloader)
     for epoch in range(epochs):
         if not epoch % epochs_til_checkpoint and epoch:
-            torch.save(model.state_dict(), os.path.join(checkpoints_dir, "model_epoch_%04d.pth" % epoch))
-            np.savetxt(os.path.join(checkpoints_dir, "train_losses_epoch_%04d.txt" % epoch),
-                       np.array([float(t) for t in torch.stack(train_losses_dev).cpu()]) if train_losses_dev else np.array([]))
+            save(lambda p: torch.save(model.state_dict(), p), "model_epoch_%04d.pth" % epoch)
+            hist = torch.stack(train_losses_dev).cpu().numpy() if train_losses_dev else np.array([])
+            save(lambda p: np.savetxt(p, hist), "train_losses_epoch_%04d.txt" % epoch)
         for step, (model_input, gt) in enumerate(train_dataloader):
             start_time = time.time()
             model_input = to_device(model_input, dev)
@@ -116,8 +124,8 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
             train_losses_dev.append(train_loss.detach().reshape(()))
             summary_step = not total_steps % steps_til_summary
             if summary_step:
-                writer.add_scalar("total_train_loss", float(train_loss), total_steps)
-                torch.save(model.state_dict(), os.path.join(checkpoints_dir, "model_current.pth"))
+                writer.add_scalar("total_train_loss", float(train_loss.detach()), total_steps)
+                save(lambda p: torch.save(model.state_dict(), p), "model_current.pth")
                 summary_fn(model, model_input, gt, model_output, writer, total_steps)
             del model_output, losses
 
@@ -134,7 +142,7 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
 
             if summary_step:
                 print("Epoch %d, Total loss %0.6f, iteration time %0.6f"
-                      % (epoch, float(train_loss), time.time() - start_time))
+                      % (epoch, float(train_loss.detach()), time.time() - start_time))
                 if val_dataloader is not None:
                     mean_val_loss = validate(model, val_dataloader, loss_fn, fourier_feat_transformer, dev)
                     writer.add_scalar("val_loss", mean_val_loss, total_steps)
@@ -142,12 +150,12 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
             last_loss = train_loss
             total_steps += 1
 
-    torch.save(model.state_dict(), os.path.join(checkpoints_dir, "model_final.pth"))
+    save(lambda p: torch.save(model.state_dict(), p), "model_final.pth")
     losses_host = torch.stack(train_losses_dev).cpu().numpy() if train_losses_dev else np.array([])
-    np.savetxt(os.path.join(checkpoints_dir, "train_losses_final.txt"), losses_host)
+    save(lambda p: np.savetxt(p, losses_host), "train_losses_final.txt")
     if mean_val_loss is not None:
         return mean_val_loss
-    return None if last_loss is None else float(last_loss) * accumulation_steps
+    return None if last_loss is None else float(last_loss.detach()) * accumulation_steps
 
 
 @torch.no_grad()

@@ -128,12 +128,12 @@ def train_ddp(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til
             self.epoch += 1
             return iter(self.dl)
 
-    rank_dir = model_dir if rank == 0 else os.path.join(model_dir, f"_rank{rank}")
     out = training.train(model, _EpochLoader(train_dataloader), epochs, lr, steps_til_summary,
-                         epochs_til_checkpoint, rank_dir, loss_fn,
+                         epochs_til_checkpoint, model_dir, loss_fn,
                          summary_fn if rank == 0 else (lambda *a, **k: None),
                          val_dataloader=val_dataloader if rank == 0 else None,
                          double_precision=double_precision, clip_grad=clip_grad, loss_schedules=loss_schedules,
                          fourier_feat_transformer=fourier_feat_transformer, hyperopt_run=True,
-                         accumulation_steps=accumulation_steps, grad_reducer=reducer)
+                         accumulation_steps=accumulation_steps, grad_reducer=reducer,
+                         write_outputs=(rank == 0))
     return out

@@ -98,7 +98,7 @@ def camera_tensor(side):
 
 
 def state_arrays(model, prefix=""):
-    return {prefix + k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+    return {prefix + k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
 
 
 def quiet(fn, *a, **k):

@@ -1,0 +1,170 @@
+"""Host-side API of siren_mri_amd against the reference's contract (CPU, no kernels):
+parameter names and init RNG order, param routing, losses, data layouts, the training loop
+(driven with the CPU oracle model) and the hypernetwork architecture/state_dict compatibility."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import siren_oracle as orc
+from siren_mri_amd import (data_consistency, dataio, diff_operators, features, loss_functions, meta,
+                           meta_modules, modules, training, utils)
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(G, name), allow_pickle=False)
+
+
+@pytest.mark.parametrize("seed,hid,nh", [(0, 64, 1), (1, 64, 1), (0, 256, 3)])
+def test_singlebvpnet_state_dict_matches_reference_init(seed, hid, nh):
+    d = load("init.npz")
+    torch.manual_seed(seed)
+    m = modules.SingleBVPNet(type="sine", hidden_features=hid, num_hidden_layers=nh, sidelength=(8, 8))
+    sd = m.state_dict()
+    prefix = f"s{seed}_h{hid}_n{nh}/"
+    ref_keys = sorted(k[len(prefix):] for k in d.files if k.startswith(prefix))
+    assert sorted(sd.keys()) == ref_keys
+    for k in ref_keys:
+        assert np.array_equal(sd[k].numpy(), d[prefix + k]), k
+
+
+def test_meta_named_parameters_order_and_subdict():
+    m = modules.SingleBVPNet(type="sine", hidden_features=32, num_hidden_layers=1)
+    names = [n for n, _ in m.meta_named_parameters()]
+    assert names == [f"net.net.{i}.0.{w}" for i in range(3) for w in ("weight", "bias")]
+    sub = meta.get_subdict(dict(m.named_parameters()), "net")
+    assert list(sub.keys())[0] == "net.0.0.weight"
+    assert meta.get_subdict(None, "net") is None
+
+
+def test_sine_forward_on_cpu_raises_no_fallback():
+    m = modules.SingleBVPNet(type="sine", hidden_features=32, num_hidden_layers=1)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m({"coords": dataio.get_mgrid(4)[None]})
+
+
+def test_relu_fcblock_runs_in_torch():
+    """Non-sine FCBlocks (the HyperNetwork's) are plain PyTorch and batch-broadcast like BatchLinear."""
+    torch.manual_seed(0)
+    blk = modules.FCBlock(8, 5, 1, 16, outermost_linear=True, nonlinearity="relu")
+    z = torch.randn(3, 8)
+    out = blk(z)
+    assert out.shape == (3, 5)
+    ref = z
+    for i, layer in enumerate(blk.net):
+        lin = layer[0]
+        ref = ref @ lin.weight.T + lin.bias
+        if i < len(blk.net) - 1:
+            ref = torch.relu(ref)
+    assert torch.allclose(out, ref, atol=1e-6)
+
+
+def test_losses_match_reference_values():
+    d = load("losses.npz")
+    pred, tgt = torch.from_numpy(d["pred"]), torch.from_numpy(d["tgt"])
+    assert loss_functions.image_mse(None, {"model_out": pred}, {"img": tgt})["img_loss"].item() == \
+        pytest.approx(float(d["image_mse_hf"]), rel=1e-6)
+    assert loss_functions.image_mse(None, {"model_out": pred}, {"img": tgt}, high_freq=False)["img_loss"].item() == \
+        pytest.approx(float(d["image_mse_plain"]), rel=1e-6)
+    out = {"model_out": pred, "latent_vec": torch.from_numpy(d["latent"]),
+           "hypo_params": {"a": torch.from_numpy(d["hp_a"]), "b": torch.from_numpy(d["hp_b"])}}
+    hl = loss_functions.image_hypernetwork_loss(None, 2.78e-8, 6.4e-6, out, {"img": tgt})
+    assert hl["latent_loss"].item() == pytest.approx(float(d["hyper_latent"]), rel=1e-6)
+    assert hl["hypo_weight_loss"].item() == pytest.approx(float(d["hyper_weight"]), rel=1e-6)
+    assert np.array_equal(utils.create_circular_mask_torch(129, 129, radius=20).numpy(), d["circ_mask"])
+
+
+def test_image_mse_off_128_is_plain_sse():
+    """bug 0.2 deviation: high_freq is ignored off the 128x128 grid (the reference raises)."""
+    a, b = torch.randn(1, 64 * 64, 1), torch.randn(1, 64 * 64, 1)
+    hf = loss_functions.image_mse(None, {"model_out": a}, {"img": b})["img_loss"]
+    plain = ((a - b) ** 2).sum() / (128 * 128)
+    assert torch.allclose(hf, plain)
+
+
+def test_dataio_layouts():
+    d = load("mgrid.npz")
+    assert np.array_equal(dataio.get_mgrid(5).numpy(), d["mgrid5"])
+    assert np.array_equal(dataio.get_mgrid((4, 6)).numpy(), d["mgrid4x6"])
+    assert np.array_equal(dataio.lin2img(torch.from_numpy(d["lin2img_in"])).numpy(), d["lin2img_out"])
+
+
+def test_camera_transform_matches_fixture():
+    d = load("train_c1.npz")
+    ds = dataio.Implicit2DWrapper(dataio.Camera(), sidelength=64)
+    inp, gt = ds[0]
+    assert inp["coords"].shape == (4096, 2)
+    assert np.array_equal(gt["img"].numpy(), d["img"][0])
+
+
+def test_gradient_ground_truth_matches_fixture():
+    d = load("train_c3.npz")
+    ds = dataio.Implicit2DWrapper(dataio.Camera(), sidelength=32, compute_diff="gradients")
+    _, gt = ds[0]
+    assert np.allclose(gt["gradients"].numpy(), d["gradients"][0], atol=1e-5)
+
+
+def test_features_and_dc_match_reference():
+    d = load("features.npz")
+    ff = features.GaussianFourierFeatureTransform(2, 8, 21, loaded_B=torch.from_numpy(d["B"]))
+    assert torch.allclose(ff(torch.from_numpy(d["x"])), torch.from_numpy(d["ff"]), atol=1e-6)
+    dc = data_consistency.DataConsistencyInKspace()(torch.from_numpy(d["pred"]), torch.from_numpy(d["k0"]),
+                                                     torch.from_numpy(d["mask"]))
+    assert np.array_equal(dc.numpy(), d["dc"])
+
+
+def test_psnr_formula():
+    p = np.array([[0.5, -1.2], [0.1, 0.9]])
+    t = np.array([[0.4, -1.0], [0.1, 1.0]])
+    pp = np.clip(p / 2 + 0.5, 0, 1)
+    tt = t / 2 + 0.5
+    assert utils.psnr(p, t) == pytest.approx(10 * np.log10(1 / np.mean((pp - tt) ** 2)))
+
+
+def test_training_loop_reproduces_reference_trajectory(tmp_path):
+    """siren_mri_amd.training.train driving the CPU oracle model reproduces the reference's own
+    training.train trajectory (losses + final params): pins the loop (Adam, loss sum, zero_grad)."""
+    d = load("train_c1.npz")
+    model = orc.OracleSiren(hidden_features=256, num_hidden_layers=1)
+    with torch.no_grad():
+        for i in range(3):
+            model.weights[i].copy_(torch.from_numpy(d[f"init/net.net.{i}.0.weight"]))
+            model.biases[i].copy_(torch.from_numpy(d[f"init/net.net.{i}.0.bias"]))
+    loader = [({"coords": dataio.get_mgrid(64)[None]}, {"img": torch.from_numpy(d["img"])})]
+    loss_fn = lambda o, g: loss_functions.image_mse(None, o, g, high_freq=False)  # noqa: E731
+    ret = training.train(model, loader, epochs=10, lr=1e-4, steps_til_summary=1000, epochs_til_checkpoint=1000,
+                         model_dir=str(tmp_path / "run"), loss_fn=loss_fn, summary_fn=lambda *a, **k: None)
+    losses = np.loadtxt(tmp_path / "run" / "checkpoints" / "train_losses_final.txt")
+    np.testing.assert_allclose(losses, d["losses"], rtol=1e-5)
+    assert ret == pytest.approx(losses[-1], rel=1e-5)
+    for i in range(3):
+        assert orc.norm_rel(model.weights[i].detach(), torch.from_numpy(d[f"final/net.net.{i}.0.weight"])) < 1e-5
+    assert (tmp_path / "run" / "checkpoints" / "model_final.pth").exists()
+
+
+def test_hypernet_architecture_matches_reference_state_dict():
+    d = load("hypernet.npz")
+    model = meta_modules.ConvolutionalNeuralProcessImplicit2DHypernetFourierFeatures(
+        in_features=16, out_features=2, image_resolution=(128, 128), fourier_features_size=16, latent_dim=16,
+        hidden_features=32, num_hidden_layers=1, hyper_hidden_features=16, hyper_hidden_layers=1,
+        conv_kernel_size=3, num_conv_res_blocks=1, w0=30)
+    sd = model.state_dict()
+    ref = {k[len("state/"):]: d[k] for k in d.files if k.startswith("state/")}
+    assert sorted(sd.keys()) == sorted(ref.keys())
+    for k in ref:
+        assert tuple(sd[k].shape) == ref[k].shape, k
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in ref.items()})
+    names = model.hyper_net.names
+    assert names == [n for n, _ in model.hypo_net.meta_named_parameters()]
+
+
+def test_diff_operators_autograd_path_for_non_siren():
+    x = torch.randn(1, 10, 2, requires_grad=True)
+    y = (x ** 3).sum(-1, keepdim=True)
+    g = diff_operators.gradient(y, x)
+    assert torch.allclose(g, 3 * x ** 2)
+    lap = diff_operators.laplace(y, x)
+    assert torch.allclose(lap, (6 * x).sum(-1, keepdim=True))

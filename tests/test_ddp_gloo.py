@@ -1,0 +1,147 @@
+"""Multi-process data-parallel path on CPU (gloo, world_size 2).
+
+1. Coordinate sharding (configs M/C1-C3 on N GPUs): each rank fits its contiguous row block of
+   the grid; one summed gradient all-reduce per step (GradAllReducer(op='sum')) makes the
+   sharded run reproduce the single-process full-grid fit exactly (SSE loss).
+2. train_ddp with a DistributedSampler (configs 4/5): averaged gradients (DDP semantics), ranks
+   stay bit-identical, only rank 0 writes checkpoints.
+The model is the CPU oracle (the SIREN kernels need a GPU); what is under test is the host-side
+exchange logic, which is device-independent.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import siren_oracle as orc
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def sse(out, gt):
+    return {"img_loss": ((out["model_out"] - gt["img"]) ** 2).sum() / (128 * 128)}
+
+
+def _sharded_worker(rank, world, port, side, steps, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    from siren_mri_amd.training_ddp import ddp_setup, shard_rows, GradAllReducer
+    ddp_setup(rank, world, backend="gloo")
+    torch.manual_seed(rank + 100)  # deliberately different local init: the broadcast must fix it
+    model = orc.OracleSiren(hidden_features=32, num_hidden_layers=1, seed=rank + 7)
+    reducer = GradAllReducer(model.parameters(), op="sum")
+    coords = orc.get_mgrid(side)
+    img = torch.sin(3 * coords[:, :1]) * torch.cos(2 * coords[:, 1:])
+    lo, hi = shard_rows(coords.shape[0], rank, world)
+    inp = {"coords": coords[lo:hi][None]}
+    gt = {"img": img[lo:hi][None]}
+    opt = torch.optim.Adam(lr=1e-3, params=model.parameters())
+    for _ in range(steps):
+        loss = sse(model(inp), gt)["img_loss"]
+        loss.backward()
+        reducer()
+        opt.step()
+        opt.zero_grad()
+    out_q.put((rank, [p.detach().numpy().copy() for p in model.parameters()]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_coordinate_sharded_fit_equals_full_fit():
+    world, side, steps = 2, 16, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, side, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single-process reference: rank 0's init (broadcast) on the full grid
+    model = orc.OracleSiren(hidden_features=32, num_hidden_layers=1, seed=7)
+    coords = orc.get_mgrid(side)
+    img = torch.sin(3 * coords[:, :1]) * torch.cos(2 * coords[:, 1:])
+    opt = torch.optim.Adam(lr=1e-3, params=model.parameters())
+    for _ in range(steps):
+        loss = sse(model({"coords": coords[None]}), {"img": img[None]})["img_loss"]
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+    for a, b in zip(results[0], results[1]):
+        assert np.array_equal(a, b), "ranks diverged"
+    for a, ref in zip(results[0], model.parameters()):
+        assert orc.norm_rel(torch.from_numpy(a), ref.detach()) < 1e-5
+
+
+class _SliceSet(torch.utils.data.Dataset):
+    def __init__(self, n=8, side=8):
+        self.coords = orc.get_mgrid(side)
+        g = torch.Generator().manual_seed(0)
+        self.imgs = [torch.randn(side * side, 1, generator=g) for _ in range(n)]
+
+    def __len__(self):
+        return len(self.imgs)
+
+    def __getitem__(self, i):
+        return {"coords": self.coords}, {"img": self.imgs[i]}
+
+
+def _train_ddp_worker(rank, world, port, root, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    from siren_mri_amd import training_ddp
+    training_ddp.ddp_setup(rank, world, backend="gloo")
+    model = orc.OracleSiren(hidden_features=16, num_hidden_layers=1, seed=rank)
+    ds = _SliceSet()
+    sampler = torch.utils.data.distributed.DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=True)
+    loader = torch.utils.data.DataLoader(ds, batch_size=2, sampler=sampler)
+    training_ddp.train_ddp(model, loader, epochs=2, lr=1e-3, steps_til_summary=1000, epochs_til_checkpoint=1000,
+                           model_dir=root, loss_fn=sse, summary_fn=lambda *a, **k: None, device=rank,
+                           clip_grad=True)
+    out_q.put((rank, [p.detach().numpy().copy() for p in model.parameters()]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_train_ddp_ranks_stay_identical(tmp_path):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    root = str(tmp_path / "ddp_run")
+    procs = [ctx.Process(target=_train_ddp_worker, args=(r, world, port, root, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for a, b in zip(results[0], results[1]):
+        assert np.array_equal(a, b)
+    assert os.path.exists(os.path.join(root, "checkpoints", "model_final.pth"))
+    losses = np.loadtxt(os.path.join(root, "checkpoints", "train_losses_final.txt"))
+    assert losses.shape == (4,)  # 2 epochs x 2 local batches of 2 slices
+
+
+def test_shard_rows_partition():
+    from siren_mri_amd.training_ddp import shard_rows
+    n, world = 262144 + 3, 8
+    spans = [shard_rows(n, r, world) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+    sizes = [b - a for a, b in spans]
+    assert max(sizes) - min(sizes) <= 1

@@ -1,0 +1,81 @@
+"""The C-ABI library loads (no GPU needed), exports every symbol include/siren_mri_amd.h declares,
+and validates descriptors / sizes workspaces without touching a device."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from siren_mri_amd import _native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "siren_mri_amd.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(siren_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_builds_and_exports_every_declared_symbol():
+    lib = _native.load_library()
+    declared = header_functions()
+    assert declared, "no functions parsed from the header"
+    assert sorted(_native.EXPORTED_SYMBOLS) == declared
+    for name in declared:
+        assert hasattr(lib, name), f"missing export {name}"
+    assert b"gfx950" in lib.siren_version()
+
+
+def test_library_is_gfx950_code_object():
+    data = open(_native.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def _desc(dims, prec=_native.PREC_BF16, **kw):
+    return _native.describe_only(dims, prec=prec, **kw)
+
+
+def test_check_accepts_reference_configs():
+    lib = _native.load_library()
+    for dims, kw in [([2, 256, 256, 256, 256, 1], dict(rows_per_batch=512 * 512)),
+                     ([2, 256, 256, 1], dict(rows_per_batch=64 * 64)),
+                     ([16, 256, 256, 256, 256, 2], dict(batch=32, rows_per_batch=16384, weights_batched=True))]:
+        for prec in (_native.PREC_F32, _native.PREC_BF16):
+            d = _desc(dims, prec=prec, **kw)
+            assert lib.siren_mlp_check(ctypes.byref(d)) == 0, _native.last_error()
+            assert lib.siren_mlp_saved_bytes(ctypes.byref(d)) > 0
+            assert lib.siren_mlp_workspace_bytes(ctypes.byref(d)) > 0
+
+
+@pytest.mark.parametrize("dims,msg", [
+    ([2, 100, 1], "hidden width"),          # not a multiple of 32
+    ([40, 256, 1], "in_features"),          # too wide a first layer
+    ([2, 256, 9], "out_features"),          # too wide an output layer
+    ([2, 1], "num_layers"),                 # a single linear layer is not an FCBlock
+])
+def test_check_rejects_unsupported(dims, msg):
+    lib = _native.load_library()
+    d = _desc(dims)
+    assert lib.siren_mlp_check(ctypes.byref(d)) != 0
+    assert msg in _native.last_error()
+
+
+def test_saved_bytes_formula_bf16():
+    """saved = prepared bf16 weights (W and W^T of each MFMA layer) + one 16-bit phase tensor per
+    sine layer — 2 bytes per activation element."""
+    lib = _native.load_library()
+    rows = 512 * 512
+    d = _desc([2, 256, 256, 256, 256, 1], rows_per_batch=rows)
+    got = lib.siren_mlp_saved_bytes(ctypes.byref(d))
+    weights = 3 * 2 * 256 * 256 * 2
+    phases = 4 * rows * 256 * 2
+    assert got == weights + phases
+
+
+def test_empty_input_rejected():
+    lib = _native.load_library()
+    d = _desc([2, 64, 1], rows_per_batch=0)
+    assert lib.siren_mlp_check(ctypes.byref(d)) != 0
+    assert "empty" in _native.last_error()
