@@ -1,0 +1,106 @@
+"""GPU: the drop-in modules and loop against the REFERENCE's recorded outputs (tests/golden).
+
+  * SingleBVPNet forward (shared and hypernetwork-batched params) vs forward.npz
+  * training.train, 10 Adam steps on the 64^2 cameraman, fp32 path vs the reference loop's own
+    losses and final parameters (train_c1.npz)
+  * the config-4 hypernetwork model (reduced sizes) with the reference's state_dict vs the
+    reference's model_out and losses (hypernet.npz)
+fp32 tolerances: 1e-5 norm-relative (north_star); bf16 path: 3e-2.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import siren_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(G, name), allow_pickle=False)
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-5), ("bf16", 3e-2)])
+def test_singlebvpnet_forward_matches_reference(precision, tol):
+    from siren_mri_amd import modules
+    d = load("forward.npz")
+    m = modules.SingleBVPNet(type="sine", hidden_features=64, num_hidden_layers=2, precision=precision)
+    m.load_state_dict({k[len("param/"):]: torch.from_numpy(d[k]) for k in d.files if k.startswith("param/")})
+    m = m.to(DEV)
+    out = m({"coords": torch.from_numpy(d["coords"]).to(DEV)})
+    assert orc.norm_rel(out["model_out"].detach().cpu(), torch.from_numpy(d["model_out"])) < tol
+    params = {k: torch.stack([v, v * 1.05]) for k, v in m.state_dict().items()}
+    outb = m({"coords": torch.from_numpy(d["coords"]).to(DEV).repeat(2, 1, 1)}, params=params)
+    assert orc.norm_rel(outb["model_out"].detach().cpu(), torch.from_numpy(d["batched_out"])) < tol
+
+
+def test_training_train_matches_reference_loop(tmp_path):
+    from siren_mri_amd import dataio, loss_functions, modules, training
+    d = load("train_c1.npz")
+    m = modules.SingleBVPNet(type="sine", hidden_features=256, num_hidden_layers=1, precision="fp32")
+    m.load_state_dict({k[len("init/"):]: torch.from_numpy(d[k]) for k in d.files if k.startswith("init/")})
+    m = m.to(DEV)
+    loader = [({"coords": dataio.get_mgrid(64)[None]}, {"img": torch.from_numpy(d["img"])})]
+    loss_fn = lambda o, g: loss_functions.image_mse(None, o, g, high_freq=False)  # noqa: E731
+    training.train(m, loader, epochs=10, lr=1e-4, steps_til_summary=1000, epochs_til_checkpoint=1000,
+                   model_dir=str(tmp_path / "run"), loss_fn=loss_fn, summary_fn=lambda *a, **k: None)
+    losses = np.loadtxt(tmp_path / "run" / "checkpoints" / "train_losses_final.txt")
+    np.testing.assert_allclose(losses, d["losses"], rtol=1e-5)
+    sd = m.state_dict()
+    for k in sd:
+        assert orc.norm_rel(sd[k].cpu(), torch.from_numpy(d["final/" + k])) < 1e-4, k
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-5), ("bf16", 5e-2)])
+def test_hypernetwork_forward_matches_reference(precision, tol):
+    from siren_mri_amd import dataio, features, loss_functions, meta_modules
+    d = load("hypernet.npz")
+    model = meta_modules.ConvolutionalNeuralProcessImplicit2DHypernetFourierFeatures(
+        in_features=16, out_features=2, image_resolution=(128, 128), fourier_features_size=16, latent_dim=16,
+        hidden_features=32, num_hidden_layers=1, hyper_hidden_features=16, hyper_hidden_layers=1,
+        conv_kernel_size=3, num_conv_res_blocks=1, w0=30, precision=precision)
+    model.load_state_dict({k[len("state/"):]: torch.from_numpy(d[k]) for k in d.files if k.startswith("state/")})
+    model = model.to(DEV)
+    ff = features.GaussianFourierFeatureTransform(2, 8, 21, loaded_B=torch.from_numpy(d["B"]), device=DEV)
+    kspace = torch.from_numpy(d["kspace"]).to(DEV)
+    mask = torch.from_numpy(d["mask"].astype(np.float32)).to(DEV)
+    coords = dataio.get_mgrid(128)[None].repeat(2, 1, 1).to(DEV)
+    torch.backends.cudnn.allow_tf32 = False
+    with torch.no_grad():
+        out = model({"coords": ff(coords), "img_sparse": mask * kspace, "dc_mask": mask})
+    assert orc.norm_rel(out["latent_vec"].cpu(), torch.from_numpy(d["latent"])) < 1e-4
+    assert orc.norm_rel(out["model_out"].cpu(), torch.from_numpy(d["model_out"])) < tol
+    gt = {"img": kspace.permute(0, 2, 3, 1).reshape(2, -1, 2)}
+    hl = loss_functions.image_hypernetwork_loss(None, 2.78e-8, 6.4e-6, out, gt)
+    assert hl["img_loss"].item() == pytest.approx(float(d["img_loss"]), rel=max(tol, 1e-5))
+
+
+def test_hypernetwork_backward_reaches_hypernet_params():
+    from siren_mri_amd import dataio, features, loss_functions, meta_modules
+    d = load("hypernet.npz")
+    model = meta_modules.ConvolutionalNeuralProcessImplicit2DHypernetFourierFeatures(
+        in_features=16, out_features=2, image_resolution=(128, 128), fourier_features_size=16, latent_dim=16,
+        hidden_features=32, num_hidden_layers=1, hyper_hidden_features=16, hyper_hidden_layers=1,
+        conv_kernel_size=3, num_conv_res_blocks=1, w0=30, precision="fp32")
+    model.load_state_dict({k[len("state/"):]: torch.from_numpy(d[k]) for k in d.files if k.startswith("state/")})
+    model = model.to(DEV)
+    ff = features.GaussianFourierFeatureTransform(2, 8, 21, loaded_B=torch.from_numpy(d["B"]), device=DEV)
+    kspace = torch.from_numpy(d["kspace"]).to(DEV)
+    mask = torch.from_numpy(d["mask"].astype(np.float32)).to(DEV)
+    coords = dataio.get_mgrid(128)[None].repeat(2, 1, 1).to(DEV)
+    torch.backends.cudnn.allow_tf32 = False
+    out = model({"coords": ff(coords), "img_sparse": mask * kspace, "dc_mask": mask})
+    gt = {"img": kspace.permute(0, 2, 3, 1).reshape(2, -1, 2)}
+    hl = loss_functions.image_hypernetwork_loss(None, 2.78e-8, 6.4e-6, out, gt)
+    (hl["img_loss"].mean() + hl["latent_loss"].mean() + hl["hypo_weight_loss"].mean()).backward()
+    checked = 0
+    for n, p in model.named_parameters():
+        key = "gradnorm/" + n
+        if key in d.files and p.grad is not None and n.startswith("hyper_net"):
+            assert p.grad.norm().item() == pytest.approx(float(d[key]), rel=1e-3), n
+            checked += 1
+    assert checked > 0
