@@ -98,6 +98,30 @@ int siren_mlp_backward(const siren_mlp_desc* d, const float* x, const float* dy,
                        float* dx, void* stream);
 
 /*
+ * Analytic spatial derivatives of the SIREN output w.r.t. its input (tangent streams carried
+ * through the fused layers instead of an autograd graph). Replaces diff_operators.gradient
+ * (diff_operators.py:39-43: grad[n][k] = sum_c dy_c/dx_k) and, with order 2, laplace
+ * (diff_operators.py:27-36: lap[n] = sum_c sum_k d2y_c/dx_k2). Needs outermost_linear and
+ * in_features <= 4. `saved` (may be NULL for order 2 / inference) keeps the per-layer phases and
+ * tangents for siren_jvp_backward.
+ */
+int64_t siren_jvp_saved_bytes(const siren_mlp_desc* d, int order);
+int64_t siren_jvp_workspace_bytes(const siren_mlp_desc* d, int order);
+int siren_jvp_forward(const siren_mlp_desc* d, int order, const float* x, float* grad, float* lap,
+                      void* saved, int64_t saved_bytes, void* workspace, int64_t workspace_bytes,
+                      void* stream);
+
+/*
+ * Backward of a loss on the gradient (order 1): from dgrad = dL/dgrad [rows, in_features] writes
+ * dweight/dbias (overwrite) and, if dx != NULL, dx. This is the double backward that
+ * loss_functions.gradients_mse (loss_functions.py:330-335) runs through autograd.
+ */
+int siren_jvp_backward(const siren_mlp_desc* d, int order, const float* x, const float* dgrad,
+                       const void* saved, int64_t saved_bytes, void* workspace,
+                       int64_t workspace_bytes, float* const* dweight, float* const* dbias,
+                       float* dx, void* stream);
+
+/*
  * Optional per-kernel-class timing, for benchmarks and profiling (not thread-safe; not for use
  * under hipGraph capture). While enabled, each launch of `kernel_class` is bracketed by a
  * hipEventRecord pair on the launch's stream (at most `max_launches` launches are recorded).

@@ -1,0 +1,593 @@
+// siren_jvp.hip — analytic spatial derivatives of a SIREN (diff_operators.gradient / laplace)
+// and the adjoint of the gradient (the double backward of gradients_mse), for gfx950.
+//
+// Reference: diff_operators.py:27-43 computes them with autograd (create_graph=True), i.e. a
+// recorded reverse pass plus a double-backward for loss_functions.gradients_mse (:330-335).
+// Here they are forward-mode "tangent streams" carried next to the primal through every layer:
+//
+//   h = sin(p), p = w0 a, a_l = W_l h_{l-1} + b_l
+//   u_l^k = W_l t_{l-1}^k        t_l^k = w0 cos(p_l) u_l^k      (u_0^k = W_0[:, k])
+//   V_l   = W_l S_{l-1}          S_l   = w0 cos(p_l) V_l - w0^2 sin(p_l) sum_k (u_l^k)^2   (V_0 = 0)
+//   gradient_k = sum_o (W_L t_{L-1}^k)_o          laplace = sum_o (W_L S_{L-1})_o
+//
+// Rows of every GEMM are STREAM-STACKED: for weight set b the operand is [S][N][K] (stream 0 the
+// primal, 1..C the tangents, C+1 the Laplacian stream), so one MFMA GEMM per layer advances all
+// streams with the same W_l; the prologue builds each stream's operand from the stored primal
+// phase P and the stored pre-activation tangents U, the epilogue stores P (stream 0) or U.
+//
+// Backward of a loss on the gradient (adjoints, stream-stacked D = [a_bar; u_bar^1..C]):
+//   u_bar^k = w0 cos(p) t_bar^k ;  a_bar = w0 (cos(p) h_bar - w0 sin(p) sum_k t_bar^k u^k)
+//   W_bar_l = D^T [h_{l-1}; t_{l-1}^k] ; b_bar_l = sum a_bar ; [h_bar; t_bar^k]_{l-1} = D W_l
+//   first layer: W_bar_0 = a_bar^T x + [sum_n u_bar^k as column k] ; x_bar = a_bar W_0
+#include "siren_common.h"
+
+namespace siren {
+
+constexpr int JMODE_FWD = 0;  // stream-stacked forward (phase/tangent prologue, P/U epilogue)
+constexpr int JMODE_BWD = 1;  // adjoint: A = D (grad_t), raw fp32 output
+
+struct JNTArgs {
+  const void* P;      // [B][N][K] phase_t (JFWD)
+  const float* U;     // [B][S-1][N][K] fp32 (JFWD)
+  const void* D;      // [B][S][N][K] grad_t (JBWD)
+  const void* W;      // [nb_w][Nout][K] op_t
+  const float* bias;  // [nb_w][Nout]
+  void* Pout;         // [B][N][Nout] phase_t (JFWD)
+  float* Uout;        // JFWD: [B][S-1][N][Nout]; JBWD: raw [B][S][N][Nout]
+  int64_t N;          // rows per stream
+  int S, C, lap;
+  int64_t w_bstride, b_bstride;
+  int K, Nout;
+  float w0;
+};
+
+constexpr int JNT_BM = 128;
+constexpr int JNT_BN = 256;
+constexpr int JNT_KC = 32;
+
+template <int PREC> struct JNTLds;
+template <> struct JNTLds<kPrecBF16> {
+  static constexpr int ROW = 40;
+  static constexpr int BYTES = (JNT_BM + JNT_BN) * ROW * 2;
+};
+template <> struct JNTLds<kPrecF32> {
+  static constexpr int ROW = 33;
+  static constexpr int BYTES = (JNT_BM + JNT_BN) * ROW * 4;
+};
+
+// Operand element of stacked row (s, n), column k, from the stored layer-(l-1) quantities.
+template <int PREC>
+DEV void jvp_operand4(const JNTArgs& a, int64_t b, int s, int64_t n, int k, float (&out)[4]) {
+  using PT = Prec<PREC>;
+  using phase_t = typename PT::phase_t;
+  const phase_t* P = (const phase_t*)a.P + (b * a.N + n) * a.K + k;
+  const int64_t plane = a.N * (int64_t)a.K;  // one stream of U
+  const float* Ub = a.U + b * (int64_t)(a.S - 1) * plane + n * a.K + k;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const phase_t p = P[e];
+    if (s == 0) {
+      out[e] = PT::sinp(p);
+    } else if (s <= a.C) {
+      out[e] = a.w0 * PT::cosp(p) * Ub[(int64_t)(s - 1) * plane + e];
+    } else {
+      float ss = 0.f;
+      for (int j = 0; j < a.C; ++j) {
+        const float u = Ub[(int64_t)j * plane + e];
+        ss = fmaf(u, u, ss);
+      }
+      out[e] = a.w0 * PT::cosp(p) * Ub[(int64_t)a.C * plane + e] - a.w0 * a.w0 * PT::sinp(p) * ss;
+    }
+  }
+}
+
+template <int PREC, int MODE>
+__global__ __launch_bounds__(256) void jvp_nt_kernel(JNTArgs a) {
+  using PT = Prec<PREC>;
+  using phase_t = typename PT::phase_t;
+  using grad_t = typename PT::grad_t;
+  using op_t = typename PT::op_t;
+  constexpr int ROW = JNTLds<PREC>::ROW;
+  constexpr bool BF = PREC == kPrecBF16;
+  __shared__ __attribute__((aligned(16))) char smem[JNTLds<PREC>::BYTES];
+  op_t* As = (op_t*)smem;
+  op_t* Bs = As + JNT_BM * ROW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t b = blockIdx.z;
+  const int64_t rows = (int64_t)a.S * a.N;  // stacked rows of this weight set
+  const int64_t m0 = (int64_t)blockIdx.x * JNT_BM;
+  const int n0 = blockIdx.y * JNT_BN;
+  const int K = a.K;
+  const op_t* W = (const op_t*)a.W + b * a.w_bstride;
+
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  // A chunk: 128 rows x 32 k = 1024 units of 4 -> 4 per thread. B chunk: 256 x 32 -> 8 units/thread.
+  float areg[4][4];
+  float breg[8][4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int u = tid + 256 * q;
+      const int r = u >> 3, k = k0 + (u & 7) * 4;
+      const int64_t row = m0 + r;
+      if (row < rows) {
+        const int s = (int)(row / a.N);
+        const int64_t n = row - (int64_t)s * a.N;
+        if constexpr (MODE == JMODE_FWD) {
+          jvp_operand4<PREC>(a, b, s, n, k, areg[q]);
+        } else {
+          const grad_t* D = (const grad_t*)a.D + (b * rows + row) * K + k;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) areg[q][e] = to_f32(D[e]);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) areg[q][e] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int u = tid + 256 * q;
+      const int c = u >> 3, k = k0 + (u & 7) * 4;
+      const int col = n0 + c;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) breg[q][e] = col < a.Nout ? to_f32(W[(int64_t)col * K + k + e]) : 0.f;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int u = tid + 256 * q;
+      const int r = u >> 3, kq = (u & 7) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) As[r * ROW + kq + e] = from_f32<op_t>(areg[q][e]);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int u = tid + 256 * q;
+      const int c = u >> 3, kq = (u & 7) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Bs[c * ROW + kq + e] = from_f32<op_t>(breg[q][e]);
+    }
+  };
+
+  const int r32 = lane & 31, h = lane >> 5;
+  const int nk = K / JNT_KC;
+  load(0);
+  for (int kc = 0; kc < nk; ++kc) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (kc + 1 < nk) load((kc + 1) * JNT_KC);
+    if constexpr (BF) {
+#pragma unroll
+      for (int ks = 0; ks < JNT_KC / 16; ++ks) {
+        bf16x8 af[2], bfr[4];
+#pragma unroll
+        for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) af[bm][e] = As[(64 * wm + 32 * bm + r32) * ROW + ks * 16 + h * 8 + e];
+#pragma unroll
+        for (int bn = 0; bn < 4; ++bn)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bfr[bn][e] = Bs[(128 * wn + 32 * bn + r32) * ROW + ks * 16 + h * 8 + e];
+#pragma unroll
+        for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+          for (int bn = 0; bn < 4; ++bn)
+            acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[bm], bfr[bn], acc[bm][bn], 0, 0, 0);
+      }
+    } else {
+#pragma unroll 4
+      for (int ks = 0; ks < JNT_KC / 2; ++ks) {
+        float af[2], bfr[4];
+#pragma unroll
+        for (int bm = 0; bm < 2; ++bm) af[bm] = As[(64 * wm + 32 * bm + r32) * ROW + 2 * ks + h];
+#pragma unroll
+        for (int bn = 0; bn < 4; ++bn) bfr[bn] = Bs[(128 * wn + 32 * bn + r32) * ROW + 2 * ks + h];
+#pragma unroll
+        for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+          for (int bn = 0; bn < 4; ++bn)
+            acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[bm], bfr[bn], acc[bm][bn], 0, 0, 0);
+      }
+    }
+  }
+
+  const float* bias = a.bias ? a.bias + b * a.b_bstride : nullptr;
+#pragma unroll
+  for (int bn = 0; bn < 4; ++bn) {
+    const int col = n0 + 128 * wn + 32 * bn + (lane & 31);
+    if (col >= a.Nout) continue;
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int64_t row = m0 + 64 * wm + 32 * bm + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        if (row >= rows) continue;
+        const float v = acc[bm][bn][e];
+        if constexpr (MODE == JMODE_FWD) {
+          const int s = (int)(row / a.N);
+          const int64_t n = row - (int64_t)s * a.N;
+          if (s == 0)
+            ((phase_t*)a.Pout)[(b * a.N + n) * a.Nout + col] = PT::enc(a.w0 * (v + bias[col]));
+          else
+            a.Uout[((b * (a.S - 1) + (s - 1)) * a.N + n) * a.Nout + col] = v;
+        } else {
+          a.Uout[(b * rows + row) * a.Nout + col] = v;
+        }
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Weight gradient over stream-stacked rows: dW[i][j] = sum_r D[r][i] X[r][j] (split-K over the
+// S' * N stacked rows), X = [sin(P); w0 cos(P) U^k]; db[i] = sum over stream-0 rows of D.
+struct JTNArgs {
+  const void* D;      // [B][S'][N][M] grad_t
+  const void* P;      // [B][N][Kin] phase_t (layer l-1)
+  const float* U;     // [B][Su][N][Kin] fp32 tangents of layer l-1 (Su = stored U streams)
+  float* part;        // split s, batch b slab at part + s*split_stride + b*(M*Kin + M)
+  int64_t N;
+  int64_t rows_per_split;
+  int64_t split_stride;
+  int S, Su;          // S' = 1 + C adjoint streams
+  int M, Kin;
+  float w0;
+};
+
+template <int PREC>
+__global__ __launch_bounds__(256) void jvp_tn_kernel(JTNArgs a) {
+  using PT = Prec<PREC>;
+  using phase_t = typename PT::phase_t;
+  using grad_t = typename PT::grad_t;
+  using op_t = typename PT::op_t;
+  constexpr int KC = 32;
+  constexpr int ROWF = 128 + 1;  // fp32 staging row (padded)
+  __shared__ float Ds[KC][ROWF];
+  __shared__ float Xs[KC][ROWF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_n = (a.Kin + 127) / 128;
+  const int i0 = (blockIdx.x / tiles_n) * 128, j0 = (blockIdx.x % tiles_n) * 128;
+  const int split = blockIdx.y;
+  const int64_t b = blockIdx.z;
+  const int64_t rows = (int64_t)a.S * a.N;
+  const int64_t r_begin = (int64_t)split * a.rows_per_split;
+  const int64_t r_end = min(r_begin + a.rows_per_split, rows);
+  const int64_t plane = a.N * (int64_t)a.Kin;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  float dbacc[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) dbacc[e] = 0.f;
+
+  for (int64_t rc = r_begin; rc < r_end; rc += KC) {
+    __syncthreads();
+    // stage 32 rows x 128 columns of D and X (16 elements per thread each)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int u = tid + 256 * q;
+      const int r = u >> 7, c = u & 127;
+      const int64_t row = rc + r;
+      float dv = 0.f, xv = 0.f;
+      if (row < r_end) {
+        const int s = (int)(row / a.N);
+        const int64_t n = row - (int64_t)s * a.N;
+        if (i0 + c < a.M) dv = to_f32(((const grad_t*)a.D)[(b * rows + row) * a.M + i0 + c]);
+        if (j0 + c < a.Kin) {
+          const phase_t p = ((const phase_t*)a.P)[(b * a.N + n) * a.Kin + j0 + c];
+          xv = (s == 0) ? PT::sinp(p)
+                        : a.w0 * PT::cosp(p) * a.U[(b * a.Su + (s - 1)) * plane + n * a.Kin + j0 + c];
+        }
+        if (s == 0) dbacc[q] += dv;
+      }
+      Ds[r][c] = to_f32(from_f32<op_t>(dv));
+      Xs[r][c] = to_f32(from_f32<op_t>(xv));
+    }
+    __syncthreads();
+    const int r32 = lane & 31, h = lane >> 5;
+    if constexpr (PREC == kPrecBF16) {
+#pragma unroll
+      for (int ks = 0; ks < KC / 16; ++ks) {
+        bf16x8 af[2], bfr[2];
+#pragma unroll
+        for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) af[bm][e] = (bf16)Ds[16 * ks + 8 * h + e][64 * wm + 32 * bm + r32];
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bfr[bn][e] = (bf16)Xs[16 * ks + 8 * h + e][64 * wn + 32 * bn + r32];
+#pragma unroll
+        for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+          for (int bn = 0; bn < 2; ++bn)
+            acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[bm], bfr[bn], acc[bm][bn], 0, 0, 0);
+      }
+    } else {
+#pragma unroll 4
+      for (int ks = 0; ks < KC / 2; ++ks) {
+        float af[2], bfr[2];
+#pragma unroll
+        for (int bm = 0; bm < 2; ++bm) af[bm] = Ds[2 * ks + h][64 * wm + 32 * bm + r32];
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn) bfr[bn] = Xs[2 * ks + h][64 * wn + 32 * bn + r32];
+#pragma unroll
+        for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+          for (int bn = 0; bn < 2; ++bn)
+            acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[bm], bfr[bn], acc[bm][bn], 0, 0, 0);
+      }
+    }
+  }
+  float* part = a.part + (int64_t)split * a.split_stride + b * ((int64_t)a.M * a.Kin + a.M);
+#pragma unroll
+  for (int bn = 0; bn < 2; ++bn) {
+    const int col = j0 + 64 * wn + 32 * bn + (lane & 31);
+    if (col >= a.Kin) continue;
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = i0 + 64 * wm + 32 * bm + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        if (row < a.M) part[(int64_t)row * a.Kin + col] = acc[bm][bn][e];
+      }
+  }
+  if (j0 == 0) {
+    // every thread staged the same column (tid & 127) in all 16 of its units
+    __syncthreads();
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s += dbacc[e];
+    Ds[tid >> 7][tid & 127] = s;
+    __syncthreads();
+    if (tid < 128 && i0 + tid < a.M) part[(int64_t)a.M * a.Kin + i0 + tid] = Ds[0][tid] + Ds[1][tid];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// First layer: P0 = enc(w0 (x W0^T + b0)), U0[k] = W0[:, k] broadcast over rows, V0 = 0.
+struct JFirstArgs {
+  const float* x;     // [B][N][C]
+  const float* W;     // [nb_w][F][C]
+  const float* bias;  // [nb_w][F]
+  void* P;            // [B][N][F]
+  float* U;           // [B][Su][N][F]
+  int64_t N;
+  int C, F, Su;
+  int64_t w_bstride, b_bstride;
+  float w0;
+};
+
+template <int PREC>
+__global__ __launch_bounds__(256) void jvp_first_kernel(JFirstArgs a) {
+  using PT = Prec<PREC>;
+  using phase_t = typename PT::phase_t;
+  const int64_t b = blockIdx.y;
+  const float* W = a.W + b * a.w_bstride;
+  const float* bias = a.bias + b * a.b_bstride;
+  const int64_t total = a.N * a.F;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+    const int64_t n = idx / a.F;
+    const int f = (int)(idx - n * a.F);
+    const float* xr = a.x + (b * a.N + n) * a.C;
+    float z = 0.f;
+    for (int c = 0; c < a.C; ++c) z = fmaf(xr[c], W[f * a.C + c], z);
+    ((phase_t*)a.P)[(b * a.N + n) * a.F + f] = PT::enc(a.w0 * (z + bias[f]));
+    for (int s = 0; s < a.Su; ++s)
+      a.U[((b * a.Su + s) * a.N + n) * a.F + f] = (s < a.C) ? W[f * a.C + s] : 0.f;
+  }
+}
+
+// Output layer: grad[n][k] = sum_o sum_f W[o][f] t^k[f]; lap[n] = sum_o sum_f W[o][f] S[f].
+// One half-wave per row.
+struct JLastArgs {
+  const void* P;      // [B][N][F]
+  const float* U;     // [B][Su][N][F]
+  const float* W;     // [nb_w][O][F]
+  float* grad;        // [B][N][C]
+  float* lap;         // [B][N] or null
+  int64_t N;
+  int C, F, O, Su;
+  int64_t w_bstride;
+  float w0;
+};
+
+template <int PREC>
+__global__ __launch_bounds__(256) void jvp_last_kernel(JLastArgs a) {
+  using PT = Prec<PREC>;
+  using phase_t = typename PT::phase_t;
+  const int l32 = threadIdx.x & 31;
+  const int64_t b = blockIdx.y;
+  const float* W = a.W + b * a.w_bstride;
+  const int64_t plane = a.N * (int64_t)a.F;
+  for (int64_t n = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5); n < a.N; n += (int64_t)gridDim.x * 8) {
+    float g[4] = {0.f, 0.f, 0.f, 0.f};
+    float lp = 0.f;
+    for (int f = l32; f < a.F; f += 32) {
+      float ws = 0.f;
+      for (int o = 0; o < a.O; ++o) ws += W[o * a.F + f];
+      const phase_t p = ((const phase_t*)a.P)[(b * a.N + n) * a.F + f];
+      const float c = PT::cosp(p), s = PT::sinp(p);
+      const float* Ub = a.U + b * (int64_t)a.Su * plane + n * a.F + f;
+      float ss = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (k < a.C) {
+          const float u = Ub[(int64_t)k * plane];
+          g[k] = fmaf(ws, a.w0 * c * u, g[k]);
+          ss = fmaf(u, u, ss);
+        }
+      }
+      if (a.lap) lp = fmaf(ws, a.w0 * c * Ub[(int64_t)a.C * plane] - a.w0 * a.w0 * s * ss, lp);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k < a.C) {
+        float v = g[k];
+#pragma unroll
+        for (int off = 16; off >= 1; off >>= 1) v += __shfl_xor(v, off, 32);
+        if (l32 == 0) a.grad[(b * a.N + n) * a.C + k] = v;
+      }
+    }
+    if (a.lap) {
+#pragma unroll
+      for (int off = 16; off >= 1; off >>= 1) lp += __shfl_xor(lp, off, 32);
+      if (l32 == 0) a.lap[b * a.N + n] = lp;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Adjoint combine for a sine layer: from t_bar^k (and h_bar) to D = [a_bar; u_bar^k] (grad_t).
+// top = 1: the output layer's adjoint, t_bar^k[f] = gbar[n][k] * sum_o W_L[o][f], h_bar = 0,
+//          and also the output-layer weight-gradient partials dW_L[o][f] = sum_n sum_k gbar t^k[f].
+// top = 0: raw = [h_bar; t_bar^1..C] (fp32, [B][S'][N][F]) from the previous adjoint GEMM.
+struct JCombArgs {
+  const void* P;      // [B][N][F] phase_t of this layer
+  const float* U;     // [B][Su][N][F] tangents of this layer
+  const float* raw;   // top=0
+  const float* gbar;  // top=1: [B][N][C]
+  const float* WL;    // top=1: [nb_w][O][F]
+  void* D;            // [B][S'][N][F] grad_t
+  float* part;        // top=1: dW_L partial slabs (split s, batch b at s*split_stride + b*(O*F + O))
+  int64_t N;
+  int64_t rows_per_split;
+  int64_t split_stride;
+  int C, F, O, Su, top;
+  int64_t w_bstride;
+  float w0;
+};
+
+template <int PREC>
+__global__ __launch_bounds__(256) void jvp_combine_kernel(JCombArgs a) {
+  using PT = Prec<PREC>;
+  using phase_t = typename PT::phase_t;
+  using grad_t = typename PT::grad_t;
+  __shared__ float red[256];
+  const int64_t b = blockIdx.y;
+  const int S = 1 + a.C;
+  const int64_t plane = a.N * (int64_t)a.F;
+  const float* WL = a.top ? a.WL + b * a.w_bstride : nullptr;
+  // thread owns feature column f = threadIdx.x (+256 k) for rows of its split
+  const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_split;
+  const int64_t r_end = min(r_begin + a.rows_per_split, a.N);
+  for (int f = threadIdx.x; f < a.F; f += 256) {
+    float ws = 0.f;
+    if (a.top)
+      for (int o = 0; o < a.O; ++o) ws += WL[o * a.F + f];
+    float dwl = 0.f;
+    for (int64_t n = r_begin; n < r_end; ++n) {
+      const phase_t p = ((const phase_t*)a.P)[(b * a.N + n) * a.F + f];
+      const float c = PT::cosp(p), s = PT::sinp(p);
+      const float* Ub = a.U + b * (int64_t)a.Su * plane + n * a.F + f;
+      float hbar = 0.f, cross = 0.f;
+      if (!a.top) hbar = a.raw[(b * S * a.N + n) * a.F + f];
+      for (int k = 0; k < a.C; ++k) {
+        const float u = Ub[(int64_t)k * plane];
+        const float tbar = a.top ? a.gbar[(b * a.N + n) * a.C + k] * ws
+                                 : a.raw[((b * S + 1 + k) * a.N + n) * a.F + f];
+        if (a.top) dwl = fmaf(a.gbar[(b * a.N + n) * a.C + k], a.w0 * c * u, dwl);
+        cross = fmaf(tbar, u, cross);
+        ((grad_t*)a.D)[((b * S + 1 + k) * a.N + n) * a.F + f] = from_f32<grad_t>(a.w0 * c * tbar);
+      }
+      ((grad_t*)a.D)[(b * S * a.N + n) * a.F + f] = from_f32<grad_t>(a.w0 * (c * hbar - a.w0 * s * cross));
+    }
+    if (a.top) {
+      float* part = a.part + (int64_t)blockIdx.x * a.split_stride + b * (int64_t)(a.O * a.F + a.O);
+      for (int o = 0; o < a.O; ++o) part[o * a.F + f] = dwl;
+      if (f < a.O) part[a.O * a.F + f] = 0.f;
+    }
+  }
+  (void)red;
+}
+
+// First layer adjoint: dW0[f][c] = sum_n a_bar[n][f] x[n][c] + sum_n u_bar^c[n][f] (c < C),
+// db0[f] = sum_n a_bar[n][f], dx[n][c] = sum_f a_bar[n][f] W0[f][c]. Thread per feature column;
+// dx via a separate pass (jvp_first_dx_kernel).
+struct JFirstBwdArgs {
+  const void* D;      // [B][S'][N][F] grad_t
+  const float* x;     // [B][N][C]
+  const float* W;     // [nb_w][F][C]
+  float* dx;          // [B][N][C] or null
+  float* part;        // slabs of F*C + F
+  int64_t N;
+  int64_t rows_per_split;
+  int64_t split_stride;
+  int C, F;
+  int64_t w_bstride;
+};
+
+template <int PREC>
+__global__ __launch_bounds__(256) void jvp_first_bwd_kernel(JFirstBwdArgs a) {
+  using PT = Prec<PREC>;
+  using grad_t = typename PT::grad_t;
+  const int64_t b = blockIdx.y;
+  const int S = 1 + a.C;
+  const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_split;
+  const int64_t r_end = min(r_begin + a.rows_per_split, a.N);
+  float* part = a.part + (int64_t)blockIdx.x * a.split_stride + b * (int64_t)(a.F * a.C + a.F);
+  for (int f = threadIdx.x; f < a.F; f += 256) {
+    float dw[4] = {0.f, 0.f, 0.f, 0.f}, db = 0.f;
+    for (int64_t n = r_begin; n < r_end; ++n) {
+      const float abar = to_f32(((const grad_t*)a.D)[(b * S * a.N + n) * a.F + f]);
+      db += abar;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (c < a.C) {
+          const float ubar = to_f32(((const grad_t*)a.D)[((b * S + 1 + c) * a.N + n) * a.F + f]);
+          dw[c] += fmaf(abar, a.x[(b * a.N + n) * a.C + c], ubar);
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (c < a.C) part[f * a.C + c] = dw[c];
+    part[a.F * a.C + f] = db;
+  }
+}
+
+template <int PREC>
+__global__ __launch_bounds__(256) void jvp_first_dx_kernel(JFirstBwdArgs a) {
+  using PT = Prec<PREC>;
+  using grad_t = typename PT::grad_t;
+  const int64_t b = blockIdx.y;
+  const int S = 1 + a.C;
+  const float* W = a.W + b * a.w_bstride;
+  const int l32 = threadIdx.x & 31;
+  for (int64_t n = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5); n < a.N; n += (int64_t)gridDim.x * 8) {
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int f = l32; f < a.F; f += 32) {
+      const float abar = to_f32(((const grad_t*)a.D)[(b * S * a.N + n) * a.F + f]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (c < a.C) s[c] = fmaf(abar, W[f * a.C + c], s[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c < a.C) {
+        float v = s[c];
+#pragma unroll
+        for (int off = 16; off >= 1; off >>= 1) v += __shfl_xor(v, off, 32);
+        if (l32 == 0) a.dx[(b * a.N + n) * a.C + c] = v;
+      }
+    }
+  }
+}
+
+}  // namespace siren

@@ -10,6 +10,7 @@
 #include "../../include/siren_mri_amd.h"
 #include "siren_valu.hip"
 #include "siren_gemm.hip"
+#include "siren_jvp.hip"
 
 using namespace siren;
 
@@ -457,6 +458,276 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
   return SIREN_OK;
 }
 
+// ============================================================================================
+// Analytic derivatives (tangent streams): layout and orchestration.
+// saved = [prepared weights][P_l phase tensors, l = 0..L-2][U_l fp32 tangent planes, l = 0..L-2]
+// ============================================================================================
+struct JLayout {
+  Layout base;             // prepared-weight offsets (w_op_off / wt_op_off / weights_bytes)
+  int C, Su, S, Sb;        // tangents, stored U planes, forward streams, adjoint streams
+  int64_t p_off[SIREN_MAX_LAYERS], u_off[SIREN_MAX_LAYERS];
+  int64_t saved_bytes;
+  int64_t d_off[2], raw_off, part_off, ws_bytes;
+};
+
+Split jtn_split(const Geo& g, int64_t stacked_rows, int M, int N) {
+  const int64_t tiles = cdiv(M, 128) * cdiv(N, 128);
+  return split_rows(stacked_rows, tiles, g.nb, 32);
+}
+Split jcol_split(const Geo& g) { return split_rows(g.rows, 1, g.nb, 64); }
+
+JLayout jlayout_of(const siren_mlp_desc* d, int order) {
+  const Geo g = geo_of(d);
+  JLayout jl;
+  memset(&jl, 0, sizeof(jl));
+  jl.base = layout_of(d);
+  jl.C = d->dims[0];
+  jl.Su = jl.C + (order >= 2 ? 1 : 0);
+  jl.S = 1 + jl.Su;
+  jl.Sb = 1 + jl.C;
+  int64_t off = jl.base.weights_bytes;
+  for (int l = 0; l + 1 < g.L; ++l) {
+    jl.p_off[l] = off;
+    off = align_up(off + g.total * d->dims[l + 1] * g.phase_sz, 256);
+  }
+  for (int l = 0; l + 1 < g.L; ++l) {
+    jl.u_off[l] = off;
+    off = align_up(off + (int64_t)jl.Su * g.total * d->dims[l + 1] * 4, 256);
+  }
+  jl.saved_bytes = off;
+  off = align_up(jl.base.weights_bytes, 256);  // workspace (prepared weights first when no saved)
+  const int64_t act = (int64_t)jl.Sb * g.total * max_hidden(d);
+  for (int k = 0; k < 2; ++k) {
+    jl.d_off[k] = off;
+    off = align_up(off + act * g.grad_sz, 256);
+  }
+  jl.raw_off = off;
+  off = align_up(off + act * 4, 256);
+  int64_t part = 0;
+  for (int l = 1; l + 1 < g.L; ++l) {
+    const int M = d->dims[l + 1], N = d->dims[l];
+    const Split s = jtn_split(g, (int64_t)jl.Sb * g.rows, M, N);
+    part = std::max(part, s.nsplit * split_stride(g, (int64_t)M * N + M));
+  }
+  {
+    const Split s = jcol_split(g);
+    const int F = d->dims[g.L - 1], O = d->dims[g.L];
+    part = std::max(part, s.nsplit * split_stride(g, (int64_t)O * F + O));
+    const int F0 = d->dims[1], C = d->dims[0];
+    part = std::max(part, s.nsplit * split_stride(g, (int64_t)F0 * C + F0));
+  }
+  jl.part_off = off;
+  off = align_up(off + part * 4, 256);
+  jl.ws_bytes = off;
+  return jl;
+}
+
+int jvp_check(const siren_mlp_desc* d, int order) {
+  int rc = siren_mlp_check(d);
+  if (rc) return rc;
+  if (order != 1 && order != 2) return fail(SIREN_EINVAL, "derivative order %d unsupported (1 or 2)", order);
+  if (!d->outermost_linear) return fail(SIREN_EINVAL, "analytic derivatives need outermost_linear");
+  if (d->dims[0] > 4) return fail(SIREN_EINVAL, "analytic derivatives support in_features <= 4");
+  return SIREN_OK;
+}
+
+template <int PREC>
+int jvp_forward_impl(const siren_mlp_desc* d, int order, const float* x, float* grad, float* lap,
+                     char* saved, char* ws, hipStream_t st) {
+  const Geo g = geo_of(d);
+  const JLayout jl = jlayout_of(d, order);
+  char* base = saved ? saved : ws;
+  int rc = prep_weights<PREC>(d, g, jl.base, base, st);
+  if (rc) return rc;
+  // without a saved buffer the per-layer tensors still need a home: use the saved layout inside
+  // the workspace tail (jvp workspace queries include it in that case, see siren_jvp_workspace_bytes)
+  char* store = saved ? saved : ws + jl.ws_bytes;
+  {
+    JFirstArgs a;
+    a.x = x;
+    a.W = d->weight[0];
+    a.bias = d->bias[0];
+    a.P = store + jl.p_off[0];
+    a.U = (float*)(store + jl.u_off[0]);
+    a.N = g.rows;
+    a.C = d->dims[0];
+    a.F = d->dims[1];
+    a.Su = jl.Su;
+    a.w_bstride = d->weights_batched ? (int64_t)d->dims[1] * d->dims[0] : 0;
+    a.b_bstride = d->weights_batched ? d->dims[1] : 0;
+    a.w0 = d->w0;
+    hipLaunchKernelGGL(jvp_first_kernel<PREC>, dim3(grid1d(g.rows * a.F, std::max<int64_t>(1, 4096 / g.nb)), (unsigned)g.nb),
+                       dim3(256), 0, st, a);
+    if ((rc = check_launch("jvp_first"))) return rc;
+  }
+  for (int l = 1; l + 1 < g.L; ++l) {
+    JNTArgs a;
+    a.P = store + jl.p_off[l - 1];
+    a.U = (const float*)(store + jl.u_off[l - 1]);
+    a.D = nullptr;
+    a.W = PREC == kPrecBF16 ? (const void*)(base + jl.base.w_op_off[l]) : (const void*)d->weight[l];
+    a.bias = d->bias[l];
+    a.Pout = store + jl.p_off[l];
+    a.Uout = (float*)(store + jl.u_off[l]);
+    a.N = g.rows;
+    a.S = jl.S;
+    a.C = jl.C;
+    a.lap = order >= 2;
+    a.w_bstride = d->weights_batched ? (int64_t)d->dims[l + 1] * d->dims[l] : 0;
+    a.b_bstride = d->weights_batched ? d->dims[l + 1] : 0;
+    a.K = d->dims[l];
+    a.Nout = d->dims[l + 1];
+    a.w0 = d->w0;
+    dim3 grid((unsigned)cdiv((int64_t)jl.S * g.rows, JNT_BM), (unsigned)cdiv(a.Nout, JNT_BN), (unsigned)g.nb);
+    hipLaunchKernelGGL((jvp_nt_kernel<PREC, JMODE_FWD>), grid, dim3(256), 0, st, a);
+    if ((rc = check_launch("jvp_nt fwd"))) return rc;
+  }
+  {
+    const int l = g.L - 1;
+    JLastArgs a;
+    a.P = store + jl.p_off[l - 1];
+    a.U = (const float*)(store + jl.u_off[l - 1]);
+    a.W = d->weight[l];
+    a.grad = grad;
+    a.lap = order >= 2 ? lap : nullptr;
+    a.N = g.rows;
+    a.C = jl.C;
+    a.F = d->dims[l];
+    a.O = d->dims[l + 1];
+    a.Su = jl.Su;
+    a.w_bstride = d->weights_batched ? (int64_t)d->dims[l + 1] * d->dims[l] : 0;
+    a.w0 = d->w0;
+    hipLaunchKernelGGL(jvp_last_kernel<PREC>, dim3((unsigned)std::min<int64_t>(cdiv(g.rows, 8), 4096 / g.nb + 1), (unsigned)g.nb),
+                       dim3(256), 0, st, a);
+    if ((rc = check_launch("jvp_last"))) return rc;
+  }
+  return SIREN_OK;
+}
+
+template <int PREC>
+int jvp_backward_impl(const siren_mlp_desc* d, const float* x, const float* gbar, const char* saved,
+                      char* ws, float* const* dW, float* const* db, float* dx, hipStream_t st) {
+  const Geo g = geo_of(d);
+  const JLayout jl = jlayout_of(d, 1);
+  float* part = (float*)(ws + jl.part_off);
+  int rc = SIREN_OK;
+  int cur = 0;
+  {
+    const int l = g.L - 1;
+    const Split s = jcol_split(g);
+    JCombArgs a;
+    a.P = saved + jl.p_off[l - 1];
+    a.U = (const float*)(saved + jl.u_off[l - 1]);
+    a.raw = nullptr;
+    a.gbar = gbar;
+    a.WL = d->weight[l];
+    a.D = ws + jl.d_off[cur];
+    a.part = part;
+    a.N = g.rows;
+    a.rows_per_split = s.rows_per_split;
+    a.C = jl.C;
+    a.F = d->dims[l];
+    a.O = d->dims[l + 1];
+    a.Su = jl.Su;
+    a.top = 1;
+    a.split_stride = split_stride(g, (int64_t)a.O * a.F + a.O);
+    a.w_bstride = d->weights_batched ? (int64_t)d->dims[l + 1] * d->dims[l] : 0;
+    a.w0 = d->w0;
+    hipLaunchKernelGGL(jvp_combine_kernel<PREC>, dim3((unsigned)s.nsplit, (unsigned)g.nb), dim3(256), 0, st, a);
+    if ((rc = check_launch("jvp_combine top"))) return rc;
+    if ((rc = launch_reduce(part, s.nsplit, a.split_stride, g.nb, (int64_t)a.O * a.F + a.O,
+                            (int64_t)a.O * a.F, dW[l], db[l], st)))
+      return rc;
+  }
+  for (int l = g.L - 2; l >= 1; --l) {
+    const int M = d->dims[l + 1], N = d->dims[l];
+    {
+      const Split s = jtn_split(g, (int64_t)jl.Sb * g.rows, M, N);
+      JTNArgs a;
+      a.D = ws + jl.d_off[cur];
+      a.P = saved + jl.p_off[l - 1];
+      a.U = (const float*)(saved + jl.u_off[l - 1]);
+      a.part = part;
+      a.N = g.rows;
+      a.rows_per_split = s.rows_per_split;
+      a.split_stride = split_stride(g, (int64_t)M * N + M);
+      a.S = jl.Sb;
+      a.Su = jl.Su;
+      a.M = M;
+      a.Kin = N;
+      a.w0 = d->w0;
+      dim3 grid((unsigned)(cdiv(M, 128) * cdiv(N, 128)), (unsigned)s.nsplit, (unsigned)g.nb);
+      hipLaunchKernelGGL(jvp_tn_kernel<PREC>, grid, dim3(256), 0, st, a);
+      if ((rc = check_launch("jvp_tn"))) return rc;
+      if ((rc = launch_reduce(part, s.nsplit, a.split_stride, g.nb, (int64_t)M * N + M, (int64_t)M * N,
+                              dW[l], db[l], st)))
+        return rc;
+    }
+    {
+      JNTArgs a;
+      memset(&a, 0, sizeof(a));
+      a.D = ws + jl.d_off[cur];
+      a.W = saved + jl.base.wt_op_off[l];
+      a.Uout = (float*)(ws + jl.raw_off);
+      a.N = g.rows;
+      a.S = jl.Sb;
+      a.C = jl.C;
+      a.w_bstride = d->weights_batched ? (int64_t)M * N : 0;
+      a.K = M;
+      a.Nout = N;
+      a.w0 = d->w0;
+      dim3 grid((unsigned)cdiv((int64_t)jl.Sb * g.rows, JNT_BM), (unsigned)cdiv(N, JNT_BN), (unsigned)g.nb);
+      hipLaunchKernelGGL((jvp_nt_kernel<PREC, JMODE_BWD>), grid, dim3(256), 0, st, a);
+      if ((rc = check_launch("jvp_nt bwd"))) return rc;
+    }
+    {
+      const Split s = jcol_split(g);
+      JCombArgs a;
+      memset(&a, 0, sizeof(a));
+      a.P = saved + jl.p_off[l - 1];
+      a.U = (const float*)(saved + jl.u_off[l - 1]);
+      a.raw = (const float*)(ws + jl.raw_off);
+      a.D = ws + jl.d_off[cur ^ 1];
+      a.N = g.rows;
+      a.rows_per_split = s.rows_per_split;
+      a.C = jl.C;
+      a.F = N;
+      a.Su = jl.Su;
+      a.top = 0;
+      a.w0 = d->w0;
+      hipLaunchKernelGGL(jvp_combine_kernel<PREC>, dim3((unsigned)s.nsplit, (unsigned)g.nb), dim3(256), 0, st, a);
+      if ((rc = check_launch("jvp_combine"))) return rc;
+      cur ^= 1;
+    }
+  }
+  {
+    const Split s = jcol_split(g);
+    JFirstBwdArgs a;
+    a.D = ws + jl.d_off[cur];
+    a.x = x;
+    a.W = d->weight[0];
+    a.dx = dx;
+    a.part = part;
+    a.N = g.rows;
+    a.rows_per_split = s.rows_per_split;
+    a.C = d->dims[0];
+    a.F = d->dims[1];
+    a.split_stride = split_stride(g, (int64_t)a.F * a.C + a.F);
+    a.w_bstride = d->weights_batched ? (int64_t)d->dims[1] * d->dims[0] : 0;
+    hipLaunchKernelGGL(jvp_first_bwd_kernel<PREC>, dim3((unsigned)s.nsplit, (unsigned)g.nb), dim3(256), 0, st, a);
+    if ((rc = check_launch("jvp_first_bwd"))) return rc;
+    if ((rc = launch_reduce(part, s.nsplit, a.split_stride, g.nb, (int64_t)a.F * a.C + a.F,
+                            (int64_t)a.F * a.C, dW[0], db[0], st)))
+      return rc;
+    if (dx) {
+      hipLaunchKernelGGL(jvp_first_dx_kernel<PREC>, dim3((unsigned)std::min<int64_t>(cdiv(g.rows, 8), 4096 / g.nb + 1), (unsigned)g.nb),
+                         dim3(256), 0, st, a);
+      if ((rc = check_launch("jvp_first_dx"))) return rc;
+    }
+  }
+  return SIREN_OK;
+}
+
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 }  // namespace
@@ -545,6 +816,58 @@ int siren_mlp_backward(const siren_mlp_desc* d, const float* x, const float* dy,
                                     dx, st);
   return backward_impl<kPrecF32>(d, x, dy, (const char*)saved, (char*)workspace, dweight, dbias, dx,
                                  st);
+}
+
+int64_t siren_jvp_saved_bytes(const siren_mlp_desc* d, int order) {
+  if (jvp_check(d, order)) return -1;
+  return jlayout_of(d, order).saved_bytes;
+}
+
+int64_t siren_jvp_workspace_bytes(const siren_mlp_desc* d, int order) {
+  if (jvp_check(d, order)) return -1;
+  const JLayout jl = jlayout_of(d, order);
+  return jl.ws_bytes + jl.saved_bytes;  // room for the per-layer tensors when no saved buffer is given
+}
+
+int siren_jvp_forward(const siren_mlp_desc* d, int order, const float* x, float* grad, float* lap,
+                      void* saved, int64_t saved_bytes, void* workspace, int64_t workspace_bytes,
+                      void* stream) {
+  int rc = jvp_check(d, order);
+  if (rc) return rc;
+  const JLayout jl = jlayout_of(d, order);
+  if (saved && saved_bytes < jl.saved_bytes)
+    return fail(SIREN_ENOSPACE, "saved buffer %lld < %lld bytes", (long long)saved_bytes, (long long)jl.saved_bytes);
+  const int64_t need = saved ? jl.ws_bytes : jl.ws_bytes + jl.saved_bytes;
+  if (!workspace || workspace_bytes < need)
+    return fail(SIREN_ENOSPACE, "workspace %lld < %lld bytes", (long long)workspace_bytes, (long long)need);
+  if (!x || !grad || (order >= 2 && !lap)) return fail(SIREN_EINVAL, "null x/grad/lap");
+  g_err.clear();
+  hipStream_t st = (hipStream_t)stream;
+  if (d->prec == SIREN_PREC_BF16)
+    return jvp_forward_impl<kPrecBF16>(d, order, x, grad, lap, (char*)saved, (char*)workspace, st);
+  return jvp_forward_impl<kPrecF32>(d, order, x, grad, lap, (char*)saved, (char*)workspace, st);
+}
+
+int siren_jvp_backward(const siren_mlp_desc* d, int order, const float* x, const float* dgrad,
+                       const void* saved, int64_t saved_bytes, void* workspace, int64_t workspace_bytes,
+                       float* const* dweight, float* const* dbias, float* dx, void* stream) {
+  int rc = jvp_check(d, order);
+  if (rc) return rc;
+  if (order != 1)
+    return fail(SIREN_EINVAL, "backward through the analytic Laplacian is not implemented (order 2)");
+  const JLayout jl = jlayout_of(d, order);
+  if (!saved || saved_bytes < jl.saved_bytes)
+    return fail(SIREN_ENOSPACE, "saved buffer %lld < %lld bytes", (long long)saved_bytes, (long long)jl.saved_bytes);
+  if (!workspace || workspace_bytes < jl.ws_bytes)
+    return fail(SIREN_ENOSPACE, "workspace %lld < %lld bytes", (long long)workspace_bytes, (long long)jl.ws_bytes);
+  if (!x || !dgrad || !dweight || !dbias) return fail(SIREN_EINVAL, "null argument");
+  for (int l = 0; l < d->num_layers; ++l)
+    if (!dweight[l] || !dbias[l]) return fail(SIREN_EINVAL, "layer %d: null gradient output", l);
+  g_err.clear();
+  hipStream_t st = (hipStream_t)stream;
+  if (d->prec == SIREN_PREC_BF16)
+    return jvp_backward_impl<kPrecBF16>(d, x, dgrad, (const char*)saved, (char*)workspace, dweight, dbias, dx, st);
+  return jvp_backward_impl<kPrecF32>(d, x, dgrad, (const char*)saved, (char*)workspace, dweight, dbias, dx, st);
 }
 
 const char* siren_last_error(void) { return g_err.c_str(); }

@@ -1,0 +1,115 @@
+"""GPU: analytic SIREN derivatives (tangent-stream kernels) vs the oracle's autograd in float64.
+
+  gradient  == diff_operators.gradient (diff_operators.py:39-43)
+  laplace   == diff_operators.laplace  (diff_operators.py:27-36)
+  backward of gradients_mse == the reference's double backward (loss_functions.py:330-335)
+Tolerance (fp32 path): 1e-5 norm-relative for values, 1e-4 for parameter gradients of the
+gradient loss (second-order adjoints through 2^10..2^12 rows). bf16 path: 5e-2.
+Also: 10 Adam steps of gradients_mse with the reference's own trajectory (train_c3.npz).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import siren_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _model(hidden, nh, seed, precision, out=1, inp=2):
+    from siren_mri_amd import modules
+    torch.manual_seed(seed)
+    return modules.SingleBVPNet(out_features=out, in_features=inp, type="sine", hidden_features=hidden,
+                                num_hidden_layers=nh, precision=precision).to(DEV)
+
+
+def _oracle_params(m):
+    sd = m.state_dict()
+    L = len(m.net.net)
+    return [(sd[f"net.net.{i}.0.weight"].double().cpu().clone().requires_grad_(True),
+             sd[f"net.net.{i}.0.bias"].double().cpu().clone().requires_grad_(True)) for i in range(L)]
+
+
+TOL = {"fp32": (1e-5, 1e-4), "bf16": (5e-2, 8e-2)}
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("side,hidden,nh,out", [(16, 64, 2, 1), (32, 256, 3, 1), (20, 128, 1, 2)])
+def test_gradient_and_laplace_forward(precision, side, hidden, nh, out):
+    from siren_mri_amd import diff_operators
+    m = _model(hidden, nh, side, precision, out=out)
+    coords = orc.get_mgrid(side)[None]
+    o = m({"coords": coords.to(DEV)})
+    g = diff_operators.gradient(o["model_out"], o["model_in"])
+    lap = diff_operators.laplace(o["model_out"], o["model_in"])
+    ps = _oracle_params(m)
+    x = coords.double().clone().requires_grad_(True)
+    y = orc.siren_forward(x, ps)
+    g_ref = orc.gradient(y, x)
+    lap_ref = orc.laplace(y, x)
+    tv, _ = TOL[precision]
+    assert g.shape == x.shape and lap.shape == y.shape[:-1] + (1,)
+    assert orc.norm_rel(g.detach().cpu(), g_ref.detach()) < tv
+    assert orc.norm_rel(lap.detach().cpu(), lap_ref.detach()) < max(tv, 1e-5) * 4
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_gradients_mse_double_backward(precision):
+    from siren_mri_amd import loss_functions
+    side, hidden, nh = 24, 64, 2
+    m = _model(hidden, nh, 3, precision)
+    coords = orc.get_mgrid(side)[None]
+    gt = torch.randn(1, side * side, 2, generator=torch.Generator().manual_seed(2))
+    o = m({"coords": coords.to(DEV)})
+    loss = loss_functions.gradients_mse(o, {"gradients": gt.to(DEV)})["gradients_loss"]
+    loss.backward()
+    ps = _oracle_params(m)
+    x = coords.double().clone().requires_grad_(True)
+    out = {"model_in": x, "model_out": orc.siren_forward(x, ps)}
+    ref = orc.gradients_mse(out, {"gradients": gt.double()})["gradients_loss"]
+    ref.backward()
+    tv, tg = TOL[precision]
+    assert loss.item() == pytest.approx(ref.item(), rel=tv)
+    for i, (W, b) in enumerate(ps):
+        lw = m.net.net[i][0]
+        assert orc.norm_rel(lw.weight.grad.cpu(), W.grad) < tg, f"layer {i} dW"
+        assert orc.norm_rel(lw.bias.grad.cpu(), b.grad) < tg, f"layer {i} db"
+
+
+def test_batched_weights_gradient():
+    """Hypernetwork-style per-sample weights through the analytic gradient."""
+    from siren_mri_amd import diff_operators
+    m = _model(64, 1, 5, "fp32")
+    B = 3
+    params = {k: torch.stack([v * (1 + 0.05 * i) for i in range(B)]) for k, v in m.state_dict().items()}
+    coords = orc.get_mgrid(12)[None].repeat(B, 1, 1)
+    o = m({"coords": coords.to(DEV)}, params=params)
+    g = diff_operators.gradient(o["model_out"], o["model_in"])
+    for bi in range(B):
+        ps = [(params[f"net.net.{i}.0.weight"][bi].double().cpu(), params[f"net.net.{i}.0.bias"][bi].double().cpu())
+              for i in range(3)]
+        x = coords[bi:bi + 1].double().clone().requires_grad_(True)
+        ref = orc.gradient(orc.siren_forward(x, ps), x)
+        assert orc.norm_rel(g[bi:bi + 1].detach().cpu(), ref.detach()) < 1e-5
+
+
+def test_gradient_loss_training_matches_reference(tmp_path):
+    """training.train + gradients_mse (config 3 analogue, 32^2) vs the reference loop's losses."""
+    from siren_mri_amd import dataio, loss_functions, modules, training
+    d = np.load(os.path.join(G, "train_c3.npz"), allow_pickle=False)
+    m = modules.SingleBVPNet(type="sine", hidden_features=64, num_hidden_layers=2, precision="fp32")
+    m.load_state_dict({k[len("init/"):]: torch.from_numpy(d[k]) for k in d.files if k.startswith("init/")})
+    m = m.to(DEV)
+    loader = [({"coords": dataio.get_mgrid(32)[None]}, {"gradients": torch.from_numpy(d["gradients"])})]
+    training.train(m, loader, epochs=10, lr=1e-4, steps_til_summary=1000, epochs_til_checkpoint=1000,
+                   model_dir=str(tmp_path / "run"), loss_fn=loss_functions.gradients_mse,
+                   summary_fn=lambda *a, **k: None)
+    losses = np.loadtxt(tmp_path / "run" / "checkpoints" / "train_losses_final.txt")
+    np.testing.assert_allclose(losses, d["losses"], rtol=1e-4)
+    sd = m.state_dict()
+    for k in sd:
+        assert orc.norm_rel(sd[k].cpu(), torch.from_numpy(d["final/" + k])) < 1e-4, k
