@@ -80,6 +80,8 @@ class _SirenJVP(torch.autograd.Function):
         if geo.squeeze_w:
             dW = [g.unsqueeze(0) for g in dW]
             db = [g.unsqueeze(0) for g in db]
+        # the output bias does not reach dy/dx: autograd leaves its .grad as None in the reference
+        db[-1] = None
         return (None, dx, *dW, *db)
 
 
