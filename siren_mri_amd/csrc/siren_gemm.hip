@@ -2,7 +2,10 @@
 //
 //   nt_gemm   MODE_FWD: P_l = enc(w0 * (sin(P_{l-1}) W_l^T + b_l))          (modules.py:25-26,38)
 //             MODE_DX : dZ_{l-1} = (dZ_l W_l) * cos(P_{l-1}) * w0            (autograd Mm/Sin/Mul bwd)
-//   tn_dw     partial dW_l = dZ_l^T sin(P_{l-1}), db_l = sum dZ_l          (split-K over rows)
+//             MODE_FIRST: P_0 = enc(w0 * (x W_0^T + b_0)) for wide inputs (in_features > 16, e.g. the
+//                         Fourier-feature coordinates of the hypernetwork SIREN, meta_modules.py:205-213)
+//             MODE_DXLIN: dx = dZ_0 W_0 (fp32, no activation) for wide inputs
+//   tn_dw     partial dW_l = dZ_l^T sin(P_{l-1}) (or dZ_0^T x), db_l = sum dZ_l   (split-K over rows)
 //
 // nt_gemm structure (one launch per layer, persistent workgroups):
 //   * 8 waves; wave w owns output columns [32w, 32w+32) and keeps that slice of W (its MFMA B
@@ -19,30 +22,39 @@ namespace siren {
 
 constexpr int MODE_FWD = 0;
 constexpr int MODE_DX = 1;
+constexpr int MODE_FIRST = 2;
+constexpr int MODE_DXLIN = 3;
 
 struct NTArgs {
-  const void* A;       // [rows, K] phase_t (FWD) or grad_t (DX)
-  const void* W;       // [nb_w][N, K] op_t   (FWD: W_l ; DX: W_l^T)
+  const void* A;       // [rows, lda] phase_t (FWD), grad_t (DX, DXLIN) or f32 (FIRST)
+  const void* W;       // [nb_w][N, K] op_t   (FWD: W_l ; DX: W_l^T ; FIRST: W_0 zero-padded to K)
   const float* bias;   // [nb_w][N] (FWD only)
   const void* Paux;    // [rows, N] phase_t (DX: P_{l-1})
-  void* C;             // [rows, N] phase_t (FWD) or grad_t (DX)
+  void* C;             // [rows, N] phase_t (FWD, FIRST), grad_t (DX) or f32 (DXLIN)
   int64_t rows_per_batch;
   int64_t w_bstride;     // elements between weight sets (0 = shared)
   int64_t bias_bstride;  // elements between bias sets (0 = shared)
   int K;
   int N;
+  int lda;             // FIRST: row stride of x (= in_features <= K); otherwise K
+  int a_vec;           // FIRST: x rows are 16-byte aligned (lda % 4 == 0, aligned base)
   float w0;
 };
 
+// Largest power-of-two divisor of the 16-byte chunks per row, capped at 16, minus one: the XOR
+// swizzle c ^ (r & smask) then stays inside the row for every K that is a multiple of 16.
+DEV int swizzle_mask(int chunks) { return min(16, chunks & -chunks) - 1; }
+
 struct TNArgs {
   const void* D;       // [rows, M] grad_t  (dZ_l)
-  const void* P;       // [rows, N] phase_t (P_{l-1})
+  const void* P;       // [rows, N] phase_t (P_{l-1}), or f32 x for the wide first layer
   float* part;         // split s, batch b slab at part + s*split_stride + b*(M*N + M)  (dW then db)
   int64_t rows_per_batch;
   int64_t rows_per_split;
   int64_t split_stride;
   int M;
   int N;
+  int p_vec;           // RAW: x rows are 16-byte aligned (N % 4 == 0, aligned base)
 };
 
 // ------------------------------------------------------------------------------------------
@@ -84,8 +96,9 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
   const int64_t ntiles = (rows + BM - 1) / BM;
   const int col_l = 32 * wave + r32;
   const bool col_ok = col_l < ncols;
+  const bool wave_on = 32 * wave < ncols;
   const int a_cpr = K >> 3;                 // 16-byte chunks per A row
-  const int smask = min(16, a_cpr) - 1;     // swizzle mask
+  const int smask = swizzle_mask(a_cpr);
   const int c_cpr = ncols >> 3;             // 16-byte chunks per C row
   const int nks = K >> 4;
 
@@ -99,23 +112,37 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) wf[ks][e] = (bf16)0.f;
   }
+  constexpr bool FWDLIKE = MODE == MODE_FWD || MODE == MODE_FIRST;
   float bcol = 0.f;
-  if constexpr (MODE == MODE_FWD) bcol = col_ok ? a.bias[batch * a.bias_bstride + n0 + col_l] : 0.f;
+  if constexpr (FWDLIKE) bcol = col_ok ? a.bias[batch * a.bias_bstride + n0 + col_l] : 0.f;
 
   auto a_off = [&](int r, int c) -> int { return r * K * 2 + ((c ^ (r & smask)) << 4); };
 
   // ---- staging ----
   u16x8 areg[4];  // FWD: next tile's phases (register staged: the sin transform happens on write)
+  f32x4 xreg[4][2];  // FIRST: next tile's raw inputs
   auto fwd_load = [&](int64_t t) {
     const int64_t m0 = t * BM;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int u = tid + 512 * q;
       const int r = u / a_cpr, c = u - r * a_cpr;
-      if (r < BM && m0 + r < rows)
-        areg[q] = *(const u16x8*)((const uint16_t*)a.A + (rowbase + m0 + r) * K + c * 8);
-      else
-        areg[q] = u16x8{};
+      const bool in = r < BM && m0 + r < rows;
+      if constexpr (MODE == MODE_FIRST) {
+        const float* src = (const float*)a.A + (rowbase + m0 + r) * a.lda + c * 8;
+        if (in && a.a_vec && c * 8 + 8 <= a.lda) {
+          xreg[q][0] = *(const f32x4*)src;
+          xreg[q][1] = *(const f32x4*)(src + 4);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xreg[q][e >> 2][e & 3] = (in && c * 8 + e < a.lda) ? src[e] : 0.f;
+        }
+      } else {
+        if (in)
+          areg[q] = *(const u16x8*)((const uint16_t*)a.A + (rowbase + m0 + r) * K + c * 8);
+        else
+          areg[q] = u16x8{};
+      }
     }
   };
   auto fwd_store = [&](int buf) {
@@ -125,8 +152,13 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
       const int r = u / a_cpr, c = u - r * a_cpr;
       if (r < BM) {
         bf16x8 v;
+        if constexpr (MODE == MODE_FIRST) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (bf16)PT::sinp(areg[q][e]);
+          for (int e = 0; e < 8; ++e) v[e] = (bf16)xreg[q][e >> 2][e & 3];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = (bf16)PT::sinp(areg[q][e]);
+        }
         *(bf16x8*)(Abase + buf * A_BYTES + a_off(r, c)) = v;
       }
     }
@@ -143,6 +175,7 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
       __builtin_amdgcn_global_load_lds((const void*)((const bf16*)a.A + (rowbase + row) * K + c * 8),
                                        (lds_void*)(Abase + buf * A_BYTES + i * 1024), 16, 0, 0);
     }
+    if constexpr (MODE == MODE_DX)
     for (int i = wave; i < n_p; i += 8) {
       const int u = i * 64 + lane;
       const int r = u / c_cpr, c = u - r * c_cpr;
@@ -154,7 +187,7 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
 
   int64_t t = blockIdx.x;
   if (t >= ntiles) return;
-  if constexpr (MODE == MODE_FWD) {
+  if constexpr (FWDLIKE) {
     fwd_load(t);
     fwd_store(0);
   } else {
@@ -167,7 +200,7 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
     const int64_t tn = t + gridDim.x;
     const bool has_next = tn < ntiles;
     if (has_next) {
-      if constexpr (MODE == MODE_FWD) fwd_load(tn);
+      if constexpr (FWDLIKE) fwd_load(tn);
       else dx_dma(tn, cur ^ 1);
     }
     f32x16 acc[BM / 32];
@@ -175,7 +208,9 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
     for (int bm = 0; bm < BM / 32; ++bm)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[bm][e] = 0.f;
-    if (col_ok) {
+    // MFMA operands come from every lane: the compute guard must be wave-uniform (a wave with a
+    // partial column slice computes with zero W rows and masks its stores below).
+    if (wave_on) {
       const char* As = Abase + cur * A_BYTES;
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
@@ -190,23 +225,26 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
       // epilogue 1: accumulators -> LDS C tile (in place over the staged P tile for DX)
       uint16_t* Cs = (uint16_t*)(Cbase + cur * C_BYTES);
 #pragma unroll
-      for (int bm = 0; bm < BM / 32; ++bm)
+      for (int bm = 0; bm < BM / 32 && col_ok; ++bm)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int rl = 32 * bm + (e & 3) + 8 * (e >> 2) + 4 * h;
           uint16_t* dst = Cs + rl * ncols + col_l;
-          if constexpr (MODE == MODE_FWD) {
+          if constexpr (FWDLIKE) {
             *dst = PT::enc(a.w0 * (acc[bm][e] + bcol));
+          } else if constexpr (MODE == MODE_DXLIN) {
+            const int64_t row = t * BM + rl;
+            if (row < rows) ((float*)a.C)[(rowbase + row) * N + n0 + col_l] = acc[bm][e];
           } else {
             const float c = PT::cosp(*dst);
             *dst = __builtin_bit_cast(uint16_t, (bf16)((acc[bm][e] * c) * a.w0));
           }
         }
     }
-    if constexpr (MODE == MODE_DX) vm_drain();  // next tile's DMA has landed (this wave's part)
+    if constexpr (MODE == MODE_DX || MODE == MODE_DXLIN) vm_drain();  // next tile's DMA has landed
     lds_barrier();
     // epilogue 2: coalesced 16-byte stores of the finished tile
-    {
+    if constexpr (MODE != MODE_DXLIN) {
       const int64_t m0 = t * BM;
       const int nch = BM * c_cpr;
       for (int u = tid; u < nch; u += 512) {
@@ -216,7 +254,7 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
               *(const u16x8*)(Cbase + cur * C_BYTES + (r * ncols + c * 8) * 2);
       }
     }
-    if constexpr (MODE == MODE_FWD) {
+    if constexpr (FWDLIKE) {
       if (has_next) fwd_store(cur ^ 1);
     }
     lds_barrier();
@@ -253,6 +291,7 @@ __global__ __launch_bounds__(512) void nt_f32_kernel(NTArgs a) {
   const int64_t ntiles = (rows + BM - 1) / BM;
   const int col_l = 32 * wave + r32;
   const bool col_ok = col_l < ncols;
+  const bool wave_on = 32 * wave < ncols;
   const int nks = K >> 1;
   const int a_cpr = K >> 2, c_cpr = ncols >> 2;
 
@@ -260,8 +299,9 @@ __global__ __launch_bounds__(512) void nt_f32_kernel(NTArgs a) {
   float wf[NKS];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) wf[ks] = (ks < nks && col_ok) ? Wb[2 * ks + h] : 0.f;
+  constexpr bool FWDLIKE = MODE == MODE_FWD || MODE == MODE_FIRST;
   float bcol = 0.f;
-  if constexpr (MODE == MODE_FWD) bcol = col_ok ? a.bias[batch * a.bias_bstride + n0 + col_l] : 0.f;
+  if constexpr (FWDLIKE) bcol = col_ok ? a.bias[batch * a.bias_bstride + n0 + col_l] : 0.f;
 
   f32x4 areg[4], preg[4];
   auto load_tile = [&](int64_t t) {
@@ -270,8 +310,19 @@ __global__ __launch_bounds__(512) void nt_f32_kernel(NTArgs a) {
     for (int q = 0; q < 4; ++q) {
       const int u = tid + 512 * q;
       const int r = u / a_cpr, c = u - r * a_cpr;
-      areg[q] = (r < BM && m0 + r < rows) ? *(const f32x4*)((const float*)a.A + (rowbase + m0 + r) * K + c * 4)
-                                          : f32x4{0.f, 0.f, 0.f, 0.f};
+      const bool in = r < BM && m0 + r < rows;
+      if constexpr (MODE == MODE_FIRST) {
+        const float* src = (const float*)a.A + (rowbase + m0 + r) * a.lda + c * 4;
+        if (in && a.a_vec && c * 4 + 4 <= a.lda) {
+          areg[q] = *(const f32x4*)src;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) areg[q][e] = (in && c * 4 + e < a.lda) ? src[e] : 0.f;
+        }
+      } else {
+        areg[q] = in ? *(const f32x4*)((const float*)a.A + (rowbase + m0 + r) * K + c * 4)
+                     : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
       if constexpr (MODE == MODE_DX) {
         const int rp = u / c_cpr, cp = u - rp * c_cpr;
         preg[q] = (rp < BM && m0 + rp < rows)
@@ -310,22 +361,28 @@ __global__ __launch_bounds__(512) void nt_f32_kernel(NTArgs a) {
     f32x16 acc;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-    if (col_ok) {
+    if (wave_on) {
       const float* As = As0 + cur * (A_BYTES / 4);
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks)
         if (ks < nks) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[r32 * AROW + 2 * ks + h], wf[ks], acc, 0, 0, 0);
       float* Cs = (float*)(Cs0 + cur * C_BYTES);
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
+      for (int e = 0; e < 16 && col_ok; ++e) {
         const int rl = (e & 3) + 8 * (e >> 2) + 4 * h;
         float* dst = Cs + rl * ncols + col_l;
-        if constexpr (MODE == MODE_FWD) *dst = PT::enc(a.w0 * (acc[e] + bcol));
-        else *dst = (acc[e] * PT::cosp(*dst)) * a.w0;
+        if constexpr (FWDLIKE) {
+          *dst = PT::enc(a.w0 * (acc[e] + bcol));
+        } else if constexpr (MODE == MODE_DXLIN) {
+          const int64_t row = t * BM + rl;
+          if (row < rows) ((float*)a.C)[(rowbase + row) * N + n0 + col_l] = acc[e];
+        } else {
+          *dst = (acc[e] * PT::cosp(*dst)) * a.w0;
+        }
       }
     }
     __syncthreads();
-    {
+    if constexpr (MODE != MODE_DXLIN) {
       const int64_t m0 = t * BM;
       const int nch = BM * c_cpr;
       for (int u = tid; u < nch; u += 512) {
@@ -356,7 +413,7 @@ template <> struct TNLds<kPrecF32> {
   static constexpr int BYTES = 2 * KC * ROW * 4;
 };
 
-template <int PREC>
+template <int PREC, bool RAW>
 __global__ __launch_bounds__(256) void tn_dw_kernel(TNArgs a) {
   using PT = Prec<PREC>;
   using phase_t = typename PT::phase_t;
@@ -402,6 +459,7 @@ __global__ __launch_bounds__(256) void tn_dw_kernel(TNArgs a) {
   using p_in_t = typename std::conditional<PREC == kPrecBF16, u16x8, f32x4>::type;
   d_in_t dreg[UPT];
   p_in_t preg[UPT];
+  float xr[UPT][VEC];  // RAW: fp32 inputs of the wide first layer
   const int cu = tid % UPR;  // this thread's column unit (fixed across chunks)
 
   auto load = [&](int64_t rc) {
@@ -416,7 +474,21 @@ __global__ __launch_bounds__(256) void tn_dw_kernel(TNArgs a) {
 #pragma unroll
         for (int e = 0; e < VEC; ++e) dreg[q][e] = 0;
       }
-      if (row < r_end && cj < a.N) {
+      if constexpr (RAW) {
+        const float* src = (const float*)a.P + (rowbase + row) * a.N + cj;
+        const bool in = row < r_end && cj < a.N;
+        if (in && a.p_vec && cj + VEC <= a.N) {
+#pragma unroll
+          for (int v = 0; v < VEC / 4; ++v) {
+            const f32x4 t4 = *(const f32x4*)(src + 4 * v);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) xr[q][4 * v + e] = t4[e];
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) xr[q][e] = (in && cj + e < a.N) ? src[e] : 0.f;
+        }
+      } else if (row < r_end && cj < a.N) {
         preg[q] = *(const p_in_t*)((const phase_t*)a.P + (rowbase + row) * a.N + cj);
       } else {
 #pragma unroll
@@ -435,7 +507,12 @@ __global__ __launch_bounds__(256) void tn_dw_kernel(TNArgs a) {
       for (int e = 0; e < VEC; ++e) dbacc[e] += to_f32(dv[e]);
       d_in_t hv;
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) hv[e] = from_f32<op_t>(valid ? PT::sinp(preg[q][e]) : 0.f);
+      for (int e = 0; e < VEC; ++e) {
+        float v = 0.f;
+        if constexpr (RAW) v = xr[q][e];
+        else v = PT::sinp(preg[q][e]);
+        hv[e] = from_f32<op_t>(valid ? v : 0.f);
+      }
       *(d_in_t*)(Hs + r * ROW + cu * VEC) = hv;
     }
   };

@@ -62,6 +62,15 @@ Geo geo_of(const siren_mlp_desc* d) {
   return g;
 }
 
+// Wide inputs (in_features > 16: Fourier-feature coordinates) run layer 0 on the MFMA GEMM path;
+// its prepared weights are zero-padded along K to a whole number of MFMA K-steps (16 bf16 / 4 f32).
+constexpr int kValuMaxIn = 16;
+inline bool wide_input(const siren_mlp_desc* d) { return d->dims[0] > kValuMaxIn; }
+inline int first_kp(const siren_mlp_desc* d) {
+  return (int)align_up(d->dims[0], d->prec == SIREN_PREC_BF16 ? 16 : 4);
+}
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
 int max_hidden(const siren_mlp_desc* d) {
   int m = 0;
   for (int l = 1; l < d->num_layers; ++l) m = std::max(m, d->dims[l]);
@@ -111,6 +120,13 @@ Layout layout_of(const siren_mlp_desc* d) {
   memset(&lo, 0, sizeof(lo));
   // saved = [prepared MFMA weights][one phase tensor per sine layer 0..L-2]
   int64_t off = 0;
+  for (int l = 0; l < SIREN_MAX_LAYERS; ++l) lo.w_op_off[l] = lo.wt_op_off[l] = -1;
+  if (wide_input(d)) {
+    lo.w_op_off[0] = off;
+    off = align_up(off + g.nb * (int64_t)d->dims[1] * first_kp(d) * g.op_sz, 256);
+    lo.wt_op_off[0] = off;
+    off = align_up(off + g.nb * (int64_t)d->dims[1] * d->dims[0] * g.op_sz, 256);
+  }
   for (int l = 1; l + 1 < g.L; ++l) {
     const int64_t n = g.nb * (int64_t)d->dims[l + 1] * d->dims[l];
     if (g.prec == SIREN_PREC_BF16) {
@@ -151,7 +167,8 @@ Layout layout_of(const siren_mlp_desc* d) {
     const int F = d->dims[g.L - 1], O = d->dims[g.L];
     part = std::max(part, s.nsplit * split_stride(g, (int64_t)O * F + O));
     const int F0 = d->dims[1], C = d->dims[0];
-    part = std::max(part, s.nsplit * split_stride(g, (int64_t)F0 * C + F0));
+    const Split s0 = wide_input(d) ? tn_split(g, F0, C) : s;
+    part = std::max(part, s0.nsplit * split_stride(g, (int64_t)F0 * C + F0));
   }
   lo.part_off = off;
   off = align_up(off + part * 4, 256);
@@ -201,21 +218,22 @@ int launch_reduce(const float* part, int64_t nsplit, int64_t sstride, int64_t nb
 // Convert every MFMA layer's weights (bf16 copy + transpose) into `dst` in one launch.
 template <int PREC>
 int prep_weights(const siren_mlp_desc* d, const Geo& g, const Layout& lo, char* dst, hipStream_t st) {
-  if (g.L < 3) return SIREN_OK;
   PrepArgs pa;
   memset(&pa, 0, sizeof(pa));
   int64_t maxn = 0;
-  for (int l = 1; l + 1 < g.L; ++l) {
-    const int k = l - 1;
+  int k = 0;
+  for (int l = wide_input(d) ? 0 : 1; l + 1 < g.L; ++l, ++k) {
     pa.W[k] = d->weight[l];
     pa.Wop[k] = lo.w_op_off[l] >= 0 ? dst + lo.w_op_off[l] : nullptr;
     pa.Wt[k] = dst + lo.wt_op_off[l];
     pa.O[k] = d->dims[l + 1];
     pa.I[k] = d->dims[l];
-    maxn = std::max(maxn, (int64_t)pa.O[k] * pa.I[k]);
+    pa.Kp[k] = l == 0 ? first_kp(d) : d->dims[l];
+    maxn = std::max(maxn, (int64_t)pa.O[k] * pa.Kp[k]);
   }
+  if (k == 0) return SIREN_OK;
   pa.nb = g.nb;
-  hipLaunchKernelGGL(prep_weights_kernel<PREC>, dim3(grid1d(g.nb * maxn, 512), (unsigned)(g.L - 2)),
+  hipLaunchKernelGGL(prep_weights_kernel<PREC>, dim3(grid1d(g.nb * maxn, 512), (unsigned)k),
                      dim3(256), 0, st, pa);
   return check_launch("prep_weights");
 }
@@ -278,7 +296,7 @@ int dispatch_first_bwd(const FirstBwdArgs& a, int64_t nsplit, int64_t nb, hipStr
 template <int PREC, int MODE>
 int launch_nt(const NTArgs& a, int64_t nb, int kclass, hipStream_t st) {
   const int ntn = (int)cdiv(a.N, 256);
-  const int kmax = a.K <= 256 ? 256 : 512;
+  const int kmax = a.K <= 256 ? 256 : 512;  // siren_mlp_check bounds K by 512 (bf16) / 256 (f32)
   const int bm = PREC == kPrecBF16 ? 64 * 256 / kmax : 32;
   const int64_t tiles = cdiv(a.rows_per_batch, bm);
   const int64_t per = std::max<int64_t>(1, 256 / std::max<int64_t>(1, nb * ntn));
@@ -291,7 +309,8 @@ int launch_nt(const NTArgs& a, int64_t nb, int kclass, hipStream_t st) {
     hipLaunchKernelGGL((nt_f32_kernel<MODE>), grid, dim3(512), 0, st, a);
   }
   tmark_end(kclass, st);
-  return check_launch(MODE == MODE_FWD ? "nt_gemm fwd" : "nt_gemm dx");
+  static const char* const names[] = {"nt_gemm fwd", "nt_gemm dx", "nt_gemm first", "nt_gemm dx-input"};
+  return check_launch(names[MODE]);
 }
 
 template <int PREC>
@@ -305,8 +324,24 @@ int forward_impl(const siren_mlp_desc* d, const float* x, float* y, char* saved,
   auto phase_buf = [&](int l) -> char* {
     return saved ? saved + lo.saved_off[l] : ws + lo.pp_off[l & 1];
   };
-  // Layer 0 (VALU).
-  {
+  // Layer 0: MFMA GEMM for wide inputs, VALU otherwise.
+  if (wide_input(d)) {
+    NTArgs a;
+    a.A = x;
+    a.W = wbuf + lo.w_op_off[0];
+    a.bias = d->bias[0];
+    a.Paux = nullptr;
+    a.C = phase_buf(0);
+    a.rows_per_batch = g.rows;
+    a.w_bstride = d->weights_batched ? (int64_t)d->dims[1] * first_kp(d) : 0;
+    a.bias_bstride = d->weights_batched ? d->dims[1] : 0;
+    a.K = first_kp(d);
+    a.N = d->dims[1];
+    a.lda = d->dims[0];
+    a.a_vec = (d->dims[0] % 4 == 0) && aligned16(x);
+    a.w0 = d->w0;
+    if ((rc = launch_nt<PREC, MODE_FIRST>(a, g.nb, 0, st))) return rc;
+  } else {
     FirstFwdArgs a;
     a.x = x;
     a.W = d->weight[0];
@@ -338,6 +373,8 @@ int forward_impl(const siren_mlp_desc* d, const float* x, float* y, char* saved,
     a.bias_bstride = d->weights_batched ? d->dims[l + 1] : 0;
     a.K = d->dims[l];
     a.N = d->dims[l + 1];
+    a.lda = a.K;
+    a.a_vec = 0;
     a.w0 = d->w0;
     if ((rc = launch_nt<PREC, MODE_FWD>(a, g.nb, SIREN_KCLASS_FWD_GEMM, st))) return rc;
   }
@@ -409,9 +446,10 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
       a.split_stride = split_stride(g, (int64_t)M * N + M);
       a.M = M;
       a.N = N;
+      a.p_vec = 0;
       dim3 grid((unsigned)(cdiv(M, TN_BM) * cdiv(N, TN_BN)), (unsigned)s.nsplit, (unsigned)g.nb);
       tmark_begin(SIREN_KCLASS_DW_GEMM, st);
-      hipLaunchKernelGGL(tn_dw_kernel<PREC>, grid, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((tn_dw_kernel<PREC, false>), grid, dim3(256), 0, st, a);
       tmark_end(SIREN_KCLASS_DW_GEMM, st);
       if ((rc = check_launch("tn_dw"))) return rc;
       if ((rc = launch_reduce(part, s.nsplit, a.split_stride, g.nb, (int64_t)M * N + M,
@@ -430,13 +468,51 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
       a.bias_bstride = 0;
       a.K = M;
       a.N = N;
+      a.lda = M;
+      a.a_vec = 0;
       a.w0 = d->w0;
       if ((rc = launch_nt<PREC, MODE_DX>(a, g.nb, SIREN_KCLASS_DX_GEMM, st))) return rc;
       cur ^= 1;
     }
   }
   // First layer.
-  {
+  if (wide_input(d)) {
+    const int F0 = d->dims[1], C = d->dims[0];
+    const Split s = tn_split(g, F0, C);
+    TNArgs a;
+    a.D = ws + lo.dz_off[cur];
+    a.P = x;
+    a.part = part;
+    a.rows_per_batch = g.rows;
+    a.rows_per_split = s.rows_per_split;
+    a.split_stride = split_stride(g, (int64_t)F0 * C + F0);
+    a.M = F0;
+    a.N = C;
+    a.p_vec = (C % 4 == 0) && aligned16(x);
+    dim3 grid((unsigned)(cdiv(F0, TN_BM) * cdiv(C, TN_BN)), (unsigned)s.nsplit, (unsigned)g.nb);
+    hipLaunchKernelGGL((tn_dw_kernel<PREC, true>), grid, dim3(256), 0, st, a);
+    if ((rc = check_launch("tn_dw first"))) return rc;
+    if ((rc = launch_reduce(part, s.nsplit, a.split_stride, g.nb, (int64_t)F0 * C + F0,
+                            (int64_t)F0 * C, dW[0], db[0], st)))
+      return rc;
+    if (dx) {
+      NTArgs n;
+      n.A = ws + lo.dz_off[cur];
+      n.W = saved + lo.wt_op_off[0];
+      n.bias = nullptr;
+      n.Paux = nullptr;
+      n.C = dx;
+      n.rows_per_batch = g.rows;
+      n.w_bstride = d->weights_batched ? (int64_t)F0 * C : 0;
+      n.bias_bstride = 0;
+      n.K = F0;
+      n.N = C;
+      n.lda = F0;
+      n.a_vec = 0;
+      n.w0 = d->w0;
+      if ((rc = launch_nt<PREC, MODE_DXLIN>(n, g.nb, 0, st))) return rc;
+    }
+  } else {
     const Split s = valu_split(g);
     FirstBwdArgs a;
     a.dZ = ws + lo.dz_off[cur];
@@ -728,8 +804,6 @@ int jvp_backward_impl(const siren_mlp_desc* d, const float* x, const float* gbar
   return SIREN_OK;
 }
 
-bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
-
 }  // namespace
 
 extern "C" {
@@ -745,8 +819,10 @@ int siren_mlp_check(const siren_mlp_desc* d) {
     return fail(SIREN_EINVAL, "empty input (batch=%lld rows=%lld)", (long long)d->batch,
                 (long long)d->rows_per_batch);
   if (d->batch > 65535) return fail(SIREN_EINVAL, "batch %lld > 65535", (long long)d->batch);
-  if (d->dims[0] < 1 || d->dims[0] > 16)
-    return fail(SIREN_EINVAL, "in_features=%d unsupported (1..16)", d->dims[0]);
+  const int kmax = d->prec == SIREN_PREC_BF16 ? 512 : 256;  // MFMA K bound of the GEMM kernels
+  if (d->dims[0] < 1 || (wide_input(d) && first_kp(d) > kmax))
+    return fail(SIREN_EINVAL, "in_features=%d unsupported (1..%d for this precision)", d->dims[0],
+                d->prec == SIREN_PREC_BF16 ? 512 : 256);
   if (d->dims[L] < 1 || d->dims[L] > 8)
     return fail(SIREN_EINVAL, "out_features=%d unsupported (1..8)", d->dims[L]);
   const int hmax = d->prec == SIREN_PREC_BF16 ? 512 : 256;

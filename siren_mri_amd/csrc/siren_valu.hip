@@ -486,27 +486,33 @@ __global__ __launch_bounds__(256) void reduce_kernel(const float* part, int nspl
 // W [nb][O][I] fp32 -> Wop [nb][O][I] op_t (bf16 only) and WtOp [nb][I][O] op_t.
 struct PrepArgs {
   const float* W[16];
-  void* Wop[16];
-  void* Wt[16];
-  int O[16], I[16];
+  void* Wop[16];  // [nb][O, Kp] op_t, zero-padded along K (Kp >= I), or null
+  void* Wt[16];   // [nb][I, O] op_t
+  int O[16], I[16], Kp[16];
   int64_t nb;
 };
 
+// Every MFMA layer's operand copies in one launch (blockIdx.y = layer).
 template <int PREC>
 __global__ __launch_bounds__(256) void prep_weights_kernel(PrepArgs a) {
   using op_t = typename Prec<PREC>::op_t;
   const int l = blockIdx.y;
-  const int O = a.O[l], I = a.I[l];
+  const int O = a.O[l], I = a.I[l], Kp = a.Kp[l];
   const float* W = a.W[l];
   op_t* Wop = (op_t*)a.Wop[l];
   op_t* Wt = (op_t*)a.Wt[l];
   const int64_t per = (int64_t)O * I;
-  const int64_t total = a.nb * per;
+  const int64_t perp = (int64_t)O * Kp;
+  const int64_t total = a.nb * perp;
   for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
-    const int64_t b = idx / per;
-    const int rem = (int)(idx - b * per);
-    const int o = rem / I, i = rem - o * I;
-    const op_t v = from_f32<op_t>(W[idx]);
+    const int64_t b = idx / perp;
+    const int rem = (int)(idx - b * perp);
+    const int o = rem / Kp, i = rem - o * Kp;
+    if (i >= I) {
+      if (Wop) Wop[idx] = from_f32<op_t>(0.f);
+      continue;
+    }
+    const op_t v = from_f32<op_t>(W[b * per + (int64_t)o * I + i]);
     if (Wop) Wop[idx] = v;
     Wt[b * per + (int64_t)i * O + o] = v;
   }

@@ -31,11 +31,18 @@ def create_circular_mask_torch(h, w, center=None, radius=None):
     return (dist <= radius).long()
 
 
+def _host(a) -> np.ndarray:
+    if isinstance(a, torch.Tensor):
+        a = a.detach().cpu().double().numpy()
+    return np.asarray(a, dtype=np.float64)
+
+
 def psnr(pred_img, gt_img) -> float:
-    """PSNR of one image pair in the reference's [-1, 1] convention (utils.py:604-610)."""
-    p = np.asarray(pred_img, dtype=np.float64) / 2.0 + 0.5
+    """PSNR of one image pair in the reference's [-1, 1] convention (utils.py:604-610);
+    numpy arrays or tensors on any device."""
+    p = _host(pred_img) / 2.0 + 0.5
     p = np.clip(p, 0.0, 1.0)
-    t = np.asarray(gt_img, dtype=np.float64) / 2.0 + 0.5
+    t = _host(gt_img) / 2.0 + 0.5
     mse = float(np.mean((p - t) ** 2))
     return float("inf") if mse == 0 else float(10.0 * np.log10(1.0 / mse))
 

@@ -86,6 +86,76 @@ def test_batched_weights_hypernet_shape(precision):
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("dims", [[2, 96, 96, 1], [2, 160, 224, 96, 1], [3, 32, 480, 2]])
+def test_irregular_hidden_widths(precision, dims):
+    # widths that are multiples of 32 but not powers of two (LDS swizzle must stay inside a row)
+    if precision == "fp32" and max(dims[1:-1]) > 256:
+        pytest.skip("fp32 hidden widths are bounded by 256")
+    params = orc.siren_init(dims, seed=sum(dims))
+    x = torch.rand(1, 517, dims[0], generator=torch.Generator().manual_seed(2)) * 2 - 1
+    _check(x, params, precision)
+
+
+def _wide_params(dims, B, seed):
+    g = torch.Generator().manual_seed(seed)
+    params = []
+    for l in range(len(dims) - 1):
+        base = orc.siren_init(dims, seed=seed + l)[l]
+        if B is None:
+            params.append(base)
+            continue
+        W = base[0].unsqueeze(0).repeat(B, 1, 1) * (1 + 0.1 * torch.randn(B, 1, 1, generator=g))
+        b = base[1].unsqueeze(0).repeat(B, 1) + 0.01 * torch.randn(B, dims[l + 1], generator=g)
+        params.append((W.contiguous(), b.contiguous()))
+    return params
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("C", [20, 120, 122])
+def test_wide_input_first_layer(precision, C):
+    # in_features > 16 (Fourier-feature coordinates, configs 4/5: 2*60 = 120) run layer 0 on the
+    # MFMA GEMM path; C = 122 exercises the unaligned-row load path
+    dims = [C, 256, 256, 2]
+    params = _wide_params(dims, None, C)
+    g = torch.Generator().manual_seed(C)
+    x = torch.sin(torch.rand(1, 700, C, generator=g) * 6.28)
+    lw = torch.randn(1, 700, 2, generator=g)
+    _check(x, params, precision, loss_w=lw)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_wide_input_batched_config4_shape(precision):
+    # config 4's SIREN (in 120, 3 hidden x 256, out 2) with per-slice hypernetwork weights
+    B, N = 3, 333
+    dims = [120, 256, 256, 256, 256, 2]
+    params = _wide_params(dims, B, 11)
+    g = torch.Generator().manual_seed(4)
+    x = torch.sin(torch.rand(B, N, 120, generator=g) * 6.28)
+    lw = torch.randn(B, N, 2, generator=g)
+    _check(x, params, precision, loss_w=lw)
+
+
+def test_wide_input_config5_shape_bf16():
+    # config 5's SIREN widths (in 2*228 = 456, hidden 512, out 2), reduced depth and rows
+    B, N = 2, 130
+    dims = [456, 512, 512, 2]
+    params = _wide_params(dims, B, 5)
+    g = torch.Generator().manual_seed(5)
+    x = torch.sin(torch.rand(B, N, 456, generator=g) * 6.28)
+    _check(x, params, "bf16")
+
+
+def test_wide_input_fp32_bound():
+    from siren_mri_amd.ops import siren_mlp
+    from siren_mri_amd._native import NativeError
+    dims = [456, 256, 1]
+    params = orc.siren_init(dims, seed=1)
+    with pytest.raises(NativeError, match="in_features"):
+        siren_mlp(torch.zeros(1, 4, 456, device=DEV), [W.to(DEV) for W, _ in params],
+                  [b.to(DEV) for _, b in params], precision="fp32")
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_sine_output_layer(precision):
     dims = [3, 64, 64, 4]
     params = orc.siren_init(dims, seed=3)
