@@ -33,9 +33,10 @@ sys.path.insert(0, ROOT)
 
 PEAK = {"bf16": (2.5e15, "TFLOP/s"), "fp32": (157.3e12, "TFLOP/s")}
 HBM_PEAK = 8.0e12
-KCLASS_NAMES = {1: "nt_gemm_kernel<fwd> (hidden-layer forward GEMM + bias/w0/sin-phase epilogue)",
-                2: "nt_gemm_kernel<dx> (hidden-layer input-gradient GEMM + cos epilogue)",
-                3: "tn_dw_kernel (hidden-layer weight-gradient split-K GEMM)"}
+KCLASS_NAMES = {1: "nt_bf16_kernel<fwd> (hidden-layer forward GEMM + bias/w0/sin-phase epilogue)",
+                2: "nt_bf16_kernel<dx> (hidden-layer input-gradient GEMM + cos epilogue)",
+                3: "tn_dw_kernel (hidden-layer weight-gradient split-K GEMM)",
+                4: "fused_fwd_bf16_kernel (whole forward: layer 0, hidden MFMA layers, output layer)"}
 
 
 def parse():
@@ -64,7 +65,7 @@ def setup_dist(args):
 
 
 def build_step(args, dev, rank, world):
-    from siren_mri_amd import dataio, loss_functions, modules
+    from siren_mri_amd import dataio, loss_functions, modules, training
     from siren_mri_amd.training_ddp import GradAllReducer
     torch.manual_seed(0)
     model = modules.SingleBVPNet(type="sine", mode="mlp", hidden_features=args.hidden,
@@ -73,7 +74,7 @@ def build_step(args, dev, rank, world):
     coords = dataio.get_mgrid(args.side)[None].to(dev)
     img = dataio.smooth_random_image(args.side, seed=rank)
     gt = {"img": torch.from_numpy(img).reshape(1, -1, 1).to(dev)}
-    opt = torch.optim.Adam(lr=1e-4, params=model.parameters())
+    opt = training.make_adam(model.parameters(), 1e-4)
     reducer = GradAllReducer(model.parameters(), op="sum") if world > 1 else None
     model_input = {"coords": coords}
 
@@ -90,9 +91,24 @@ def build_step(args, dev, rank, world):
     return step, model
 
 
-def layer_flops(args, kclass):
+def kernel_model(args, kclass):
+    """Algorithmic FLOPs and HBM bytes of ONE launch of a kernel class at the bench workload
+    (DESIGN.md §5): F = hidden width, e = bytes per stored activation element (2 in bf16 mode:
+    16-bit phases / bf16 gradients; 4 in fp32 mode), C = 2 inputs, O = 1 output."""
     rows = args.side * args.side
-    return 2.0 * rows * args.hidden * args.hidden
+    F, nh = args.hidden, args.num_hidden_layers
+    e = 2 if args.precision == "bf16" else 4
+    C, O = 2, 1
+    if kclass == 1:    # P_l = enc(w0 (sin(P_{l-1}) W^T + b)): read P_{l-1}, write P_l
+        return 2.0 * rows * F * F, rows * F * 2 * e
+    if kclass == 2:    # dZ_{l-1} = (dZ_l W) cos(P_{l-1}) w0: read dZ_l, P_{l-1}; write dZ_{l-1}
+        return 2.0 * rows * F * F, rows * F * 3 * e
+    if kclass == 3:    # dW_l = dZ_l^T sin(P_{l-1}): read dZ_l, P_{l-1}
+        return 2.0 * rows * F * F, rows * F * 2 * e
+    if kclass == 4:    # x in, every sine layer's phases out (kept for backward), y out
+        flops = 2.0 * rows * (C * F + nh * F * F + F * O)
+        return flops, rows * (4 * C + (nh + 1) * F * e + 4 * O)
+    raise ValueError(kclass)
 
 
 def timed_region(step, steps, world):
@@ -144,7 +160,7 @@ def cpu_baseline(args, budget_s):
 def psnr_check(args, dev):
     """64^2 cameraman, 3 hidden layers, Adam 1e-4, seed 0: PSNR at steps 0/50/100/200/500 vs the
     reference's trajectory recorded in tests/golden/psnr_c1.npz (image_mse, high_freq=False)."""
-    from siren_mri_amd import dataio, loss_functions, modules, utils
+    from siren_mri_amd import dataio, loss_functions, modules, training, utils
     gold = np.load(os.path.join(ROOT, "tests", "golden", "psnr_c1.npz"), allow_pickle=False)
     steps = list(gold["steps"])
     img = dataio.Implicit2DWrapper(dataio.Camera(), sidelength=64)[0][1]["img"][None].to(dev)
@@ -154,7 +170,7 @@ def psnr_check(args, dev):
         torch.manual_seed(0)
         m = modules.SingleBVPNet(type="sine", hidden_features=256, num_hidden_layers=3, sidelength=(64, 64),
                                  precision=prec).to(dev)
-        opt = torch.optim.Adam(lr=1e-4, params=m.parameters())
+        opt = training.make_adam(m.parameters(), 1e-4)
         vals = []
         for s in range(max(steps) + 1):
             out = m({"coords": coords})
@@ -199,7 +215,8 @@ def main():
 
     # pick the dominant kernel class from a short untimed probe (3 steps per class)
     totals = {}
-    for kc in (_native.KCLASS_FWD_GEMM, _native.KCLASS_DX_GEMM, _native.KCLASS_DW_GEMM):
+    for kc in (_native.KCLASS_FWD_GEMM, _native.KCLASS_DX_GEMM, _native.KCLASS_DW_GEMM,
+               _native.KCLASS_FWD_FUSED):
         with _native.KernelTimer(kc) as t:
             for _ in range(3):
                 step()
@@ -216,13 +233,20 @@ def main():
     coords_per_rank = args.side * args.side
     value = world * coords_per_rank * args.steps / elapsed
     avg_s = kt.avg_ms * 1e-3
-    flops = layer_flops(args, dom)
-    peak, unit = PEAK[args.precision]
-    achieved = flops / avg_s if avg_s > 0 else float("nan")
-    roofline = {"bound": "mfma", "kernel": KCLASS_NAMES[dom], "achieved": round(achieved / 1e12, 2),
-                "peak": round(peak / 1e12, 1), "unit": unit, "frac": round(achieved / peak, 4),
+    flops, nbytes = kernel_model(args, dom)
+    mfma_peak, _ = PEAK[args.precision]
+    # the binding roofline: whichever resource the algorithmic work needs longer on at peak
+    if nbytes / HBM_PEAK >= flops / mfma_peak:
+        bound, work, peak, unit, scale = "hbm", nbytes, HBM_PEAK, "GB/s", 1e9
+    else:
+        bound, work, peak, unit, scale = "mfma", flops, mfma_peak, "TFLOP/s", 1e12
+    achieved = work / avg_s if avg_s > 0 else float("nan")
+    roofline = {"bound": bound, "kernel": KCLASS_NAMES[dom], "achieved": round(achieved / scale, 2),
+                "peak": round(peak / scale, 1), "unit": unit, "frac": round(achieved / peak, 4),
                 "traffic": traffic_from_profile(dom, args),
-                "flops_per_launch": flops, "avg_launch_ms": round(kt.avg_ms, 4), "launches": kt.launches,
+                "algorithmic_bytes_per_launch": nbytes, "flops_per_launch": flops,
+                "achieved_tflops": round(flops / avg_s / 1e12, 2) if avg_s > 0 else None,
+                "avg_launch_ms": round(kt.avg_ms, 4), "launches": kt.launches,
                 "kernel_class_ms_per_3_steps": {KCLASS_NAMES[k].split(" ")[0] + f"[{k}]": round(v, 3)
                                                 for k, v in totals.items()}}
     result = {

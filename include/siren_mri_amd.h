@@ -131,9 +131,22 @@ int siren_jvp_backward(const siren_mlp_desc* d, int order, const float* x, const
 #define SIREN_KCLASS_FWD_GEMM 1 /* hidden-layer forward GEMM + bias/w0/phase epilogue     */
 #define SIREN_KCLASS_DX_GEMM 2  /* hidden-layer input-gradient GEMM + cos-weighted epilogue */
 #define SIREN_KCLASS_DW_GEMM 3  /* hidden-layer weight-gradient split-K GEMM               */
+#define SIREN_KCLASS_FWD_FUSED 4 /* whole forward in one kernel (bf16, narrow in/out layers) */
 int siren_timing_enable(int kernel_class, int max_launches);
 int siren_timing_collect(double* total_ms, int64_t* launches);
 void siren_timing_disable(void);
+
+/*
+ * Process-wide execution options (no reference counterpart; used by tests and benchmarks to
+ * compare code paths). Keys:
+ *   "fused_forward"  1 (default): bf16 stacks of equal power-of-two hidden widths run their
+ *                    forward as one kernel; 0: one kernel per layer.
+ *   "debug_fused_profile"  device address of an int64 buffer [grid][4] that receives per-
+ *                    workgroup cycle counts of the fused forward's phases, or 0 (off).
+ * Returns SIREN_OK, or SIREN_EINVAL for an unknown key / value. Not thread-safe.
+ */
+int siren_config_set(const char* key, int64_t value);
+int64_t siren_config_get(const char* key); /* -1 for an unknown key */
 
 /* Thread-local message of the last failing call ("" if none). */
 const char* siren_last_error(void);

@@ -36,6 +36,8 @@ EXPORTED_SYMBOLS = (
     "siren_timing_enable",
     "siren_timing_collect",
     "siren_timing_disable",
+    "siren_config_set",
+    "siren_config_get",
     "siren_last_error",
     "siren_version",
 )
@@ -43,6 +45,7 @@ EXPORTED_SYMBOLS = (
 KCLASS_FWD_GEMM = 1
 KCLASS_DX_GEMM = 2
 KCLASS_DW_GEMM = 3
+KCLASS_FWD_FUSED = 4
 
 
 class SirenMLPDesc(ctypes.Structure):
@@ -101,6 +104,10 @@ def _declare(lib):
     lib.siren_timing_collect.restype = ctypes.c_int
     lib.siren_timing_disable.argtypes = []
     lib.siren_timing_disable.restype = None
+    lib.siren_config_set.argtypes = [ctypes.c_char_p, i64]
+    lib.siren_config_set.restype = ctypes.c_int
+    lib.siren_config_get.argtypes = [ctypes.c_char_p]
+    lib.siren_config_get.restype = i64
     lib.siren_last_error.argtypes = []
     lib.siren_last_error.restype = ctypes.c_char_p
     lib.siren_version.argtypes = []
@@ -127,6 +134,19 @@ def load_library(path: str | None = None):
 
 def lib():
     return _lib if _lib is not None else load_library()
+
+
+def set_option(key: str, value: int) -> None:
+    """siren_config_set: process-wide execution options (e.g. "fused_forward")."""
+    if lib().siren_config_set(key.encode(), int(value)) != 0:
+        raise NativeError(last_error())
+
+
+def get_option(key: str) -> int:
+    v = lib().siren_config_get(key.encode())
+    if v < 0:
+        raise NativeError(f"unknown option {key!r}")
+    return int(v)
 
 
 def last_error() -> str:

@@ -36,8 +36,13 @@ template <> struct Prec<kPrecF32> {
   using grad_t = float;
   using op_t = float;
   static DEV phase_t enc(float p) { return p; }
+  // phase of w0 * (z + b): the reference's sin(w0 * (xW^T + b)) argument (modules.py:26,38)
+  static DEV phase_t encz(float z, float b, float w0) { return w0 * (z + b); }
   static DEV float sinp(phase_t v) { return sinf(v); }
   static DEV float cosp(phase_t v) { return cosf(v); }
+  // sin / cos of an fp32 radian argument (the sine output layer, outermost_linear=False)
+  static DEV float sinr(float x) { return sinf(x); }
+  static DEV float cosr(float x) { return cosf(x); }
 };
 
 template <> struct Prec<kPrecBF16> {
@@ -49,9 +54,28 @@ template <> struct Prec<kPrecBF16> {
     r = r - floorf(r);
     return (uint16_t)((uint32_t)__builtin_rintf(r * 65536.0f) & 0xFFFFu);
   }
+  // Phase of w0 * (z + b) in one FMA: round(z k + b k) with k = w0 * 2^16 / 2pi; the low 16 bits
+  // of the two's-complement integer are the phase mod 2pi (valid for |w0 (z + b)| < 2^15 * 2pi * 2^15).
+  static DEV float enck(float w0) { return w0 * (65536.0f * kInv2Pi); }
+  static DEV phase_t encz(float z, float b, float w0) {
+    const float k = enck(w0);
+    return enc_scaled(z, b * k, k);
+  }
+  // the same with the bias already multiplied by k = enck(w0)
+  static DEV phase_t enc_scaled(float z, float bk, float k) {
+    return (uint16_t)(int)__builtin_rintf(fmaf(z, k, bk));
+  }
   static DEV float rev(phase_t v) { return (float)v * (1.0f / 65536.0f); }
   static DEV float sinp(phase_t v) { return __builtin_amdgcn_sinf(rev(v)); }
   static DEV float cosp(phase_t v) { return __builtin_amdgcn_cosf(rev(v)); }
+  static DEV float sinr(float x) {
+    const float r = x * kInv2Pi;
+    return __builtin_amdgcn_sinf(r - floorf(r));
+  }
+  static DEV float cosr(float x) {
+    const float r = x * kInv2Pi;
+    return __builtin_amdgcn_cosf(r - floorf(r));
+  }
 };
 
 DEV float to_f32(float v) { return v; }

@@ -231,7 +231,7 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
           const int rl = 32 * bm + (e & 3) + 8 * (e >> 2) + 4 * h;
           uint16_t* dst = Cs + rl * ncols + col_l;
           if constexpr (FWDLIKE) {
-            *dst = PT::enc(a.w0 * (acc[bm][e] + bcol));
+            *dst = PT::encz(acc[bm][e], bcol, a.w0);
           } else if constexpr (MODE == MODE_DXLIN) {
             const int64_t row = t * BM + rl;
             if (row < rows) ((float*)a.C)[(rowbase + row) * N + n0 + col_l] = acc[bm][e];
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(512) void nt_f32_kernel(NTArgs a) {
         const int rl = (e & 3) + 8 * (e >> 2) + 4 * h;
         float* dst = Cs + rl * ncols + col_l;
         if constexpr (FWDLIKE) {
-          *dst = PT::enc(a.w0 * (acc[e] + bcol));
+          *dst = PT::encz(acc[e], bcol, a.w0);
         } else if constexpr (MODE == MODE_DXLIN) {
           const int64_t row = t * BM + rl;
           if (row < rows) ((float*)a.C)[(rowbase + row) * N + n0 + col_l] = acc[e];

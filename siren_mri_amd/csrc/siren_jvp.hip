@@ -218,7 +218,7 @@ __global__ __launch_bounds__(256) void jvp_nt_kernel(JNTArgs a) {
           const int s = (int)(row / a.N);
           const int64_t n = row - (int64_t)s * a.N;
           if (s == 0)
-            ((phase_t*)a.Pout)[(b * a.N + n) * a.Nout + col] = PT::enc(a.w0 * (v + bias[col]));
+            ((phase_t*)a.Pout)[(b * a.N + n) * a.Nout + col] = PT::encz(v, bias[col], a.w0);
           else
             a.Uout[((b * (a.S - 1) + (s - 1)) * a.N + n) * a.Nout + col] = v;
         } else {
@@ -388,7 +388,7 @@ __global__ __launch_bounds__(256) void jvp_first_kernel(JFirstArgs a) {
     const float* xr = a.x + (b * a.N + n) * a.C;
     float z = 0.f;
     for (int c = 0; c < a.C; ++c) z = fmaf(xr[c], W[f * a.C + c], z);
-    ((phase_t*)a.P)[(b * a.N + n) * a.F + f] = PT::enc(a.w0 * (z + bias[f]));
+    ((phase_t*)a.P)[(b * a.N + n) * a.F + f] = PT::encz(z, bias[f], a.w0);
     for (int s = 0; s < a.Su; ++s)
       a.U[((b * a.Su + s) * a.N + n) * a.F + f] = (s < a.C) ? W[f * a.C + s] : 0.f;
   }

@@ -11,6 +11,7 @@
 #include "siren_valu.hip"
 #include "siren_gemm.hip"
 #include "siren_jvp.hip"
+#include "siren_fused.hip"
 
 using namespace siren;
 
@@ -71,6 +72,20 @@ inline int first_kp(const siren_mlp_desc* d) {
 }
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// Shapes the single-kernel forward (siren_fused.hip) covers: bf16, 1..4 inputs, 1..8 outputs,
+// every hidden width 256, up to FUSED_MAXH hidden MFMA layers.
+bool g_fused_forward = true;
+long long* g_fused_prof = nullptr;  // debug: per-workgroup phase cycle counters of the fused forward
+bool fused_shape(const siren_mlp_desc* d) {
+  if (d->prec != SIREN_PREC_BF16) return false;
+  if (d->dims[0] > FUSED_MAXC || d->dims[d->num_layers] > FUSED_MAXO) return false;
+  const int F = d->dims[1];
+  if (F != 256) return false;
+  for (int l = 1; l < d->num_layers; ++l)
+    if (d->dims[l] != F) return false;
+  return d->num_layers - 2 <= FUSED_MAXH;
+}
+
 int max_hidden(const siren_mlp_desc* d) {
   int m = 0;
   for (int l = 1; l < d->num_layers; ++l) m = std::max(m, d->dims[l]);
@@ -112,6 +127,7 @@ struct Layout {
   int64_t part_off;
   int64_t ws_bytes;
   int64_t weights_bytes;  // prepared MFMA weights (front of `saved`, or of the workspace)
+  int64_t frag_off;       // fused-forward fragment-order hidden weights (-1: shape not eligible)
 };
 
 Layout layout_of(const siren_mlp_desc* d) {
@@ -137,6 +153,11 @@ Layout layout_of(const siren_mlp_desc* d) {
     }
     lo.wt_op_off[l] = off;
     off = align_up(off + n * g.op_sz, 256);
+  }
+  lo.frag_off = -1;
+  if (fused_shape(d) && g.L > 2) {
+    lo.frag_off = off;
+    off = align_up(off + g.nb * (int64_t)(g.L - 2) * d->dims[1] * d->dims[1] * 2, 256);
   }
   lo.weights_bytes = off;
   for (int l = 0; l + 1 < g.L; ++l) {
@@ -313,14 +334,65 @@ int launch_nt(const NTArgs& a, int64_t nb, int kclass, hipStream_t st) {
   return check_launch(names[MODE]);
 }
 
+int fused_forward(const siren_mlp_desc* d, const Geo& g, const Layout& lo, const float* x, float* y,
+                  char* saved, char* wbuf, hipStream_t st) {
+  const int F = d->dims[1], nh = g.L - 2;
+  if (nh > 0) {
+    FragPrepArgs fp;
+    memset(&fp, 0, sizeof(fp));
+    for (int l = 1; l + 1 < g.L; ++l) fp.W[l - 1] = d->weight[l];
+    fp.out = (bf16*)(wbuf + lo.frag_off);
+    fp.nb = g.nb;
+    fp.F = F;
+    fp.nh = nh;
+    hipLaunchKernelGGL(prep_frag_kernel, dim3(grid1d(g.nb * nh * (int64_t)F * F / 8, 1024)), dim3(256), 0,
+                       st, fp);
+    int rc = check_launch("prep_frag");
+    if (rc) return rc;
+  }
+  FusedFwdArgs a;
+  memset(&a, 0, sizeof(a));
+  a.x = x;
+  a.W0 = d->weight[0];
+  a.b0 = d->bias[0];
+  a.Wfrag = nh > 0 ? (const bf16*)(wbuf + lo.frag_off) : nullptr;
+  for (int l = 1; l + 1 < g.L; ++l) a.bias[l - 1] = d->bias[l];
+  a.WL = d->weight[g.L - 1];
+  a.bL = d->bias[g.L - 1];
+  for (int l = 0; l + 1 < g.L; ++l) a.P[l] = saved ? saved + lo.saved_off[l] : nullptr;
+  a.y = y;
+  a.prof = g_fused_prof;
+  a.rows_per_batch = g.rows;
+  a.batched = d->weights_batched ? 1 : 0;
+  a.C = d->dims[0];
+  a.F = F;
+  a.O = d->dims[g.L];
+  a.nh = nh;
+  a.sine_out = d->outermost_linear ? 0 : 1;
+  a.w0 = d->w0;
+  const int64_t tiles = cdiv(g.rows, FUSED_BM);
+  const int64_t per = std::max<int64_t>(1, 256 / g.nb);
+  dim3 grid((unsigned)std::min<int64_t>(tiles, per), (unsigned)g.nb);
+  tmark_begin(SIREN_KCLASS_FWD_FUSED, st);
+  using KernelFn = void (*)(FusedFwdArgs);
+  static const KernelFn table[FUSED_MAXC] = {fused_fwd_bf16_kernel<256, 1>, fused_fwd_bf16_kernel<256, 2>,
+                                             fused_fwd_bf16_kernel<256, 3>, fused_fwd_bf16_kernel<256, 4>};
+  hipLaunchKernelGGL(table[a.C - 1], grid, dim3(512), 0, st, a);
+  tmark_end(SIREN_KCLASS_FWD_FUSED, st);
+  return check_launch("fused_fwd");
+}
+
 template <int PREC>
 int forward_impl(const siren_mlp_desc* d, const float* x, float* y, char* saved, char* ws,
                  hipStream_t st) {
   const Geo g = geo_of(d);
   const Layout lo = layout_of(d);
   char* wbuf = saved ? saved : ws;  // prepared weights live in `saved` so backward reuses them
+  const bool fused = PREC == kPrecBF16 && g_fused_forward && fused_shape(d);
+  if (fused && !saved) return fused_forward(d, g, lo, x, y, nullptr, wbuf, st);
   int rc = prep_weights<PREC>(d, g, lo, wbuf, st);
   if (rc) return rc;
+  if (fused) return fused_forward(d, g, lo, x, y, saved, wbuf, st);
   auto phase_buf = [&](int l) -> char* {
     return saved ? saved + lo.saved_off[l] : ws + lo.pp_off[l & 1];
   };
@@ -987,6 +1059,23 @@ void siren_timing_disable(void) {
     delete[] g_timing.ev;
   }
   g_timing = Timing();
+}
+
+int siren_config_set(const char* key, int64_t value) {
+  if (key && strcmp(key, "fused_forward") == 0 && (value == 0 || value == 1)) {
+    g_fused_forward = value != 0;
+    return SIREN_OK;
+  }
+  if (key && strcmp(key, "debug_fused_profile") == 0) {  // device pointer or 0
+    g_fused_prof = (long long*)(intptr_t)value;
+    return SIREN_OK;
+  }
+  return fail(SIREN_EINVAL, "unknown option %s=%lld", key ? key : "(null)", (long long)value);
+}
+
+int64_t siren_config_get(const char* key) {
+  if (key && strcmp(key, "fused_forward") == 0) return g_fused_forward ? 1 : 0;
+  return -1;
 }
 
 const char* siren_version(void) {

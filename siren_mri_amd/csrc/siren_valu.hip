@@ -167,8 +167,8 @@ __global__ __launch_bounds__(256) void first_fwd_kernel(FirstFwdArgs a) {
     phase_t out[8];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      out[e] = PT::enc(a.w0 * (z[e] + b0v[e]));
-      out[e + 4] = PT::enc(a.w0 * (z[e + 4] + b1v[e]));
+      out[e] = PT::encz(z[e], b0v[e], a.w0);
+      out[e + 4] = PT::encz(z[e + 4], b1v[e], a.w0);
     }
     store8((phase_t*)a.P + row * F + f, out);
   }
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(256) void last_fwd_kernel(LastFwdArgs a) {
     for (int o = 0; o < MAXO; ++o) {
       if (o < a.O) {
         float z = half_sum(acc[o]) + bias[o];
-        if (a.sine_out) z = sinf(a.w0 * z);
+        if (a.sine_out) z = PT::sinr(a.w0 * z);
         if (l32 == o) a.y[row * a.O + o] = z;
       }
     }
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(256) void last_bwd_kernel(LastBwdArgs a) {
           }
 #pragma unroll
       for (int o = 0; o < MAXO; ++o)
-        if (o < a.O) g[o] = (g[o] * cosf(a.w0 * (half_sum(acc[o]) + bias[o]))) * a.w0;
+        if (o < a.O) g[o] = (g[o] * PT::cosr(a.w0 * (half_sum(acc[o]) + bias[o]))) * a.w0;
     }
 #pragma unroll
     for (int o = 0; o < MAXO; ++o) db[o] += g[o];

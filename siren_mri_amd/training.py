@@ -79,6 +79,14 @@ def compute_loss(losses, loss_schedules, total_steps, writer):
     return train_loss
 
 
+def make_adam(params, lr):
+    """torch.optim.Adam as training.py:29 builds it; on GPU parameters the single-kernel (fused)
+    implementation of the same update rule, instead of the multi-launch foreach one."""
+    params = list(params)
+    fused = len(params) > 0 and all(p.is_cuda for p in params)
+    return torch.optim.Adam(lr=lr, params=params, fused=fused)
+
+
 def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_checkpoint, model_dir, loss_fn,
           summary_fn, val_dataloader=None, double_precision=False, clip_grad=False, use_lbfgs=False,
           loss_schedules=None, fourier_feat_transformer=None, device=None, hyperopt_run=False,
@@ -86,7 +94,7 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
     """Fit `model` (training.py:19-146). `grad_reducer`, if given, is called after each backward
     (before clipping) — the data-parallel gradient exchange of training_ddp. With
     write_outputs=False (non-zero data-parallel ranks) nothing is written to disk."""
-    optim = torch.optim.Adam(lr=lr, params=model.parameters())
+    optim = make_adam(model.parameters(), lr)
     dev = model_device(model) if device is None else torch.device(device)
     if write_outputs:
         summaries_dir, checkpoints_dir = prepare_model_dir(model_dir, hyperopt_run)

@@ -1,0 +1,96 @@
+"""GPU: the single-kernel bf16 forward (siren_fused.hip) against the per-layer kernels and the
+fp64 oracle. The fused and per-layer paths share their arithmetic (same phase encoding, same
+bf16 operands, same output-layer reduction order); they may differ only through the MFMA's
+internal summation order, so y agrees to ~1e-3 norm-relative and parity vs the oracle keeps the
+bf16 tolerances of test_gpu_siren_stack.py (3e-2 forward, 5e-2 gradients)."""
+import pytest
+import torch
+
+from oracle import siren_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _params(dims, B, seed):
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for l in range(len(dims) - 1):
+        W, b = orc.siren_init(dims, seed=seed + l)[l]
+        if B is not None:
+            W = (W.unsqueeze(0).repeat(B, 1, 1) * (1 + 0.1 * torch.randn(B, 1, 1, generator=g))).contiguous()
+            b = (b.unsqueeze(0).repeat(B, 1) + 0.01 * torch.randn(B, dims[l + 1], generator=g)).contiguous()
+        out.append((W, b))
+    return out
+
+
+def _forward(x, params, fused, grad, outermost_linear=True):
+    from siren_mri_amd import _native
+    from siren_mri_amd.ops import siren_mlp
+    _native.set_option("fused_forward", 1 if fused else 0)
+    try:
+        ws = [W.to(DEV).requires_grad_(grad) for W, _ in params]
+        bs = [b.to(DEV).requires_grad_(grad) for _, b in params]
+        with torch.set_grad_enabled(grad):
+            y = siren_mlp(x.to(DEV), ws, bs, precision="bf16", outermost_linear=outermost_linear)
+            if grad:
+                y.square().sum().backward()
+        torch.cuda.synchronize()
+        grads = [(w.grad.cpu(), b.grad.cpu()) for w, b in zip(ws, bs)] if grad else None
+        return y.detach().cpu(), grads
+    finally:
+        _native.set_option("fused_forward", 1)
+
+
+CASES = [
+    ([2, 256, 256, 256, 256, 1], None, 4096),    # metric architecture
+    ([2, 256, 256, 1], None, 1000),              # ragged tail (1000 = 7 x 128 + 104)
+    ([2, 256, 1], None, 300),                    # no hidden MFMA layer
+    ([3, 128, 128, 128, 4], None, 777),
+    ([4, 64, 64, 2], None, 129),
+    ([2, 256, 256, 256, 2], 3, 500),             # per-set weights (hypernetwork shape)
+]
+
+
+@pytest.mark.parametrize("dims,B,n", CASES)
+def test_fused_matches_per_layer_and_oracle(dims, B, n):
+    params = _params(dims, B, seed=len(dims) + n)
+    g = torch.Generator().manual_seed(n)
+    x = torch.rand(B or 1, n, dims[0], generator=g) * 2 - 1
+    y_f, g_f = _forward(x, params, fused=True, grad=True)
+    y_u, g_u = _forward(x, params, fused=False, grad=True)
+    assert orc.norm_rel(y_f, y_u) < 2e-3
+    with torch.no_grad():
+        y_ref = orc.siren_forward(x.double(), [(W.double(), b.double()) for W, b in params])
+    assert orc.norm_rel(y_f, y_ref) < 3e-2
+    for (dWf, dbf), (dWu, dbu) in zip(g_f, g_u):
+        assert orc.norm_rel(dWf, dWu) < 2e-2
+        assert orc.norm_rel(dbf, dbu) < 2e-2
+
+
+def test_fused_no_grad_forward_equals_training_forward():
+    dims = [2, 256, 256, 256, 256, 1]
+    params = _params(dims, None, seed=3)
+    x = orc.get_mgrid(64).unsqueeze(0)
+    y_train, _ = _forward(x, params, fused=True, grad=True)
+    y_eval, _ = _forward(x, params, fused=True, grad=False)
+    assert torch.equal(y_train, y_eval)
+
+
+def test_fused_sine_output():
+    dims = [3, 64, 64, 4]
+    params = _params(dims, None, seed=8)
+    x = torch.rand(1, 200, 3, generator=torch.Generator().manual_seed(1)) * 2 - 1
+    y_f, _ = _forward(x, params, fused=True, grad=False, outermost_linear=False)
+    y_u, _ = _forward(x, params, fused=False, grad=False, outermost_linear=False)
+    assert orc.norm_rel(y_f, y_u) < 2e-3
+
+
+def test_config_option_roundtrip():
+    from siren_mri_amd import _native
+    assert _native.get_option("fused_forward") == 1
+    _native.set_option("fused_forward", 0)
+    assert _native.get_option("fused_forward") == 0
+    _native.set_option("fused_forward", 1)
+    with pytest.raises(_native.NativeError):
+        _native.set_option("no_such_option", 1)

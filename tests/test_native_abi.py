@@ -68,15 +68,23 @@ def test_check_rejects_unsupported(dims, msg):
 
 
 def test_saved_bytes_formula_bf16():
-    """saved = prepared bf16 weights (W and W^T of each MFMA layer) + one 16-bit phase tensor per
-    sine layer — 2 bytes per activation element."""
+    """saved = prepared bf16 weights (W, W^T and the fused forward's fragment-order copy of each
+    MFMA layer) + one 16-bit phase tensor per sine layer — 2 bytes per activation element."""
     lib = _native.load_library()
     rows = 512 * 512
     d = _desc([2, 256, 256, 256, 256, 1], rows_per_batch=rows)
     got = lib.siren_mlp_saved_bytes(ctypes.byref(d))
-    weights = 3 * 2 * 256 * 256 * 2
+    weights = 3 * 3 * 256 * 256 * 2
     phases = 4 * rows * 256 * 2
     assert got == weights + phases
+
+
+def test_config_options():
+    lib = _native.load_library()
+    assert lib.siren_config_get(b"fused_forward") in (0, 1)
+    assert lib.siren_config_get(b"nope") == -1
+    assert lib.siren_config_set(b"nope", 1) != 0
+    assert "unknown option" in _native.last_error()
 
 
 def test_empty_input_rejected():
