@@ -141,6 +141,14 @@ void siren_timing_disable(void);
  * compare code paths). Keys:
  *   "fused_forward"  1 (default): bf16 stacks of equal power-of-two hidden widths run their
  *                    forward as one kernel; 0: one kernel per layer.
+ *   "fused_backward" 1 (default): bf16 backward folds the first layer's weight gradient into
+ *                    the bottom hidden layer's input-gradient kernel (when no input gradient is
+ *                    requested), and the output layer into the top hidden layer's kernels when
+ *                    "fuse_output_layer" is 1 (default 0); 0: separate kernels.
+ *   "dx_ring"        1 (default): 256x256 bf16 input-gradient layers use the 4-stage
+ *                    load pipeline kernel; 0: the double-buffered one.
+ *   "dw_ring"        1 (default): 256x256 bf16 weight-gradient layers use the ring kernel
+ *                    (one full 256x256 partial per workgroup); 0: 128x128-tile split-K kernel.
  *   "debug_fused_profile"  device address of an int64 buffer [grid][4] that receives per-
  *                    workgroup cycle counts of the fused forward's phases, or 0 (off).
  * Returns SIREN_OK, or SIREN_EINVAL for an unknown key / value. Not thread-safe.

@@ -25,6 +25,32 @@ constexpr int MODE_DX = 1;
 constexpr int MODE_FIRST = 2;
 constexpr int MODE_DXLIN = 3;
 
+// Output-layer fusion into the top hidden layer's backward (outermost_linear, O <= 2): the
+// kernels form dZ_top = (dy W_L) cos(P_top) w0 on the fly instead of reading it from HBM, exactly
+// as last_bwd_kernel computes it (modules.py:25-26 backward; the output layer is linear).
+constexpr int TOP_MAXO = 2;
+struct TopArgs {
+  const void* Ptop;    // [rows, F_top] phase of the last sine layer
+  const float* dy;     // [rows, O]
+  const float* WL;     // [nb_w][O, F_top]
+  int64_t wl_bstride;
+  float* partL;        // tn_dw only: dW_L / db_L partial slabs [split][nb][O*F_top + O]
+  int64_t partL_stride;
+  int O;
+};
+// First-layer fusion into the bottom hidden layer's input-gradient kernel (C <= 4, no dx): the
+// epilogue accumulates dW_0 = dZ_0^T x and db_0 = sum dZ_0 (first_bwd_kernel's sums) instead of
+// storing dZ_0.
+constexpr int BOT_MAXC = 4;
+struct BotArgs {
+  const float* x;      // [rows, C]
+  const float* W0;     // [nb_w][F0, C] fp32 (dx_ring: dx = dZ_0 W_0)
+  int64_t w0_bstride;
+  float* part;         // [grid.x][nb][F0*C + F0] partial slabs (slab index = workgroup)
+  int64_t split_stride;
+  int C;
+};
+
 struct NTArgs {
   const void* A;       // [rows, lda] phase_t (FWD), grad_t (DX, DXLIN) or f32 (FIRST)
   const void* W;       // [nb_w][N, K] op_t   (FWD: W_l ; DX: W_l^T ; FIRST: W_0 zero-padded to K)
@@ -39,6 +65,8 @@ struct NTArgs {
   int lda;             // FIRST: row stride of x (= in_features <= K); otherwise K
   int a_vec;           // FIRST: x rows are 16-byte aligned (lda % 4 == 0, aligned base)
   float w0;
+  TopArgs top;         // DX with TOP
+  BotArgs bot;         // DX with BOT
 };
 
 // Largest power-of-two divisor of the 16-byte chunks per row, capped at 16, minus one: the XOR
@@ -55,6 +83,8 @@ struct TNArgs {
   int M;
   int N;
   int p_vec;           // RAW: x rows are 16-byte aligned (N % 4 == 0, aligned base)
+  float w0;            // TOP
+  TopArgs top;         // TOP: D = dZ_top formed from P_top, dy and W_L; also dW_L / db_L partials
 };
 
 // ------------------------------------------------------------------------------------------
@@ -73,16 +103,24 @@ DEV void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-template <int MODE, int KMAX>
+template <int MODE, int KMAX, bool TOP = false, bool BOT = false>
 __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
   using PT = Prec<kPrecBF16>;
   constexpr int BM = 64 * 256 / KMAX;
   constexpr int A_BYTES = BM * KMAX * 2;
   constexpr int C_BYTES = BM * 256 * 2;
+  constexpr int X_BYTES = BOT ? BM * BOT_MAXC * 4 : 0;  // staged x tile (BOT)
+  constexpr int G_BYTES = TOP ? BM * TOP_MAXO * 4 : 0;  // staged dy tile (TOP)
+  constexpr int WL_BYTES = TOP ? TOP_MAXO * KMAX * 4 : 0;  // W_L (TOP)
   constexpr int NKS = KMAX / 16;
-  __shared__ __attribute__((aligned(16))) char smem[2 * A_BYTES + 2 * C_BYTES];
+  static_assert(!(TOP || BOT) || MODE == MODE_DX, "fusions apply to the input-gradient GEMM");
+  __shared__ __attribute__((aligned(16)))
+  char smem[2 * A_BYTES + 2 * C_BYTES + 2 * X_BYTES + 2 * G_BYTES + WL_BYTES];
   char* const Abase = smem;
   char* const Cbase = smem + 2 * A_BYTES;
+  char* const Xbase = smem + 2 * A_BYTES + 2 * C_BYTES;
+  char* const Gbase = Xbase + 2 * X_BYTES;
+  float* const WLs = (float*)(Gbase + 2 * G_BYTES);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -163,16 +201,73 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
       }
     }
   };
+  // TOP: the dZ_top tile is formed from the register-staged P_top phases, the dy tile (LDS-DMA)
+  // and W_L (LDS), exactly as last_bwd_kernel forms it, and written into the A image.
+  if constexpr (TOP) {
+    for (int i = tid; i < TOP_MAXO * K; i += 512) {
+      const int o = i / K, f = i - o * K;
+      WLs[i] = o < a.top.O ? a.top.WL[batch * a.top.wl_bstride + (int64_t)o * K + f] : 0.f;
+    }
+  }
+  // In place over the A image, whose chunks the DMA filled with P_top phases (same swizzle).
+  auto top_store = [&](int buf) {
+    const float* gt = (const float*)(Gbase + buf * G_BYTES);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int u = tid + 512 * q;
+      const int r = u / a_cpr, c = u - r * a_cpr;
+      if (r < BM) {
+        char* p = Abase + buf * A_BYTES + a_off(r, c);
+        const u16x8 ph = *(const u16x8*)p;
+        float g[TOP_MAXO];
+#pragma unroll
+        for (int o = 0; o < TOP_MAXO; ++o) g[o] = o < a.top.O ? gt[r * a.top.O + o] : 0.f;
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float dh = 0.f;
+#pragma unroll
+          for (int o = 0; o < TOP_MAXO; ++o) dh = fmaf(g[o], WLs[o * K + 8 * c + e], dh);
+          v[e] = (bf16)((dh * PT::cosp(ph[e])) * a.w0);
+        }
+        *(bf16x8*)p = v;
+      }
+    }
+  };
+  // BOT: per-lane sums of dZ_0 x (its column, C inputs) and dZ_0, over every row it sees.
+  float bot_dw[BOT ? BOT_MAXC : 1], bot_db = 0.f;
+#pragma unroll
+  for (int ci = 0; ci < (BOT ? BOT_MAXC : 1); ++ci) bot_dw[ci] = 0.f;
+
   // DX: LDS-DMA of the dZ tile (A image, swizzle applied on the source address) and the P tile.
   auto dx_dma = [&](int64_t t, int buf) {
     const int64_t m0 = t * BM;
     const int n_a = BM * a_cpr / 64, n_p = BM * c_cpr / 64;
+    if constexpr (BOT) {
+      // x tile rows [m0, m0 + BM) are contiguous: BM*C floats in 16-byte pieces
+      const int nx = BM * a.bot.C / 4;
+      if (wave == 7 && lane < nx) {
+        const int64_t el = min((int64_t)(m0 * a.bot.C) + 4 * lane, rows * a.bot.C - 4);
+        __builtin_amdgcn_global_load_lds((const void*)(a.bot.x + rowbase * a.bot.C + el),
+                                         (lds_void*)(Xbase + buf * X_BYTES), 16, 0, 0);
+      }
+    }
+    if constexpr (TOP) {
+      // dy rows [m0, m0 + BM): BM*O floats in 16-byte pieces (rows past the end are masked later)
+      const int ng = BM * a.top.O / 4;
+      if (wave == 6 && lane < ng) {
+        const int64_t el = min((int64_t)(m0 * a.top.O) + 4 * lane, rows * a.top.O - 4);
+        __builtin_amdgcn_global_load_lds((const void*)(a.top.dy + rowbase * a.top.O + el),
+                                         (lds_void*)(Gbase + buf * G_BYTES), 16, 0, 0);
+      }
+    }
+    const void* asrc = TOP ? a.top.Ptop : a.A;  // TOP: P_top phases, converted in place later
     for (int i = wave; i < n_a; i += 8) {
       const int u = i * 64 + lane;
       const int r = u / a_cpr, p = u - r * a_cpr;
       const int c = p ^ (r & smask);
       const int64_t row = min(m0 + r, rows - 1);
-      __builtin_amdgcn_global_load_lds((const void*)((const bf16*)a.A + (rowbase + row) * K + c * 8),
+      __builtin_amdgcn_global_load_lds((const void*)((const bf16*)asrc + (rowbase + row) * K + c * 8),
                                        (lds_void*)(Abase + buf * A_BYTES + i * 1024), 16, 0, 0);
     }
     if constexpr (MODE == MODE_DX)
@@ -193,6 +288,10 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
   } else {
     dx_dma(t, 0);
     vm_drain();
+    if constexpr (TOP) {
+      lds_barrier();  // W_L and the dy tile visible
+      top_store(0);
+    }
   }
   lds_barrier();
   int cur = 0;
@@ -201,7 +300,9 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
     const bool has_next = tn < ntiles;
     if (has_next) {
       if constexpr (FWDLIKE) fwd_load(tn);
-      else dx_dma(tn, cur ^ 1);
+      else {
+        dx_dma(tn, cur ^ 1);
+      }
     }
     f32x16 acc[BM / 32];
 #pragma unroll
@@ -235,6 +336,17 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
           } else if constexpr (MODE == MODE_DXLIN) {
             const int64_t row = t * BM + rl;
             if (row < rows) ((float*)a.C)[(rowbase + row) * N + n0 + col_l] = acc[bm][e];
+          } else if constexpr (BOT) {
+            // the bf16-rounded dZ_0 (what first_bwd would read back), summed against x
+            const float c = PT::cosp(*dst);
+            const float dz = (float)(bf16)((acc[bm][e] * c) * a.w0);
+            if (t * BM + rl < rows) {
+              const float* xr = (const float*)(Xbase + cur * X_BYTES) + rl * a.bot.C;
+              bot_db += dz;
+#pragma unroll
+              for (int ci = 0; ci < BOT_MAXC; ++ci)
+                if (ci < a.bot.C) bot_dw[ci] = fmaf(dz, xr[ci], bot_dw[ci]);
+            }
           } else {
             const float c = PT::cosp(*dst);
             *dst = __builtin_bit_cast(uint16_t, (bf16)((acc[bm][e] * c) * a.w0));
@@ -244,7 +356,7 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
     if constexpr (MODE == MODE_DX || MODE == MODE_DXLIN) vm_drain();  // next tile's DMA has landed
     lds_barrier();
     // epilogue 2: coalesced 16-byte stores of the finished tile
-    if constexpr (MODE != MODE_DXLIN) {
+    if constexpr (MODE != MODE_DXLIN && !BOT) {
       const int64_t m0 = t * BM;
       const int nch = BM * c_cpr;
       for (int u = tid; u < nch; u += 512) {
@@ -257,8 +369,23 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
     if constexpr (FWDLIKE) {
       if (has_next) fwd_store(cur ^ 1);
     }
+    if constexpr (TOP) {
+      if (has_next) top_store(cur ^ 1);
+    }
     lds_barrier();
     cur ^= 1;
+  }
+  if constexpr (BOT) {
+    // lanes l and l + 32 hold the same column: combine, then one slab row per column
+    bot_db += __shfl_xor(bot_db, 32, 64);
+#pragma unroll
+    for (int ci = 0; ci < BOT_MAXC; ++ci) bot_dw[ci] += __shfl_xor(bot_dw[ci], 32, 64);
+    if (h == 0 && col_ok) {
+      const int F0 = N, f = n0 + col_l;
+      float* part = a.bot.part + (int64_t)blockIdx.x * a.bot.split_stride + batch * (int64_t)(F0 * a.bot.C + F0);
+      for (int ci = 0; ci < a.bot.C; ++ci) part[f * a.bot.C + ci] = bot_dw[ci];
+      part[F0 * a.bot.C + f] = bot_db;
+    }
   }
 }
 
@@ -413,7 +540,7 @@ template <> struct TNLds<kPrecF32> {
   static constexpr int BYTES = 2 * KC * ROW * 4;
 };
 
-template <int PREC, bool RAW>
+template <int PREC, bool RAW, bool TOP = false>
 __global__ __launch_bounds__(256) void tn_dw_kernel(TNArgs a) {
   using PT = Prec<PREC>;
   using phase_t = typename PT::phase_t;
@@ -430,10 +557,28 @@ __global__ __launch_bounds__(256) void tn_dw_kernel(TNArgs a) {
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int tiles_n = (a.N + TN_BN - 1) / TN_BN;
-  const int ti = blockIdx.x / tiles_n, tj = blockIdx.x % tiles_n;
+  // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so consecutive slots of one
+  // XCD take all output tiles of one (split, batch) row range — its dZ / P rows are then read from
+  // HBM once and re-read from that XCD's L2.
+  int tile, split;
+  int64_t batch;
+  {
+    const int64_t gx = gridDim.x, groups = (int64_t)gridDim.y * gridDim.z;
+    const int64_t lin = blockIdx.x + gx * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z);
+    int64_t grp;
+    if (groups % 8 == 0) {
+      const int64_t slot = lin >> 3;
+      tile = (int)(slot % gx);
+      grp = (slot / gx) * 8 + (lin & 7);
+    } else {
+      tile = blockIdx.x;
+      grp = blockIdx.y + (int64_t)gridDim.y * blockIdx.z;
+    }
+    split = (int)(grp % gridDim.y);
+    batch = grp / gridDim.y;
+  }
+  const int ti = tile / tiles_n, tj = tile % tiles_n;
   const int i0 = ti * TN_BM, j0 = tj * TN_BN;
-  const int split = blockIdx.y;
-  const int64_t batch = blockIdx.z;
   const int64_t rowbase = batch * a.rows_per_batch;
   const int64_t r_begin = (int64_t)split * a.rows_per_split;
   int64_t r_end = r_begin + a.rows_per_split;
@@ -461,6 +606,25 @@ __global__ __launch_bounds__(256) void tn_dw_kernel(TNArgs a) {
   p_in_t preg[UPT];
   float xr[UPT][VEC];  // RAW: fp32 inputs of the wide first layer
   const int cu = tid % UPR;  // this thread's column unit (fixed across chunks)
+  static_assert(!TOP || PREC == kPrecBF16, "output-layer fusion is a bf16-mode path");
+  // TOP: phases of P_top for the D columns, dy rows, this thread's W_L columns, dW_L/db_L sums
+  u16x8 tph[TOP ? UPT : 1];
+  float tg[TOP ? UPT : 1][TOP_MAXO];
+  float twl[TOP_MAXO][TOP ? VEC : 1];
+  float tdw[TOP_MAXO][TOP ? VEC : 1];
+  float tdb[TOP_MAXO];
+  if constexpr (TOP) {
+#pragma unroll
+    for (int o = 0; o < TOP_MAXO; ++o) {
+      tdb[o] = 0.f;
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const int ci = i0 + cu * VEC + e;
+        twl[o][e] = (o < a.top.O && ci < a.M) ? a.top.WL[batch * a.top.wl_bstride + (int64_t)o * a.M + ci] : 0.f;
+        tdw[o][e] = 0.f;
+      }
+    }
+  }
 
   auto load = [&](int64_t rc) {
 #pragma unroll
@@ -468,7 +632,13 @@ __global__ __launch_bounds__(256) void tn_dw_kernel(TNArgs a) {
       const int r = (tid + 256 * q) / UPR;
       const int64_t row = rc + r;
       const int ci = i0 + cu * VEC, cj = j0 + cu * VEC;
-      if (row < r_end && ci < a.M) {
+      if constexpr (TOP) {
+        const bool in = row < r_end && ci < a.M;
+        const int64_t rr = rowbase + (in ? row : 0);
+        tph[q] = in ? *(const u16x8*)((const uint16_t*)a.top.Ptop + rr * a.M + ci) : u16x8{};
+#pragma unroll
+        for (int o = 0; o < TOP_MAXO; ++o) tg[q][o] = (in && o < a.top.O) ? a.top.dy[rr * a.top.O + o] : 0.f;
+      } else if (row < r_end && ci < a.M) {
         dreg[q] = *(const d_in_t*)((const grad_t*)a.D + (rowbase + row) * a.M + ci);
       } else {
 #pragma unroll
@@ -502,6 +672,26 @@ __global__ __launch_bounds__(256) void tn_dw_kernel(TNArgs a) {
       const int r = (tid + 256 * q) / UPR;
       const bool valid = (rc + r) < r_end;
       d_in_t dv = dreg[q];
+      if constexpr (TOP) {
+        // dZ_top exactly as last_bwd_kernel forms it; dW_L / db_L sums on the side (tj == 0)
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          float dh = 0.f;
+#pragma unroll
+          for (int o = 0; o < TOP_MAXO; ++o) dh = fmaf(tg[q][o], twl[o][e], dh);
+          dv[e] = from_f32<op_t>((dh * PT::cosp(tph[q][e])) * a.w0);
+        }
+        if (do_db) {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) {
+            const float sv = PT::sinp(tph[q][e]);
+#pragma unroll
+            for (int o = 0; o < TOP_MAXO; ++o) tdw[o][e] = fmaf(tg[q][o], sv, tdw[o][e]);
+          }
+#pragma unroll
+          for (int o = 0; o < TOP_MAXO; ++o) tdb[o] += tg[q][o];
+        }
+      }
       *(d_in_t*)(Ds + r * ROW + cu * VEC) = dv;
 #pragma unroll
       for (int e = 0; e < VEC; ++e) dbacc[e] += to_f32(dv[e]);
@@ -594,7 +784,416 @@ __global__ __launch_bounds__(256) void tn_dw_kernel(TNArgs a) {
       if (row < a.M) part[(int64_t)a.M * a.N + row] = s;
     }
   }
+  if constexpr (TOP) {
+    if (do_db) {
+      // dW_L[o][i0 + cu*VEC + e] summed over the 256/UPR threads sharing the column unit
+      __syncthreads();
+      float* red = (float*)smem;  // [256 / UPR][TOP_MAXO * 128 + TOP_MAXO]
+      constexpr int RS = TOP_MAXO * 128 + TOP_MAXO;
+      const int slot = tid / UPR;
+#pragma unroll
+      for (int o = 0; o < TOP_MAXO; ++o)
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) red[slot * RS + o * 128 + cu * VEC + e] = tdw[o][e];
+      if (cu == 0) {
+#pragma unroll
+        for (int o = 0; o < TOP_MAXO; ++o) red[slot * RS + TOP_MAXO * 128 + o] = tdb[o];
+      }
+      __syncthreads();
+      float* pl = a.top.partL + (int64_t)split * a.top.partL_stride + batch * (int64_t)(a.top.O * a.M + a.top.O);
+      for (int idx = tid; idx < a.top.O * 128; idx += 256) {
+        const int o = idx >> 7, col = i0 + (idx & 127);
+        if (col < a.M) {
+          float sum = 0.f;
+          for (int k = 0; k < 256 / UPR; ++k) sum += red[k * RS + idx];
+          pl[o * a.M + col] = sum;
+        }
+      }
+      if (ti == 0 && tid < a.top.O) {
+        float sum = 0.f;
+        for (int k = 0; k < 256 / UPR; ++k) sum += red[k * RS + TOP_MAXO * 128 + tid];
+        pl[a.top.O * a.M + tid] = sum;
+      }
+    }
+  }
 }
 
+
+}  // namespace siren
+
+namespace siren {
+
+// ------------------------------------------------------------------------------------------
+// dx_ring: the 256 x 256 input-gradient layer (MODE_DX of nt_bf16_kernel) with a deeper load
+// pipeline. 32-row tiles flow through a 4-stage LDS ring (dZ tile in the swizzled A image, P tile
+// in the C image; 32 KB per stage), so three tiles' DMA (96 KB per CU) are in flight while one
+// is computed. Waits are counted (s_waitcnt vmcnt(N) for exactly the stage being consumed), never
+// vmcnt(0) in steady state, so the stores of earlier tiles keep draining under the compute.
+// ------------------------------------------------------------------------------------------
+constexpr int RING_S = 4;
+constexpr int RING_BM = 32;
+
+template <int VMCNT>
+DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMCNT) : "memory"); }
+
+// BOTC > 0: the bottom hidden layer with the first layer folded in (C = BOTC inputs): dZ_0 stays
+// in LDS; a VALU pass over it accumulates dW_0 / db_0 (first_bwd_kernel's sums, per-workgroup
+// partial slabs in a.bot.part) and, with DXOUT, writes dx = dZ_0 W_0 (a.C, [rows, C] f32).
+// The x tile rides in the ring with the other operands (one 16-byte DMA lane per input channel
+// per wave), so the counted vector-memory waits stay exact.
+template <int BOTC, bool DXOUT>
+__global__ __launch_bounds__(512) void dx_ring_bf16_kernel(NTArgs a) {
+  using PT = Prec<kPrecBF16>;
+  constexpr int K = 256, N = 256, BM = RING_BM, S = RING_S;
+  constexpr int X_BYTES = BOTC > 0 ? BM * BOTC * 4 : 0;
+  constexpr int A_BYTES = BM * K * 2, C_BYTES = BM * N * 2, STAGE = A_BYTES + C_BYTES + X_BYTES;
+  constexpr int NKS = K / 16;
+  constexpr int A_CPR = K / 8, C_CPR = N / 8;   // 16-byte chunks per row
+  constexpr int SMASK = 15;
+  constexpr int NA = BM * A_CPR / 64 / 8;       // DMA instructions per wave per stage (A) = 2
+  constexpr int NP = BM * C_CPR / 64 / 8;       // (P) = 2
+  constexpr int NQ = BM * C_CPR / 512;          // chunks per thread in the store / BOT pass = 2
+  constexpr bool BOT = BOTC > 0;
+  constexpr int NST = BOT ? (DXOUT ? NQ : 0) : NQ;  // vector stores per thread per tile
+  // VMEM ops issued after stage i's DMA when iteration i waits for it: the stores of the S-1
+  // previous tiles and the DMAs of the S-2 stages issued in between.
+  constexpr int NX = BOT ? 1 : 0;               // x DMA instructions per wave per stage
+  constexpr int STEADY = (S - 1) * NST + (S - 2) * (NA + NP + NX);
+  static_assert(!DXOUT || BOT, "dx output belongs to the first-layer fusion");
+  __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int64_t batch = blockIdx.y;
+  const int64_t rows = a.rows_per_batch;
+  const int64_t rowbase = batch * rows;
+  const int64_t ntiles = (rows + BM - 1) / BM;
+  const int col = 32 * wave + r32;
+
+  const bf16* Wb = (const bf16*)a.W + batch * a.w_bstride + (int64_t)col * K;
+  bf16x8 wf[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) wf[ks] = *(const bf16x8*)(Wb + 16 * ks + 8 * h);
+
+  // BOT pass mapping: thread owns features 8 cth .. +8 of rows rth + 16 q
+  constexpr int CB = BOT ? BOTC : 1;
+  const int cth = tid & 31, rth = tid >> 5;
+  float w0r[8][CB], bdw[8][CB], bdb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    bdb[e] = 0.f;
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      bdw[e][c] = 0.f;
+      w0r[e][c] = 0.f;
+    }
+  }
+  if constexpr (BOT) {
+    const float* W0 = a.bot.W0 + batch * a.bot.w0_bstride;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int c = 0; c < CB; ++c) w0r[e][c] = W0[(8 * cth + e) * BOTC + c];
+  }
+
+  auto a_off = [&](int r, int c) -> int { return r * K * 2 + ((c ^ (r & SMASK)) << 4); };
+  auto dma = [&](int64_t t, int st) {
+    char* base = smem + st * STAGE;
+    const int64_t m0 = t * BM;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      const int i = wave + 8 * k;
+      const int u = i * 64 + lane;
+      const int r = u / A_CPR, p = u - r * A_CPR;
+      const int c = p ^ (r & SMASK);
+      const int64_t row = min(m0 + r, rows - 1);
+      __builtin_amdgcn_global_load_lds((const void*)((const bf16*)a.A + (rowbase + row) * K + c * 8),
+                                       (lds_void*)(base + i * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int i = wave + 8 * k;
+      const int u = i * 64 + lane;
+      const int r = u / C_CPR, c = u - r * C_CPR;
+      const int64_t row = min(m0 + r, rows - 1);
+      __builtin_amdgcn_global_load_lds((const void*)((const uint16_t*)a.Paux + (rowbase + row) * N + c * 8),
+                                       (lds_void*)(base + A_BYTES + i * 1024), 16, 0, 0);
+    }
+    if constexpr (BOT) {
+      // x rows [m0, m0 + BM): BM*C floats; wave w moves bytes [16 C w, 16 C (w + 1)) (C lanes)
+      if (lane < BOTC) {
+        const int64_t el = min((m0 + rowbase) * BOTC + 4 * (BOTC * wave + lane), (rowbase + rows) * BOTC - 4);
+        __builtin_amdgcn_global_load_lds((const void*)(a.bot.x + el),
+                                         (lds_void*)(base + A_BYTES + C_BYTES + 16 * BOTC * wave), 16, 0, 0);
+      }
+    }
+  };
+
+  const int64_t t0 = blockIdx.x, G = gridDim.x;
+  const int64_t niter = t0 < ntiles ? (ntiles - t0 + G - 1) / G : 0;
+  for (int s = 0; s < S - 1; ++s)
+    if (s < niter) dma(t0 + s * G, s);
+
+  for (int64_t i = 0; i < niter; ++i) {
+    const int st = (int)(i % S);
+    const int64_t t = t0 + i * G;
+    // wait for this stage's DMA (this wave's part), then for every wave's part and for every
+    // wave to be done with the stage the next DMA overwrites (consumed in iteration i - 1)
+    if (i + S - 2 < niter && i >= S - 1) vm_wait<STEADY>();
+    else vm_drain();
+    lds_barrier();
+    if (i + S - 1 < niter) dma(t0 + (i + S - 1) * G, (int)((i + S - 1) % S));
+    char* base = smem + st * STAGE;
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const bf16x8 af = *(const bf16x8*)(base + a_off(r32, 2 * ks + h));
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, wf[ks], acc, 0, 0, 0);
+    }
+    // epilogue 1: dZ_{l-1} = acc * cos(P) * w0, in place over the staged P tile
+    uint16_t* Cs = (uint16_t*)(base + A_BYTES);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int rl = (e & 3) + 8 * (e >> 2) + 4 * h;
+      uint16_t* dst = Cs + rl * N + col;
+      const float c = PT::cosp(*dst);
+      *dst = __builtin_bit_cast(uint16_t, (bf16)((acc[e] * c) * a.w0));
+    }
+    lds_barrier();
+    const int64_t m0 = t * BM;
+    if constexpr (!BOT) {
+      // epilogue 2: coalesced 16-byte stores
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int u = tid + 512 * q;
+        const int r = u / C_CPR, c = u - r * C_CPR;
+        const u16x8 v = *(const u16x8*)(base + A_BYTES + (r * N + c * 8) * 2);
+        if (m0 + r < rows) *(u16x8*)((uint16_t*)a.C + (rowbase + m0 + r) * N + c * 8) = v;
+      }
+    } else {
+      // first layer: dW_0 += dZ_0^T x, db_0 += sum dZ_0, dx = dZ_0 W_0 (32-lane row reduction)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int r = rth + 16 * q;
+        const bf16x8 dv = *(const bf16x8*)(base + A_BYTES + (r * N + 8 * cth) * 2);
+        const float* xs = (const float*)(base + A_BYTES + C_BYTES) + r * BOTC;
+        float xv[CB];
+#pragma unroll
+        for (int c = 0; c < CB; ++c) xv[c] = xs[c];
+        const bool valid = m0 + r < rows;
+        float dxp[CB];
+#pragma unroll
+        for (int c = 0; c < CB; ++c) dxp[c] = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float dz = valid ? (float)dv[e] : 0.f;
+          bdb[e] += dz;
+#pragma unroll
+          for (int c = 0; c < CB; ++c) {
+            bdw[e][c] = fmaf(dz, xv[c], bdw[e][c]);
+            dxp[c] = fmaf(dz, w0r[e][c], dxp[c]);
+          }
+        }
+        if constexpr (DXOUT) {
+#pragma unroll
+          for (int c = 0; c < CB; ++c)
+#pragma unroll
+            for (int off = 16; off >= 1; off >>= 1) dxp[c] += __shfl_xor(dxp[c], off, 32);
+          typedef float fvec __attribute__((ext_vector_type(BOTC == 3 ? 4 : BOTC)));
+          if (cth == 0 && valid) {
+            float* dst = (float*)a.C + (rowbase + m0 + r) * BOTC;
+            if constexpr (BOTC == 3) {
+              dst[0] = dxp[0];
+              dst[1] = dxp[1];
+              dst[2] = dxp[2];
+            } else {
+              fvec v;
+#pragma unroll
+              for (int c = 0; c < CB; ++c) v[c] = dxp[c];
+              *(fvec*)dst = v;
+            }
+          }
+        }
+      }
+    }
+  }
+  if constexpr (BOT) {
+    // per-workgroup slab: dW_0 [F0][C] then db_0 [F0], summed over the 16 row slots
+    __syncthreads();
+    float* red = (float*)smem;  // [16][256 * (C + 1)]
+    constexpr int RS = 256 * (CB + 1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int f = 8 * cth + e;
+#pragma unroll
+      for (int c = 0; c < CB; ++c) red[rth * RS + f * BOTC + c] = bdw[e][c];
+      red[rth * RS + 256 * BOTC + f] = bdb[e];
+    }
+    __syncthreads();
+    float* part = a.bot.part + (int64_t)blockIdx.x * a.bot.split_stride + batch * (int64_t)RS;
+    for (int idx = tid; idx < RS; idx += 512) {
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) sum += red[k * RS + idx];
+      part[idx] = sum;
+    }
+  }
+}
+
+}  // namespace siren
+
+namespace siren {
+
+// ------------------------------------------------------------------------------------------
+// dw_ring: the 256 x 256 weight-gradient layer, dW_l = dZ_l^T sin(P_{l-1}), db_l = sum dZ_l,
+// one 256 x 256 fp32 partial per workgroup over a contiguous row range (split-K; 128 accumulator
+// registers per lane: wave w owns dW rows [64 (w & 3), +64) x cols [128 (w >> 2), +128)).
+// 32-row chunks of dZ and P stream through a 4-stage LDS ring by DMA (16-byte chunks XOR-
+// swizzled by 2 (row & 7), which keeps the transposing ds_read_b64_tr_b16 fragment reads
+// conflict-free); each stage's phases are turned into bf16 sin(P) in place, then 16 MFMAs per
+// wave per stage. Counted waits keep three stages (96 KB per CU) in flight.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(512) void dw_ring_bf16_kernel(TNArgs a) {
+  using PT = Prec<kPrecBF16>;
+  constexpr int M = 256, N = 256, KC = 32, S = RING_S;
+  constexpr int D_BYTES = KC * M * 2, P_BYTES = KC * N * 2, STAGE = D_BYTES + P_BYTES;
+  constexpr int CPR = 32;                                  // 16-byte chunks per row (both)
+  constexpr int ND = KC * CPR / 64 / 8, NP = KC * CPR / 64 / 8;  // DMA instrs per wave per stage
+  constexpr int STEADY = (S - 2) * (ND + NP);
+  static_assert(STEADY == 8, "counted wait below");
+  __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 3, wn = wave >> 2;
+  const int split = blockIdx.x;
+  const int64_t batch = blockIdx.y;
+  const int64_t rowbase = batch * a.rows_per_batch;
+  const int64_t r_begin = (int64_t)split * a.rows_per_split;
+  int64_t r_end = r_begin + a.rows_per_split;
+  if (r_end > a.rows_per_batch) r_end = a.rows_per_batch;
+  const int64_t nchunk = r_end > r_begin ? (r_end - r_begin + KC - 1) / KC : 0;
+
+  auto swz = [](int r, int c) -> int { return c ^ (2 * (r & 7)); };
+  auto dma = [&](int64_t k, int st) {
+    char* base = smem + st * STAGE;
+    const int64_t r0 = r_begin + k * KC;
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const int i = wave + 8 * j;                 // 1 KB = 2 rows
+      const int r = 2 * i + (lane >> 5), p = lane & 31;
+      const int64_t row = min(r0 + r, r_end - 1);
+      __builtin_amdgcn_global_load_lds(
+          (const void*)((const bf16*)a.D + (rowbase + row) * M + 8 * swz(r, p)),
+          (lds_void*)(base + i * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const int i = wave + 8 * j;
+      const int r = 2 * i + (lane >> 5), p = lane & 31;
+      const int64_t row = min(r0 + r, r_end - 1);
+      __builtin_amdgcn_global_load_lds(
+          (const void*)((const uint16_t*)a.P + (rowbase + row) * N + 8 * swz(r, p)),
+          (lds_void*)(base + D_BYTES + i * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  // db: the convert pass thread owns columns 8 * (tid & 31) .. +8 of rows tid/32 + 16 q
+  const int cth = tid & 31, rth = tid >> 5;
+  float dbacc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) dbacc[e] = 0.f;
+
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nchunk) dma(s, s);
+
+  const int g = lane >> 4, t = lane & 15, q = t >> 2, p = t & 3;
+  for (int64_t k = 0; k < nchunk; ++k) {
+    const int st = (int)(k % S);
+    if (k + S - 2 < nchunk && k >= S - 1) vm_wait<STEADY>();
+    else vm_drain();
+    lds_barrier();
+    if (k + S - 1 < nchunk) dma(k + S - 1, (int)((k + S - 1) % S));
+    char* Db = smem + st * STAGE;
+    char* Pb = Db + D_BYTES;
+    // convert pass: P -> bf16 sin(P) in place (rows past the range -> 0); db from the same rows
+#pragma unroll
+    for (int qq = 0; qq < KC * CPR / 512; ++qq) {
+      const int r = rth + 16 * qq;
+      const bool valid = r_begin + k * KC + r < r_end;
+      const int off = r * 512 + swz(r, cth) * 16;
+      const u16x8 ph = *(const u16x8*)(Pb + off);
+      bf16x8 hv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) hv[e] = (bf16)(valid ? PT::sinp(ph[e]) : 0.f);
+      *(bf16x8*)(Pb + off) = hv;
+      if (valid) {
+        const bf16x8 dv = *(const bf16x8*)(Db + off);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dbacc[e] += (float)dv[e];
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int ks = 0; ks < KC / 16; ++ks) {
+      const int nb = 16 * ks + 8 * (g >> 1) + q;
+      bf16x8 af[2], bfr[4];
+#pragma unroll
+      for (int bm = 0; bm < 2; ++bm) {
+        const int c = 64 * wm + 32 * bm + 16 * (g & 1) + 4 * p;
+        const int o0 = nb * 512 + swz(nb, c >> 3) * 16 + (c & 7) * 2;
+        const int o1 = (nb + 4) * 512 + swz(nb + 4, c >> 3) * 16 + (c & 7) * 2;
+        af[bm] = lds_read_tr16_pair(Db + o0, Db + o1);
+      }
+#pragma unroll
+      for (int bn = 0; bn < 4; ++bn) {
+        const int c = 128 * wn + 32 * bn + 16 * (g & 1) + 4 * p;
+        const int o0 = nb * 512 + swz(nb, c >> 3) * 16 + (c & 7) * 2;
+        const int o1 = (nb + 4) * 512 + swz(nb + 4, c >> 3) * 16 + (c & 7) * 2;
+        bfr[bn] = lds_read_tr16_pair(Pb + o0, Pb + o1);
+      }
+#pragma unroll
+      for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+        for (int bn = 0; bn < 4; ++bn)
+          acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[bm], bfr[bn], acc[bm][bn], 0, 0, 0);
+    }
+  }
+
+  // partial slab: dW (row-major M x N) then db (M)
+  float* part = a.part + (int64_t)split * a.split_stride + batch * ((int64_t)M * N + M);
+#pragma unroll
+  for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+    for (int bn = 0; bn < 4; ++bn) {
+      const int col = 128 * wn + 32 * bn + (lane & 31);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = 64 * wm + 32 * bm + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        part[(int64_t)row * N + col] = acc[bm][bn][e];
+      }
+    }
+  __syncthreads();
+  float* red = (float*)smem;  // [16 row slots][256]
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rth * 256 + 8 * cth + e] = dbacc[e];
+  __syncthreads();
+  if (tid < 256) {
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sum += red[k * 256 + tid];
+    part[(int64_t)M * N + tid] = sum;
+  }
+}
 
 }  // namespace siren

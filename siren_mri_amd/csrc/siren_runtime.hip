@@ -75,6 +75,10 @@ inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // Shapes the single-kernel forward (siren_fused.hip) covers: bf16, 1..4 inputs, 1..8 outputs,
 // every hidden width 256, up to FUSED_MAXH hidden MFMA layers.
 bool g_fused_forward = true;
+bool g_fused_backward = true;
+bool g_fuse_top = false;
+bool g_dx_ring = true;  // 256x256 input-gradient layers on the 4-stage ring kernel
+bool g_dw_ring = true;  // 256x256 weight-gradient layers on the 4-stage ring kernel  // output-layer fusion: measured slower than last_bwd + plain kernels
 long long* g_fused_prof = nullptr;  // debug: per-workgroup phase cycle counters of the fused forward
 bool fused_shape(const siren_mlp_desc* d) {
   if (d->prec != SIREN_PREC_BF16) return false;
@@ -111,6 +115,14 @@ Split tn_split(const Geo& g, int M, int N) {
   return split_rows(g.rows, tiles, g.nb, 64);
 }
 Split valu_split(const Geo& g) { return split_rows(g.rows, 1, g.nb, 64); }
+// dw_ring_bf16_kernel: one workgroup per CU, each a contiguous row range of one weight set
+Split dw_ring_split(const Geo& g) {
+  const int64_t want = std::max<int64_t>(1, 256 / g.nb);
+  Split s;
+  s.rows_per_split = std::max<int64_t>(32, align_up(cdiv(g.rows, want), 32));
+  s.nsplit = std::max<int64_t>(1, cdiv(g.rows, s.rows_per_split));
+  return s;
+}
 
 // Distance between consecutive split slabs (all weight sets of one split), padded to float4.
 int64_t split_stride(const Geo& g, int64_t slab) { return align_up(g.nb * slab, 4); }
@@ -125,6 +137,7 @@ struct Layout {
   int64_t pp_off[2];     // phase ping-pong (forward without saved buffer)
   int64_t dz_off[2];     // dZ ping-pong
   int64_t part_off;
+  int64_t partL_off;      // output-layer partial slabs of the fused top backward layer
   int64_t ws_bytes;
   int64_t weights_bytes;  // prepared MFMA weights (front of `saved`, or of the workspace)
   int64_t frag_off;       // fused-forward fragment-order hidden weights (-1: shape not eligible)
@@ -182,6 +195,7 @@ Layout layout_of(const siren_mlp_desc* d) {
     const int M = d->dims[l + 1], N = d->dims[l];
     const Split s = tn_split(g, M, N);
     part = std::max(part, s.nsplit * split_stride(g, (int64_t)M * N + M));
+    part = std::max(part, dw_ring_split(g).nsplit * split_stride(g, (int64_t)M * N + M));
   }
   {
     const Split s = valu_split(g);
@@ -190,9 +204,17 @@ Layout layout_of(const siren_mlp_desc* d) {
     const int F0 = d->dims[1], C = d->dims[0];
     const Split s0 = wide_input(d) ? tn_split(g, F0, C) : s;
     part = std::max(part, s0.nsplit * split_stride(g, (int64_t)F0 * C + F0));
+    // fused bottom layer: one first-layer slab per input-gradient workgroup (<= 256)
+    part = std::max(part, (int64_t)256 * split_stride(g, (int64_t)F0 * C + F0));
   }
   lo.part_off = off;
   off = align_up(off + part * 4, 256);
+  lo.partL_off = off;
+  if (g.L >= 3) {
+    const int F = d->dims[g.L - 1], O = d->dims[g.L];
+    const Split s = tn_split(g, F, d->dims[g.L - 2]);
+    off = align_up(off + s.nsplit * split_stride(g, (int64_t)O * F + O) * 4, 256);
+  }
   lo.ws_bytes = off;
   return lo;
 }
@@ -314,19 +336,57 @@ int dispatch_first_bwd(const FirstBwdArgs& a, int64_t nsplit, int64_t nb, hipStr
 
 // One hidden-layer GEMM launch (MODE_FWD or MODE_DX). Persistent grid: one 512-thread workgroup
 // per CU (~131 KB LDS each), spread over weight sets and 256-column tiles.
-template <int PREC, int MODE>
-int launch_nt(const NTArgs& a, int64_t nb, int kclass, hipStream_t st) {
+dim3 nt_grid(const NTArgs& a, int64_t nb, int prec) {
   const int ntn = (int)cdiv(a.N, 256);
   const int kmax = a.K <= 256 ? 256 : 512;  // siren_mlp_check bounds K by 512 (bf16) / 256 (f32)
-  const int bm = PREC == kPrecBF16 ? 64 * 256 / kmax : 32;
+  const int bm = prec == kPrecBF16 ? 64 * 256 / kmax : 32;
   const int64_t tiles = cdiv(a.rows_per_batch, bm);
   const int64_t per = std::max<int64_t>(1, 256 / std::max<int64_t>(1, nb * ntn));
-  dim3 grid((unsigned)std::min<int64_t>(tiles, per), (unsigned)nb, (unsigned)ntn);
+  return dim3((unsigned)std::min<int64_t>(tiles, per), (unsigned)nb, (unsigned)ntn);
+}
+
+dim3 ring_grid(const NTArgs& a, int64_t nb) {
+  const int64_t tiles = cdiv(a.rows_per_batch, RING_BM);
+  const int64_t per = std::max<int64_t>(1, 256 / nb);
+  return dim3((unsigned)std::min<int64_t>(tiles, per), (unsigned)nb, 1);
+}
+
+// Bottom 256x256 input-gradient layer with the first layer folded in (dx_ring_bf16_kernel BOTC).
+int launch_dx_ring_bot(const NTArgs& a, int64_t nb, int C, bool dxout, int kclass, hipStream_t st) {
+  const dim3 grid = ring_grid(a, nb);
+  tmark_begin(kclass, st);
+#define SIREN_RING_BOT(CC)                                                                       \
+  if (dxout) hipLaunchKernelGGL((dx_ring_bf16_kernel<CC, true>), grid, dim3(512), 0, st, a);    \
+  else hipLaunchKernelGGL((dx_ring_bf16_kernel<CC, false>), grid, dim3(512), 0, st, a);
+  switch (C) {
+    case 1: SIREN_RING_BOT(1) break;
+    case 2: SIREN_RING_BOT(2) break;
+    case 3: SIREN_RING_BOT(3) break;
+    default: SIREN_RING_BOT(4) break;
+  }
+#undef SIREN_RING_BOT
+  tmark_end(kclass, st);
+  return check_launch("dx_ring first-layer");
+}
+
+template <int PREC, int MODE, bool TOP = false, bool BOT = false>
+int launch_nt(const NTArgs& a, int64_t nb, int kclass, hipStream_t st) {
+  const int kmax = a.K <= 256 ? 256 : 512;
+  if constexpr (PREC == kPrecBF16 && MODE == MODE_DX && !TOP && !BOT) {
+    if (g_dx_ring && a.K == 256 && a.N == 256) {
+      tmark_begin(kclass, st);
+      hipLaunchKernelGGL((dx_ring_bf16_kernel<0, false>), ring_grid(a, nb), dim3(512), 0, st, a);
+      tmark_end(kclass, st);
+      return check_launch("dx_ring");
+    }
+  }
+  const dim3 grid = nt_grid(a, nb, PREC);
   tmark_begin(kclass, st);
   if constexpr (PREC == kPrecBF16) {
-    if (kmax == 256) hipLaunchKernelGGL((nt_bf16_kernel<MODE, 256>), grid, dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((nt_bf16_kernel<MODE, 512>), grid, dim3(512), 0, st, a);
+    if (kmax == 256) hipLaunchKernelGGL((nt_bf16_kernel<MODE, 256, TOP, BOT>), grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((nt_bf16_kernel<MODE, 512, TOP, BOT>), grid, dim3(512), 0, st, a);
   } else {
+    static_assert(PREC == kPrecBF16 || !(TOP || BOT), "backward fusions are bf16-mode paths");
     hipLaunchKernelGGL((nt_f32_kernel<MODE>), grid, dim3(512), 0, st, a);
   }
   tmark_end(kclass, st);
@@ -478,9 +538,23 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
   int rc = SIREN_OK;
   float* part = (float*)(ws + lo.part_off);
   auto P = [&](int l) -> const void* { return saved + lo.saved_off[l]; };
+  const int O = d->dims[g.L], C = d->dims[0], F0 = d->dims[1];
+  // bf16-mode fusions (siren_gemm.hip TopArgs / BotArgs): the output layer's backward folds into
+  // the top hidden layer's kernels, the first layer's weight gradient into the bottom one's.
+  const bool fuse = PREC == kPrecBF16 && g_fused_backward && g.L >= 3;
+  const bool top = fuse && g_fuse_top && d->outermost_linear && O <= TOP_MAXO && (g.rows * O) % 4 == 0 && g.rows * O >= 4 &&
+                   aligned16(dy) && d->dims[g.L - 1] <= 256;
+  // first-layer fusion: the ring kernel (256x256 bottom layer) also produces dx; the older
+  // kernel only without dx
+  const bool ring_bot = fuse && g_dx_ring && !wide_input(d) && C <= BOT_MAXC && F0 == 256 &&
+                        d->dims[2] == 256 && !(top && g.L == 3) && (g.rows * C) % 4 == 0 &&
+                        g.rows * C >= 4 && aligned16(x);
+  const bool bot = ring_bot || (fuse && !dx && !wide_input(d) && C <= BOT_MAXC && F0 <= 256 &&
+                                (g.rows * C) % 4 == 0 && g.rows * C >= 4 && aligned16(x) &&
+                                !(top && g.L == 3));  // one hidden layer: the output-layer fusion only
   int cur = 0;  // dz ping-pong index holding dZ of the current layer
   // Output layer: dZ_{L-2}, dW_{L-1}, db_{L-1}.
-  {
+  if (!top) {
     const int l = g.L - 1;
     const Split s = valu_split(g);
     LastBwdArgs a;
@@ -504,12 +578,28 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
                             (int64_t)a.O * a.F, dW[l], db[l], st)))
       return rc;
   }
+  TopArgs ta;
+  memset(&ta, 0, sizeof(ta));
+  if (top) {
+    const int FL = d->dims[g.L - 1];
+    ta.Ptop = P(g.L - 2);
+    ta.dy = dy;
+    ta.WL = d->weight[g.L - 1];
+    ta.wl_bstride = d->weights_batched ? (int64_t)O * FL : 0;
+    ta.partL = (float*)(ws + lo.partL_off);
+    ta.partL_stride = split_stride(g, (int64_t)O * FL + O);
+    ta.O = O;
+  }
   // Hidden MFMA layers, top to bottom.
   for (int l = g.L - 2; l >= 1; --l) {
     const int M = d->dims[l + 1], N = d->dims[l];
+    const bool is_top = top && l == g.L - 2;
+    const bool is_bot = bot && l == 1;
+    const bool ring = PREC == kPrecBF16 && g_dw_ring && !is_top && M == 256 && N == 256;
     {
-      const Split s = tn_split(g, M, N);
+      const Split s = ring ? dw_ring_split(g) : tn_split(g, M, N);
       TNArgs a;
+      memset(&a, 0, sizeof(a));
       a.D = ws + lo.dz_off[cur];
       a.P = P(l - 1);
       a.part = part;
@@ -519,17 +609,31 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
       a.M = M;
       a.N = N;
       a.p_vec = 0;
+      a.w0 = d->w0;
+      a.top = ta;
       dim3 grid((unsigned)(cdiv(M, TN_BM) * cdiv(N, TN_BN)), (unsigned)s.nsplit, (unsigned)g.nb);
       tmark_begin(SIREN_KCLASS_DW_GEMM, st);
-      hipLaunchKernelGGL((tn_dw_kernel<PREC, false>), grid, dim3(256), 0, st, a);
+      if constexpr (PREC == kPrecBF16) {
+        if (ring)
+          hipLaunchKernelGGL(dw_ring_bf16_kernel, dim3((unsigned)s.nsplit, (unsigned)g.nb), dim3(512), 0, st, a);
+        else if (is_top) hipLaunchKernelGGL((tn_dw_kernel<PREC, false, true>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((tn_dw_kernel<PREC, false>), grid, dim3(256), 0, st, a);
+      } else {
+        hipLaunchKernelGGL((tn_dw_kernel<PREC, false>), grid, dim3(256), 0, st, a);
+      }
       tmark_end(SIREN_KCLASS_DW_GEMM, st);
       if ((rc = check_launch("tn_dw"))) return rc;
       if ((rc = launch_reduce(part, s.nsplit, a.split_stride, g.nb, (int64_t)M * N + M,
                               (int64_t)M * N, dW[l], db[l], st)))
         return rc;
+      if (is_top &&
+          (rc = launch_reduce(ta.partL, s.nsplit, ta.partL_stride, g.nb, (int64_t)O * M + O, (int64_t)O * M,
+                              dW[g.L - 1], db[g.L - 1], st)))
+        return rc;
     }
     {
       NTArgs a;
+      memset(&a, 0, sizeof(a));
       a.A = ws + lo.dz_off[cur];
       a.W = saved + lo.wt_op_off[l];
       a.bias = nullptr;
@@ -543,7 +647,35 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
       a.lda = M;
       a.a_vec = 0;
       a.w0 = d->w0;
-      if ((rc = launch_nt<PREC, MODE_DX>(a, g.nb, SIREN_KCLASS_DX_GEMM, st))) return rc;
+      a.top = ta;
+      const int64_t bot_stride = split_stride(g, (int64_t)F0 * C + F0);
+      if (is_bot) {
+        a.bot.x = x;
+        a.bot.W0 = d->weight[0];
+        a.bot.w0_bstride = d->weights_batched ? (int64_t)F0 * C : 0;
+        a.bot.part = part;
+        a.bot.split_stride = bot_stride;
+        a.bot.C = C;
+      }
+      if constexpr (PREC == kPrecBF16) {
+        if (is_bot && ring_bot) {
+          a.C = dx;  // [rows, C] f32, or not written
+          rc = launch_dx_ring_bot(a, g.nb, C, dx != nullptr, SIREN_KCLASS_DX_GEMM, st);
+        } else if (is_top && is_bot) rc = launch_nt<PREC, MODE_DX, true, true>(a, g.nb, SIREN_KCLASS_DX_GEMM, st);
+        else if (is_top) rc = launch_nt<PREC, MODE_DX, true, false>(a, g.nb, SIREN_KCLASS_DX_GEMM, st);
+        else if (is_bot) rc = launch_nt<PREC, MODE_DX, false, true>(a, g.nb, SIREN_KCLASS_DX_GEMM, st);
+        else rc = launch_nt<PREC, MODE_DX>(a, g.nb, SIREN_KCLASS_DX_GEMM, st);
+      } else {
+        rc = launch_nt<PREC, MODE_DX>(a, g.nb, SIREN_KCLASS_DX_GEMM, st);
+      }
+      if (rc) return rc;
+      if (is_bot) {
+        const int64_t nslab = ring_bot ? ring_grid(a, g.nb).x : nt_grid(a, g.nb, PREC).x;
+        if ((rc = launch_reduce(part, nslab, bot_stride, g.nb, (int64_t)F0 * C + F0, (int64_t)F0 * C, dW[0],
+                                db[0], st)))
+          return rc;
+        return SIREN_OK;  // first layer done
+      }
       cur ^= 1;
     }
   }
@@ -1066,6 +1198,22 @@ int siren_config_set(const char* key, int64_t value) {
     g_fused_forward = value != 0;
     return SIREN_OK;
   }
+  if (key && strcmp(key, "fused_backward") == 0 && (value == 0 || value == 1)) {
+    g_fused_backward = value != 0;
+    return SIREN_OK;
+  }
+  if (key && strcmp(key, "fuse_output_layer") == 0 && (value == 0 || value == 1)) {
+    g_fuse_top = value != 0;
+    return SIREN_OK;
+  }
+  if (key && strcmp(key, "dw_ring") == 0 && (value == 0 || value == 1)) {
+    g_dw_ring = value != 0;
+    return SIREN_OK;
+  }
+  if (key && strcmp(key, "dx_ring") == 0 && (value == 0 || value == 1)) {
+    g_dx_ring = value != 0;
+    return SIREN_OK;
+  }
   if (key && strcmp(key, "debug_fused_profile") == 0) {  // device pointer or 0
     g_fused_prof = (long long*)(intptr_t)value;
     return SIREN_OK;
@@ -1075,6 +1223,10 @@ int siren_config_set(const char* key, int64_t value) {
 
 int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "fused_forward") == 0) return g_fused_forward ? 1 : 0;
+  if (key && strcmp(key, "fused_backward") == 0) return g_fused_backward ? 1 : 0;
+  if (key && strcmp(key, "fuse_output_layer") == 0) return g_fuse_top ? 1 : 0;
+  if (key && strcmp(key, "dx_ring") == 0) return g_dx_ring ? 1 : 0;
+  if (key && strcmp(key, "dw_ring") == 0) return g_dw_ring ? 1 : 0;
   return -1;
 }
 

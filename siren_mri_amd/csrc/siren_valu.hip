@@ -257,18 +257,34 @@ __global__ __launch_bounds__(256) void last_bwd_kernel(LastBwdArgs a) {
 #pragma unroll
   for (int o = 0; o < MAXO; ++o) db[o] = 0.f;
 
-  for (int64_t r = r_begin + grp; r < r_end; r += 8) {
-    const int64_t row = batch * a.rows_per_batch + r;
-    const phase_t* pr = (const phase_t*)a.P + row * a.F;
-    float g[MAXO];
+  // RU rows per half-wave in flight: their loads are issued together (memory-level parallelism),
+  // then processed in row order (the same per-thread summation order as one row at a time).
+  constexpr int RU = (IT == 1 && MAXO <= 2) ? 4 : (IT == 2 && MAXO <= 2) ? 2 : 1;
+  for (int64_t r0 = r_begin + grp; r0 < r_end; r0 += 8 * RU) {
+  float gq[RU][MAXO];
+  phase_t pq[RU][IT][8];
 #pragma unroll
-    for (int o = 0; o < MAXO; ++o) g[o] = (o < a.O) ? a.dy[row * a.O + o] : 0.f;
-    phase_t pv[IT][8];
+  for (int k = 0; k < RU; ++k) {
+    const int64_t r = r0 + 8 * k;
+    const int64_t row = batch * a.rows_per_batch + (r < r_end ? r : r0);
+    const phase_t* pr = (const phase_t*)a.P + row * a.F;
+#pragma unroll
+    for (int o = 0; o < MAXO; ++o) gq[k][o] = (o < a.O) ? a.dy[row * a.O + o] : 0.f;
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
       const int f = 256 * it + 8 * l32;
-      if (f < a.F) load8(pr + f, pv[it]);
+      if (f < a.F) load8(pr + f, pq[k][it]);
     }
+  }
+#pragma unroll
+  for (int k = 0; k < RU; ++k) {
+    const int64_t r = r0 + 8 * k;
+    if (r >= r_end) break;
+    const int64_t row = batch * a.rows_per_batch + r;
+    float g[MAXO];
+#pragma unroll
+    for (int o = 0; o < MAXO; ++o) g[o] = gq[k][o];
+    phase_t (&pv)[IT][8] = pq[k];
     if (a.sine_out) {
       float acc[MAXO];
 #pragma unroll
@@ -307,6 +323,7 @@ __global__ __launch_bounds__(256) void last_bwd_kernel(LastBwdArgs a) {
         store8f((grad_t*)a.dZ + row * a.F + f, dz);
       }
     }
+  }
   }
   // Reduce the 8 row groups through LDS, 256 features at a time; one slab write per block.
   float* part = a.part + (int64_t)split * a.split_stride + batch * (int64_t)(a.O * a.F + a.O);
@@ -374,11 +391,38 @@ __global__ __launch_bounds__(256) void first_bwd_kernel(FirstBwdArgs a) {
         dw[it][e][c] = 0.f;
       }
     }
-  for (int64_t r = r_begin + grp; r < r_end; r += GROUPS) {
+  constexpr int RU = 1;  // (4 rows in flight measured slower here than in last_bwd_kernel)
+  for (int64_t r0 = r_begin + grp; r0 < r_end; r0 += GROUPS * RU) {
+  float xq[RU][MAXC];
+  float dzq[RU][IT][8];
+#pragma unroll
+  for (int k = 0; k < RU; ++k) {
+    const int64_t r = r0 + GROUPS * k;
+    const int64_t row = batch * a.rows_per_batch + (r < r_end ? r : r0);
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) xq[k][c] = (c < a.C) ? a.x[row * a.C + c] : 0.f;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int f = 256 * it + FPL * li;
+      if (f < a.F) {
+        if constexpr (FPL == 8) {
+          load8f((const grad_t*)a.dZ + row * a.F + f, dzq[k][it]);
+        } else {
+          const grad_t* src = (const grad_t*)a.dZ + row * a.F + f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dzq[k][it][e] = to_f32(src[e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < RU; ++k) {
+    const int64_t r = r0 + GROUPS * k;
+    if (r >= r_end) break;
     const int64_t row = batch * a.rows_per_batch + r;
     float xv[MAXC];
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) xv[c] = (c < a.C) ? a.x[row * a.C + c] : 0.f;
+    for (int c = 0; c < MAXC; ++c) xv[c] = xq[k][c];
     float dxp[MAXC];
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) dxp[c] = 0.f;
@@ -386,14 +430,7 @@ __global__ __launch_bounds__(256) void first_bwd_kernel(FirstBwdArgs a) {
     for (int it = 0; it < IT; ++it) {
       const int f = 256 * it + FPL * li;
       if (f < a.F) {
-        float dz[8];
-        if constexpr (FPL == 8) {
-          load8f((const grad_t*)a.dZ + row * a.F + f, dz);
-        } else {
-          const grad_t* src = (const grad_t*)a.dZ + row * a.F + f;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) dz[e] = to_f32(src[e]);
-        }
+        float (&dz)[8] = dzq[k][it];
 #pragma unroll
         for (int e = 0; e < FPL; ++e) {
           db[it][e] += dz[e];
@@ -416,6 +453,7 @@ __global__ __launch_bounds__(256) void first_bwd_kernel(FirstBwdArgs a) {
         }
       }
     }
+  }
   }
   float* part = a.part + (int64_t)split * a.split_stride + batch * (int64_t)(a.F * a.C + a.F);
 #pragma unroll

@@ -94,3 +94,95 @@ def test_config_option_roundtrip():
     _native.set_option("fused_forward", 1)
     with pytest.raises(_native.NativeError):
         _native.set_option("no_such_option", 1)
+
+
+def _grads(x, params, fused_bwd, need_dx, B):
+    from siren_mri_amd import _native
+    from siren_mri_amd.ops import siren_mlp
+    _native.set_option("fused_backward", 1 if fused_bwd else 0)
+    _native.set_option("fuse_output_layer", 1 if fused_bwd else 0)
+    try:
+        ws = [W.to(DEV).requires_grad_(True) for W, _ in params]
+        bs = [b.to(DEV).requires_grad_(True) for _, b in params]
+        xd = x.to(DEV).requires_grad_(need_dx)
+        y = siren_mlp(xd, ws, bs, precision="bf16")
+        lw = torch.randn(y.shape, generator=torch.Generator().manual_seed(9)).to(DEV)
+        (y * lw).sum().backward()
+        torch.cuda.synchronize()
+        return [(w.grad.cpu(), b.grad.cpu()) for w, b in zip(ws, bs)], (xd.grad.cpu() if need_dx else None)
+    finally:
+        _native.set_option("fused_backward", 1)
+        _native.set_option("fuse_output_layer", 0)
+
+
+BWD_CASES = [
+    ([2, 256, 256, 256, 256, 1], None, 4096),   # metric architecture: output + first-layer fusions
+    ([2, 256, 256, 1], None, 1000),             # one hidden layer: output-layer fusion only
+    ([3, 128, 128, 128, 2], None, 640),
+    ([2, 256, 256, 256, 2], 3, 500),            # per-set weights
+    ([2, 256, 256, 256, 1], None, 333),         # rows*O not a multiple of 4: unfused fallback
+]
+
+
+@pytest.mark.parametrize("dims,B,n", BWD_CASES)
+@pytest.mark.parametrize("need_dx", [False, True])
+def test_fused_backward_matches_unfused(dims, B, n, need_dx):
+    params = _params(dims, B, seed=n)
+    x = torch.rand(B or 1, n, dims[0], generator=torch.Generator().manual_seed(n + 1)) * 2 - 1
+    g_f, dx_f = _grads(x, params, True, need_dx, B)
+    g_u, dx_u = _grads(x, params, False, need_dx, B)
+    for l, ((dWf, dbf), (dWu, dbu)) in enumerate(zip(g_f, g_u)):
+        assert orc.norm_rel(dWf, dWu) < 1e-4, l
+        assert orc.norm_rel(dbf, dbu) < 1e-4, l
+    if need_dx:
+        assert orc.norm_rel(dx_f, dx_u) < 1e-4
+    # and against the fp64 oracle at the bf16 tolerance
+    ps = [(W.double().requires_grad_(True), b.double().requires_grad_(True)) for W, b in params]
+    y = orc.siren_forward(x.double(), ps)
+    lw = torch.randn(y.shape, generator=torch.Generator().manual_seed(9)).double()
+    (y * lw).sum().backward()
+    for (dWf, dbf), (W, b) in zip(g_f, ps):
+        assert orc.norm_rel(dWf, W.grad) < 5e-2
+        assert orc.norm_rel(dbf, b.grad) < 5e-2
+
+
+@pytest.mark.parametrize("n,C", [(4096, 2), (1000, 2), (33, 4), (8, 1), (1000, 3)])
+def test_dx_ring_matches_double_buffered(n, C):
+    from siren_mri_amd import _native
+    dims = [C, 256, 256, 256, 1]
+    params = _params(dims, None, seed=n)
+    x = torch.rand(1, n, C, generator=torch.Generator().manual_seed(n)) * 2 - 1
+    res = []
+    for ring in (1, 0):
+        _native.set_option("dx_ring", ring)
+        try:
+            res.append(_grads(x, params, True, True, None))
+        finally:
+            _native.set_option("dx_ring", 1)
+    (g1, dx1), (g0, dx0) = res
+    # hidden layers bit-identical; the first layer (folded into the ring kernel's epilogue) and
+    # dx differ only in fp32 summation order
+    for l, ((a1, b1), (a0, b0)) in enumerate(zip(g1, g0)):
+        if l == 0:
+            assert orc.norm_rel(a1, a0) < 1e-5 and orc.norm_rel(b1, b0) < 1e-5
+        else:
+            assert torch.equal(a1, a0) and torch.equal(b1, b0)
+    assert orc.norm_rel(dx1, dx0) < 1e-5
+
+
+@pytest.mark.parametrize("n,B", [(4096, None), (1000, None), (45, None), (700, 3)])
+def test_dw_ring_matches_tiled(n, B):
+    from siren_mri_amd import _native
+    dims = [2, 256, 256, 256, 1] if B is None else [2, 256, 256, 256, 2]
+    params = _params(dims, B, seed=n)
+    x = torch.rand(B or 1, n, 2, generator=torch.Generator().manual_seed(n)) * 2 - 1
+    res = []
+    for ring in (1, 0):
+        _native.set_option("dw_ring", ring)
+        try:
+            res.append(_grads(x, params, True, False, B))
+        finally:
+            _native.set_option("dw_ring", 1)
+    (g1, _), (g0, _) = res
+    for (a1, b1), (a0, b0) in zip(g1, g0):
+        assert orc.norm_rel(a1, a0) < 1e-5 and orc.norm_rel(b1, b0) < 1e-5

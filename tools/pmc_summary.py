@@ -1,0 +1,61 @@
+"""Per-kernel mean of rocprofv3 PMC counters over the dispatches of tools/pmc_bench.sh passes.
+
+FETCH_SIZE is reported in KB and, on gfx950, counts half the bytes of 16-B/lane streaming reads
+(MI355X_MICROARCH.md §HBM): HBM read bytes = 2 x FETCH_SIZE x 1024. WRITE_SIZE (KB) is exact.
+"""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+
+def load(pattern):
+    out = defaultdict(lambda: defaultdict(list))
+    for path in glob.glob(pattern, recursive=True):
+        for r in csv.DictReader(open(path)):
+            name = r.get("Kernel_Name") or r.get("Kernel-Name") or r.get("KernelName")
+            cname = r.get("Counter_Name") or r.get("Counter-Name")
+            val = r.get("Counter_Value") or r.get("Counter-Value")
+            disp = r.get("Dispatch_Id") or r.get("Dispatch-Id")
+            if name is None or cname is None:
+                continue
+            out[name][cname].append((disp, float(val)))
+    return out
+
+
+def main(prefix):
+    merged = defaultdict(dict)
+    for k in (1, 2, 3):
+        data = load(f"{prefix}_pmc{k}/**/*counter_collection.csv")
+        for name, counters in data.items():
+            for c, vals in counters.items():
+                # sum per dispatch (counters may be reported per XCD / instance), then mean
+                per = defaultdict(float)
+                for disp, v in vals:
+                    per[disp] += v
+                merged[name][c] = sum(per.values()) / max(1, len(per))
+    print("| kernel | HBM read MB (2xFETCH) | HBM write MB | MFMA busy % | VALU active % | wait % |")
+    print("|---|---:|---:|---:|---:|---:|")
+    rows = []
+    for name, c in merged.items():
+        short = name.split("(")[0].replace("void ", "")[-60:]
+        rd = 2 * c.get("FETCH_SIZE", float("nan")) * 1024 / 1e6
+        wr = c.get("WRITE_SIZE", float("nan")) * 1024 / 1e6
+        wc = c.get("SQ_WAVE_CYCLES", float("nan"))
+        mfma = c.get("SQ_VALU_MFMA_BUSY_CYCLES", float("nan"))
+        valu = c.get("SQ_ACTIVE_INST_VALU", float("nan"))
+        wait = c.get("SQ_WAIT_ANY", float("nan"))
+        rows.append((rd + (wr if wr == wr else 0), name, short, rd, wr, mfma, valu, wait, wc, c))
+    rows.sort(key=lambda r: -r[0] if r[0] == r[0] else 0)
+    for _, name, short, rd, wr, mfma, valu, wait, wc, c in rows:
+        print(f"| `{short}` | {rd:.1f} | {wr:.1f} | {mfma:.3g} | {100 * valu / wc if wc else float('nan'):.1f} | "
+              f"{100 * wait / wc if wc else float('nan'):.1f} |")
+    print()
+    print("raw means per dispatch:")
+    for _, name, short, *_r, c in rows:
+        print(f"- `{short}`: " + ", ".join(f"{k}={v:.4g}" for k, v in sorted(c.items())))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
