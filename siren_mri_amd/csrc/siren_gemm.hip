@@ -46,6 +46,8 @@ struct BotArgs {
   const float* x;      // [rows, C]
   const float* W0;     // [nb_w][F0, C] fp32 (dx_ring: dx = dZ_0 W_0)
   int64_t w0_bstride;
+  const float* b0;     // [nb_w][F0] (P_0 recompute)
+  int64_t b0_bstride;
   float* part;         // [grid.x][nb][F0*C + F0] partial slabs (slab index = workgroup)
   int64_t split_stride;
   int C;
@@ -83,7 +85,11 @@ struct TNArgs {
   int M;
   int N;
   int p_vec;           // RAW: x rows are 16-byte aligned (N % 4 == 0, aligned base)
-  float w0;            // TOP
+  float w0;            // TOP, dw_ring RECC
+  const float* rec_W0; // dw_ring RECC: W_0 [nb_w][F0, C], b_0 [nb_w][F0] (P = x)
+  int64_t rec_w0_bstride;
+  const float* rec_b0;
+  int64_t rec_b0_bstride;
   TopArgs top;         // TOP: D = dZ_top formed from P_top, dy and W_L; also dW_L / db_L partials
 };
 
@@ -841,7 +847,10 @@ DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMCNT) : "memory")
 // partial slabs in a.bot.part) and, with DXOUT, writes dx = dZ_0 W_0 (a.C, [rows, C] f32).
 // The x tile rides in the ring with the other operands (one 16-byte DMA lane per input channel
 // per wave), so the counted vector-memory waits stay exact.
-template <int BOTC, bool DXOUT>
+// REC (with BOTC > 0): P_0 was not kept by the forward; the epilogue recomputes each phase from
+// the staged x tile, W_0 and b_0 with the forward's arithmetic (first layer of fused_fwd_bf16 /
+// first_fwd: fmaf chain over the inputs, then PT::encz), so cos(P_0) is bit-identical.
+template <int BOTC, bool DXOUT, bool REC = false>
 __global__ __launch_bounds__(512) void dx_ring_bf16_kernel(NTArgs a) {
   using PT = Prec<kPrecBF16>;
   constexpr int K = 256, N = 256, BM = RING_BM, S = RING_S;
@@ -851,7 +860,8 @@ __global__ __launch_bounds__(512) void dx_ring_bf16_kernel(NTArgs a) {
   constexpr int A_CPR = K / 8, C_CPR = N / 8;   // 16-byte chunks per row
   constexpr int SMASK = 15;
   constexpr int NA = BM * A_CPR / 64 / 8;       // DMA instructions per wave per stage (A) = 2
-  constexpr int NP = BM * C_CPR / 64 / 8;       // (P) = 2
+  constexpr int NP = REC ? 0 : BM * C_CPR / 64 / 8;  // (P) = 2, none when P_0 is recomputed
+  static_assert(!REC || BOTC > 0, "P_0 recompute needs the staged x tile");
   constexpr int NQ = BM * C_CPR / 512;          // chunks per thread in the store / BOT pass = 2
   constexpr bool BOT = BOTC > 0;
   constexpr int NST = BOT ? (DXOUT ? NQ : 0) : NQ;  // vector stores per thread per tile
@@ -895,6 +905,16 @@ __global__ __launch_bounds__(512) void dx_ring_bf16_kernel(NTArgs a) {
     for (int e = 0; e < 8; ++e)
 #pragma unroll
       for (int c = 0; c < CB; ++c) w0r[e][c] = W0[(8 * cth + e) * BOTC + c];
+  }
+  // REC: this lane's epilogue column of W_0 and b_0
+  float wcol[CB], bcol0 = 0.f;
+#pragma unroll
+  for (int c = 0; c < CB; ++c) wcol[c] = 0.f;
+  if constexpr (REC) {
+    const float* W0 = a.bot.W0 + batch * a.bot.w0_bstride;
+#pragma unroll
+    for (int c = 0; c < CB; ++c) wcol[c] = W0[col * BOTC + c];
+    bcol0 = a.bot.b0[batch * a.bot.b0_bstride + col];
   }
 
   auto a_off = [&](int r, int c) -> int { return r * K * 2 + ((c ^ (r & SMASK)) << 4); };
@@ -959,7 +979,17 @@ __global__ __launch_bounds__(512) void dx_ring_bf16_kernel(NTArgs a) {
     for (int e = 0; e < 16; ++e) {
       const int rl = (e & 3) + 8 * (e >> 2) + 4 * h;
       uint16_t* dst = Cs + rl * N + col;
-      const float c = PT::cosp(*dst);
+      uint16_t ph;
+      if constexpr (REC) {
+        const float* xr = (const float*)(base + A_BYTES + C_BYTES) + rl * BOTC;
+        float z = 0.f;
+#pragma unroll
+        for (int c = 0; c < CB; ++c) z = fmaf(xr[c], wcol[c], z);
+        ph = PT::encz(z, bcol0, a.w0);
+      } else {
+        ph = *dst;
+      }
+      const float c = PT::cosp(ph);
       *dst = __builtin_bit_cast(uint16_t, (bf16)((acc[e] * c) * a.w0));
     }
     lds_barrier();
@@ -1056,14 +1086,18 @@ namespace siren {
 // conflict-free); each stage's phases are turned into bf16 sin(P) in place, then 16 MFMAs per
 // wave per stage. Counted waits keep three stages (96 KB per CU) in flight.
 // ------------------------------------------------------------------------------------------
+// RECC > 0: layer 1 with P_0 not kept by the forward: the x tile (RECC inputs) rides in the ring
+// instead of P_0, and the convert pass recomputes the phases exactly as the forward did.
+template <int RECC = 0>
 __global__ __launch_bounds__(512) void dw_ring_bf16_kernel(TNArgs a) {
   using PT = Prec<kPrecBF16>;
   constexpr int M = 256, N = 256, KC = 32, S = RING_S;
-  constexpr int D_BYTES = KC * M * 2, P_BYTES = KC * N * 2, STAGE = D_BYTES + P_BYTES;
+  constexpr int X_BYTES = RECC > 0 ? KC * RECC * 4 : 0;
+  constexpr int D_BYTES = KC * M * 2, P_BYTES = KC * N * 2, STAGE = D_BYTES + P_BYTES + X_BYTES;
   constexpr int CPR = 32;                                  // 16-byte chunks per row (both)
-  constexpr int ND = KC * CPR / 64 / 8, NP = KC * CPR / 64 / 8;  // DMA instrs per wave per stage
+  constexpr int ND = KC * CPR / 64 / 8;                    // DMA instrs per wave per stage
+  constexpr int NP = RECC > 0 ? 1 : KC * CPR / 64 / 8;
   constexpr int STEADY = (S - 2) * (ND + NP);
-  static_assert(STEADY == 8, "counted wait below");
   __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
 
   const int tid = threadIdx.x;
@@ -1090,14 +1124,23 @@ __global__ __launch_bounds__(512) void dw_ring_bf16_kernel(TNArgs a) {
           (const void*)((const bf16*)a.D + (rowbase + row) * M + 8 * swz(r, p)),
           (lds_void*)(base + i * 1024), 16, 0, 0);
     }
+    if constexpr (RECC > 0) {
+      // x rows [r0, r0 + KC): wave w moves bytes [16 C w, 16 C (w + 1)) (C lanes)
+      if (lane < RECC) {
+        const int64_t el = min((r0 + rowbase) * RECC + 4 * (RECC * wave + lane), (rowbase + r_end) * RECC - 4);
+        __builtin_amdgcn_global_load_lds((const void*)((const float*)a.P + el),
+                                         (lds_void*)(base + D_BYTES + P_BYTES + 16 * RECC * wave), 16, 0, 0);
+      }
+    } else {
 #pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const int i = wave + 8 * j;
-      const int r = 2 * i + (lane >> 5), p = lane & 31;
-      const int64_t row = min(r0 + r, r_end - 1);
-      __builtin_amdgcn_global_load_lds(
-          (const void*)((const uint16_t*)a.P + (rowbase + row) * N + 8 * swz(r, p)),
-          (lds_void*)(base + D_BYTES + i * 1024), 16, 0, 0);
+      for (int j = 0; j < NP; ++j) {
+        const int i = wave + 8 * j;
+        const int r = 2 * i + (lane >> 5), p = lane & 31;
+        const int64_t row = min(r0 + r, r_end - 1);
+        __builtin_amdgcn_global_load_lds(
+            (const void*)((const uint16_t*)a.P + (rowbase + row) * N + 8 * swz(r, p)),
+            (lds_void*)(base + D_BYTES + i * 1024), 16, 0, 0);
+      }
     }
   };
 
@@ -1113,6 +1156,25 @@ __global__ __launch_bounds__(512) void dw_ring_bf16_kernel(TNArgs a) {
   float dbacc[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) dbacc[e] = 0.f;
+  // RECC: W_0 rows and b_0 of this thread's 8 features
+  constexpr int CR = RECC > 0 ? RECC : 1;
+  float w0r[8][CR], b0r[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    b0r[e] = 0.f;
+#pragma unroll
+    for (int c = 0; c < CR; ++c) w0r[e][c] = 0.f;
+  }
+  if constexpr (RECC > 0) {
+    const float* W0 = a.rec_W0 + batch * a.rec_w0_bstride;
+    const float* b0 = a.rec_b0 + batch * a.rec_b0_bstride;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      b0r[e] = b0[8 * cth + e];
+#pragma unroll
+      for (int c = 0; c < CR; ++c) w0r[e][c] = W0[(8 * cth + e) * RECC + c];
+    }
+  }
 
   for (int s = 0; s < S - 1; ++s)
     if (s < nchunk) dma(s, s);
@@ -1132,7 +1194,19 @@ __global__ __launch_bounds__(512) void dw_ring_bf16_kernel(TNArgs a) {
       const int r = rth + 16 * qq;
       const bool valid = r_begin + k * KC + r < r_end;
       const int off = r * 512 + swz(r, cth) * 16;
-      const u16x8 ph = *(const u16x8*)(Pb + off);
+      u16x8 ph;
+      if constexpr (RECC > 0) {
+        const float* xr = (const float*)(Pb + P_BYTES) + r * RECC;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float z = 0.f;
+#pragma unroll
+          for (int c = 0; c < CR; ++c) z = fmaf(xr[c], w0r[e][c], z);
+          ph[e] = PT::encz(z, b0r[e], a.w0);
+        }
+      } else {
+        ph = *(const u16x8*)(Pb + off);
+      }
       bf16x8 hv;
 #pragma unroll
       for (int e = 0; e < 8; ++e) hv[e] = (bf16)(valid ? PT::sinp(ph[e]) : 0.f);

@@ -90,6 +90,17 @@ bool fused_shape(const siren_mlp_desc* d) {
   return d->num_layers - 2 <= FUSED_MAXH;
 }
 
+// bf16 stacks of the fused/ring shapes do not keep P_0: the layer-1 ring kernels recompute it from
+// x (C <= 4 inputs) — 2 B per row-feature less written by the forward and read twice by the
+// backward. Decided from the descriptor alone, so forward and backward always agree.
+bool p0_recompute(const siren_mlp_desc* d) {
+  if (!fused_shape(d) || d->num_layers < 3) return false;
+  const int64_t C = d->dims[0], rpb = d->rows_per_batch, total = d->batch * rpb;
+  if ((total * C) % 4 != 0 || total * C < 4) return false;
+  if (d->weights_batched && (rpb * C) % 4 != 0) return false;
+  return true;
+}
+
 int max_hidden(const siren_mlp_desc* d) {
   int m = 0;
   for (int l = 1; l < d->num_layers; ++l) m = std::max(m, d->dims[l]);
@@ -138,6 +149,8 @@ struct Layout {
   int64_t dz_off[2];     // dZ ping-pong
   int64_t part_off;
   int64_t partL_off;      // output-layer partial slabs of the fused top backward layer
+  int64_t xcopy_off;      // 16-byte aligned copy of x (P_0 recompute with a misaligned x)
+  bool p0_rec;
   int64_t ws_bytes;
   int64_t weights_bytes;  // prepared MFMA weights (front of `saved`, or of the workspace)
   int64_t frag_off;       // fused-forward fragment-order hidden weights (-1: shape not eligible)
@@ -173,7 +186,12 @@ Layout layout_of(const siren_mlp_desc* d) {
     off = align_up(off + g.nb * (int64_t)(g.L - 2) * d->dims[1] * d->dims[1] * 2, 256);
   }
   lo.weights_bytes = off;
+  lo.p0_rec = p0_recompute(d);
   for (int l = 0; l + 1 < g.L; ++l) {
+    if (l == 0 && lo.p0_rec) {
+      lo.saved_off[0] = -1;
+      continue;
+    }
     lo.saved_off[l] = off;
     off = align_up(off + g.total * d->dims[l + 1] * g.phase_sz, 256);
   }
@@ -215,6 +233,8 @@ Layout layout_of(const siren_mlp_desc* d) {
     const Split s = tn_split(g, F, d->dims[g.L - 2]);
     off = align_up(off + s.nsplit * split_stride(g, (int64_t)O * F + O) * 4, 256);
   }
+  lo.xcopy_off = off;
+  if (lo.p0_rec) off = align_up(off + g.total * d->dims[0] * 4, 256);
   lo.ws_bytes = off;
   return lo;
 }
@@ -352,12 +372,17 @@ dim3 ring_grid(const NTArgs& a, int64_t nb) {
 }
 
 // Bottom 256x256 input-gradient layer with the first layer folded in (dx_ring_bf16_kernel BOTC).
-int launch_dx_ring_bot(const NTArgs& a, int64_t nb, int C, bool dxout, int kclass, hipStream_t st) {
+int launch_dx_ring_bot(const NTArgs& a, int64_t nb, int C, bool dxout, bool rec, int kclass, hipStream_t st) {
   const dim3 grid = ring_grid(a, nb);
   tmark_begin(kclass, st);
-#define SIREN_RING_BOT(CC)                                                                       \
-  if (dxout) hipLaunchKernelGGL((dx_ring_bf16_kernel<CC, true>), grid, dim3(512), 0, st, a);    \
-  else hipLaunchKernelGGL((dx_ring_bf16_kernel<CC, false>), grid, dim3(512), 0, st, a);
+#define SIREN_RING_BOT(CC)                                                                              \
+  if (rec) {                                                                                             \
+    if (dxout) hipLaunchKernelGGL((dx_ring_bf16_kernel<CC, true, true>), grid, dim3(512), 0, st, a);     \
+    else hipLaunchKernelGGL((dx_ring_bf16_kernel<CC, false, true>), grid, dim3(512), 0, st, a);          \
+  } else {                                                                                               \
+    if (dxout) hipLaunchKernelGGL((dx_ring_bf16_kernel<CC, true>), grid, dim3(512), 0, st, a);           \
+    else hipLaunchKernelGGL((dx_ring_bf16_kernel<CC, false>), grid, dim3(512), 0, st, a);                \
+  }
   switch (C) {
     case 1: SIREN_RING_BOT(1) break;
     case 2: SIREN_RING_BOT(2) break;
@@ -419,7 +444,7 @@ int fused_forward(const siren_mlp_desc* d, const Geo& g, const Layout& lo, const
   for (int l = 1; l + 1 < g.L; ++l) a.bias[l - 1] = d->bias[l];
   a.WL = d->weight[g.L - 1];
   a.bL = d->bias[g.L - 1];
-  for (int l = 0; l + 1 < g.L; ++l) a.P[l] = saved ? saved + lo.saved_off[l] : nullptr;
+  for (int l = 0; l + 1 < g.L; ++l) a.P[l] = (saved && lo.saved_off[l] >= 0) ? saved + lo.saved_off[l] : nullptr;
   a.y = y;
   a.prof = g_fused_prof;
   a.rows_per_batch = g.rows;
@@ -454,7 +479,8 @@ int forward_impl(const siren_mlp_desc* d, const float* x, float* y, char* saved,
   if (rc) return rc;
   if (fused) return fused_forward(d, g, lo, x, y, saved, wbuf, st);
   auto phase_buf = [&](int l) -> char* {
-    return saved ? saved + lo.saved_off[l] : ws + lo.pp_off[l & 1];
+    if (saved && lo.saved_off[l] >= 0) return saved + lo.saved_off[l];
+    return ws + lo.pp_off[l & 1];  // (P_0 of a recompute stack: only layer 1 reads it)
   };
   // Layer 0: MFMA GEMM for wide inputs, VALU otherwise.
   if (wide_input(d)) {
@@ -542,13 +568,21 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
   // bf16-mode fusions (siren_gemm.hip TopArgs / BotArgs): the output layer's backward folds into
   // the top hidden layer's kernels, the first layer's weight gradient into the bottom one's.
   const bool fuse = PREC == kPrecBF16 && g_fused_backward && g.L >= 3;
+  // P_0 not kept (p0_recompute): layer 1 runs on the ring kernels that rebuild it from x, whatever
+  // the options say; they DMA x in 16-byte pieces, so a misaligned x is copied first.
+  const bool rec = lo.p0_rec;
+  if (rec && !aligned16(x)) {
+    if (hipMemcpyAsync(ws + lo.xcopy_off, x, g.total * C * sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess)
+      return fail(SIREN_ELAUNCH, "x copy: %s", hipGetErrorString(hipGetLastError()));
+    x = (const float*)(ws + lo.xcopy_off);
+  }
   const bool top = fuse && g_fuse_top && d->outermost_linear && O <= TOP_MAXO && (g.rows * O) % 4 == 0 && g.rows * O >= 4 &&
-                   aligned16(dy) && d->dims[g.L - 1] <= 256;
+                   aligned16(dy) && d->dims[g.L - 1] <= 256 && !(rec && g.L == 3);
   // first-layer fusion: the ring kernel (256x256 bottom layer) also produces dx; the older
   // kernel only without dx
-  const bool ring_bot = fuse && g_dx_ring && !wide_input(d) && C <= BOT_MAXC && F0 == 256 &&
-                        d->dims[2] == 256 && !(top && g.L == 3) && (g.rows * C) % 4 == 0 &&
-                        g.rows * C >= 4 && aligned16(x);
+  const bool ring_bot = rec || (fuse && g_dx_ring && !wide_input(d) && C <= BOT_MAXC && F0 == 256 &&
+                                d->dims[2] == 256 && !(top && g.L == 3) && (g.rows * C) % 4 == 0 &&
+                                g.rows * C >= 4 && aligned16(x));
   const bool bot = ring_bot || (fuse && !dx && !wide_input(d) && C <= BOT_MAXC && F0 <= 256 &&
                                 (g.rows * C) % 4 == 0 && g.rows * C >= 4 && aligned16(x) &&
                                 !(top && g.L == 3));  // one hidden layer: the output-layer fusion only
@@ -595,17 +629,24 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
     const int M = d->dims[l + 1], N = d->dims[l];
     const bool is_top = top && l == g.L - 2;
     const bool is_bot = bot && l == 1;
-    const bool ring = PREC == kPrecBF16 && g_dw_ring && !is_top && M == 256 && N == 256;
+    const bool rec1 = rec && l == 1;
+    const bool ring = rec1 || (PREC == kPrecBF16 && g_dw_ring && !is_top && M == 256 && N == 256);
     {
       const Split s = ring ? dw_ring_split(g) : tn_split(g, M, N);
       TNArgs a;
       memset(&a, 0, sizeof(a));
       a.D = ws + lo.dz_off[cur];
-      a.P = P(l - 1);
+      a.P = rec1 ? (const void*)x : P(l - 1);
       a.part = part;
       a.rows_per_batch = g.rows;
       a.rows_per_split = s.rows_per_split;
       a.split_stride = split_stride(g, (int64_t)M * N + M);
+      if (rec1) {
+        a.rec_W0 = d->weight[0];
+        a.rec_w0_bstride = d->weights_batched ? (int64_t)F0 * C : 0;
+        a.rec_b0 = d->bias[0];
+        a.rec_b0_bstride = d->weights_batched ? F0 : 0;
+      }
       a.M = M;
       a.N = N;
       a.p_vec = 0;
@@ -614,8 +655,16 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
       dim3 grid((unsigned)(cdiv(M, TN_BM) * cdiv(N, TN_BN)), (unsigned)s.nsplit, (unsigned)g.nb);
       tmark_begin(SIREN_KCLASS_DW_GEMM, st);
       if constexpr (PREC == kPrecBF16) {
-        if (ring)
-          hipLaunchKernelGGL(dw_ring_bf16_kernel, dim3((unsigned)s.nsplit, (unsigned)g.nb), dim3(512), 0, st, a);
+        const dim3 rg((unsigned)s.nsplit, (unsigned)g.nb);
+        if (rec1) {
+          switch (C) {
+            case 1: hipLaunchKernelGGL((dw_ring_bf16_kernel<1>), rg, dim3(512), 0, st, a); break;
+            case 2: hipLaunchKernelGGL((dw_ring_bf16_kernel<2>), rg, dim3(512), 0, st, a); break;
+            case 3: hipLaunchKernelGGL((dw_ring_bf16_kernel<3>), rg, dim3(512), 0, st, a); break;
+            default: hipLaunchKernelGGL((dw_ring_bf16_kernel<4>), rg, dim3(512), 0, st, a); break;
+          }
+        } else if (ring)
+          hipLaunchKernelGGL((dw_ring_bf16_kernel<0>), rg, dim3(512), 0, st, a);
         else if (is_top) hipLaunchKernelGGL((tn_dw_kernel<PREC, false, true>), grid, dim3(256), 0, st, a);
         else hipLaunchKernelGGL((tn_dw_kernel<PREC, false>), grid, dim3(256), 0, st, a);
       } else {
@@ -637,7 +686,7 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
       a.A = ws + lo.dz_off[cur];
       a.W = saved + lo.wt_op_off[l];
       a.bias = nullptr;
-      a.Paux = P(l - 1);
+      a.Paux = rec1 ? nullptr : P(l - 1);
       a.C = ws + lo.dz_off[cur ^ 1];
       a.rows_per_batch = g.rows;
       a.w_bstride = d->weights_batched ? (int64_t)M * N : 0;
@@ -653,6 +702,8 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
         a.bot.x = x;
         a.bot.W0 = d->weight[0];
         a.bot.w0_bstride = d->weights_batched ? (int64_t)F0 * C : 0;
+        a.bot.b0 = d->bias[0];
+        a.bot.b0_bstride = d->weights_batched ? F0 : 0;
         a.bot.part = part;
         a.bot.split_stride = bot_stride;
         a.bot.C = C;
@@ -660,7 +711,7 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
       if constexpr (PREC == kPrecBF16) {
         if (is_bot && ring_bot) {
           a.C = dx;  // [rows, C] f32, or not written
-          rc = launch_dx_ring_bot(a, g.nb, C, dx != nullptr, SIREN_KCLASS_DX_GEMM, st);
+          rc = launch_dx_ring_bot(a, g.nb, C, dx != nullptr, rec1, SIREN_KCLASS_DX_GEMM, st);
         } else if (is_top && is_bot) rc = launch_nt<PREC, MODE_DX, true, true>(a, g.nb, SIREN_KCLASS_DX_GEMM, st);
         else if (is_top) rc = launch_nt<PREC, MODE_DX, true, false>(a, g.nb, SIREN_KCLASS_DX_GEMM, st);
         else if (is_bot) rc = launch_nt<PREC, MODE_DX, false, true>(a, g.nb, SIREN_KCLASS_DX_GEMM, st);

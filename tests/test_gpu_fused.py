@@ -186,3 +186,29 @@ def test_dw_ring_matches_tiled(n, B):
     (g1, _), (g0, _) = res
     for (a1, b1), (a0, b0) in zip(g1, g0):
         assert orc.norm_rel(a1, a0) < 1e-5 and orc.norm_rel(b1, b0) < 1e-5
+
+
+def test_p0_recompute_with_misaligned_x():
+    # P_0 is rebuilt from x by the layer-1 ring kernels; an x view that is not 16-byte aligned
+    # takes the aligned-copy path and gives the same gradients as an aligned x
+    from siren_mri_amd.ops import siren_mlp
+    dims = [2, 256, 256, 256, 1]
+    params = _params(dims, None, seed=21)
+    big = (torch.rand(1, 1001, 2, generator=torch.Generator().manual_seed(21)) * 2 - 1).to(DEV)
+
+    def run(x):
+        ws = [W.to(DEV).requires_grad_(True) for W, _ in params]
+        bs = [b.to(DEV).requires_grad_(True) for _, b in params]
+        xl = x.detach().requires_grad_(True)
+        y = siren_mlp(xl, ws, bs, precision="bf16")
+        lw = torch.randn(y.shape, generator=torch.Generator().manual_seed(9)).to(DEV)
+        (y * lw).sum().backward()
+        return [(w.grad.cpu(), b.grad.cpu()) for w, b in zip(ws, bs)], xl.grad.cpu()
+
+    xv = big[:, 1:, :]  # 8-byte offset view
+    assert xv.data_ptr() % 16 != 0
+    g_mis, dx_mis = run(xv)
+    g_al, dx_al = run(xv.clone())
+    for (a1, b1), (a0, b0) in zip(g_mis, g_al):
+        assert torch.equal(a1, a0) and torch.equal(b1, b0)
+    assert torch.equal(dx_mis, dx_al)
