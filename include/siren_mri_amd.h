@@ -147,6 +147,8 @@ void siren_timing_disable(void);
  *                    "fuse_output_layer" is 1 (default 0); 0: separate kernels.
  *   "dx_ring"        1 (default): 256x256 bf16 input-gradient layers use the 4-stage
  *                    load pipeline kernel; 0: the double-buffered one.
+ *   "fused_forward_pipe"  1 (default): the fused forward overlaps one half-tile's MFMA work with
+ *                    the other's epilogue; 0: the sequential single-kernel forward.
  *   "dw_ring"        1 (default): 256x256 bf16 weight-gradient layers use the ring kernel
  *                    (one full 256x256 partial per workgroup); 0: 128x128-tile split-K kernel.
  *   "debug_fused_profile"  device address of an int64 buffer [grid][4] that receives per-

@@ -21,6 +21,8 @@
 //   * convert pass: each thread takes 16-byte phase chunks, stores them to P_l (coalesced rows),
 //     and writes sin(P_l) as bf16 back to the same LDS chunk (the next layer's operand), or — for
 //     the last sine layer — forms the output dot products (32-lane shuffle reduction per row).
+#include <type_traits>
+
 #include "siren_common.h"
 
 namespace siren {
@@ -326,6 +328,333 @@ __global__ __launch_bounds__(256) void prep_frag_kernel(FragPrepArgs a) {
     for (int j = 0; j < 8; ++j) v[j] = (bf16)src[j];
     *(bf16x8*)(a.out + idx * 8) = v;
   }
+}
+
+}  // namespace siren
+
+namespace siren {
+
+// ------------------------------------------------------------------------------------------
+// fused_fwd_pipe: the same forward (hidden width 256, 1..14 hidden layers) with the MFMA work of
+// one half-tile overlapped with the VALU work of the other. A 128-row tile is two 64-row halves
+// A and B with their own LDS operand buffers; every segment pairs the K loop of one half with the
+// epilogue/convert (EC) of the other, and segments are separated by one barrier:
+//
+//   L0(A) + EC(nh,B of previous tile) | K(1,A) + L0(B) | K(1,B) + EC(1,A) | K(2,A) + EC(1,B) | ...
+//   ... | K(nh,B) + EC(nh,A) | (next tile) L0(A') + EC(nh,B) | ...
+//
+// EC is wave-local: a wave converts only the 32 features it computed (phases to LDS, read back as
+// 16-byte chunks, stored to P_l, turned into bf16 sin in place), so K and EC of different halves
+// need no barrier between them and the compiler can interleave MFMA and VALU issue. Stores go
+// through buffer resources sized to the valid rows (ragged tiles drop out-of-range stores in
+// hardware, no branches). The output layer accumulates per-wave partial dot products in LDS
+// (ds_add_f32) and a small pass writes y after the next barrier. x comes in one tile ahead and
+// is parked in LDS so no vector-memory wait ever covers the stores.
+// ------------------------------------------------------------------------------------------
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+DEV __amdgpu_buffer_rsrc_t fused_rsrc(const void* base, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                           (int)(bytes > 0x7fffffff ? 0x7fffffff : bytes), 0x00020000);
+}
+
+// SIREN_PIPE_NW waves (8: two per SIMD, 256 registers each; 4: one per SIMD, 512): wave w owns
+// FB = 8 / NW blocks of 32 features, holds their W_l fragments and the accumulators of both
+// halves, and issues a slice of the other half's VALU work after each K step's MFMAs.
+#ifndef SIREN_PIPE_NW
+#define SIREN_PIPE_NW 8
+#endif
+template <int C>
+__global__ __launch_bounds__(64 * SIREN_PIPE_NW)
+void fused_fwd_pipe_kernel(FusedFwdArgs a) {
+  using PT = Prec<kPrecBF16>;
+  constexpr int F = 256, BM = 128, HB = 64, NKS = F / 16, SMASK = 15;
+  constexpr int NW = SIREN_PIPE_NW, NT = 64 * NW, FB = 8 / NW;  // waves, threads, 32-feature blocks per wave
+  // H rows padded to 528 bytes (no swizzle): every LDS address below is one per-lane base plus a
+  // compile-time offset, and the MFMA B-fragment reads stay conflict-free (row stride = 4 banks)
+  constexpr int RS = F * 2 + 16;
+  constexpr int H_BYTES = HB * RS;
+  constexpr int CPW = F / 8 / NW;          // 16-byte chunks per row owned by a wave (8)
+  constexpr int NTASK = HB * CPW / 64;     // wave-local chunk tasks per lane (8)
+
+  __shared__ __attribute__((aligned(16))) char Hs[2][H_BYTES];
+  __shared__ __attribute__((aligned(16))) float Sw0[C * F + F];           // W0^T [C][F], k * b0
+  __shared__ __attribute__((aligned(16))) float Sb[FUSED_MAXH * F];       // k * hidden biases
+  __shared__ __attribute__((aligned(16))) float Swl[FUSED_MAXO * F + FUSED_MAXO];
+  __shared__ __attribute__((aligned(16))) float Xs[2][BM * C];            // x tiles
+  // output partial sums, one slot per wave (summed in wave order: deterministic)
+  __shared__ __attribute__((aligned(16))) float Yp[2][NW][HB * FUSED_MAXO];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int j32 = lane & 31, hh = lane >> 5;
+  const int64_t batch = blockIdx.y;
+  const int64_t wb = a.batched ? batch : 0;
+  const int O = a.O, nh = a.nh;
+  const float w0 = a.w0;
+  const float kph = PT::enck(w0);
+  const int64_t rows = a.rows_per_batch;
+  const int64_t ntiles = (rows + BM - 1) / BM;
+  const int64_t G = gridDim.x;
+
+  for (int i = tid; i < F * C; i += NT) {
+    const int f = i / C, c = i - f * C;
+    Sw0[c * F + f] = a.W0[wb * F * C + i];
+  }
+  for (int f = tid; f < F; f += NT) Sw0[C * F + f] = a.b0[wb * F + f] * kph;
+  for (int l = 0; l < nh; ++l)
+    for (int f = tid; f < F; f += NT) Sb[l * F + f] = a.bias[l][wb * F + f] * kph;
+  for (int i = tid; i < O * F; i += NT) Swl[i] = a.WL[wb * O * F + i];
+  if (tid < O) Swl[FUSED_MAXO * F + tid] = a.bL[wb * O + tid];
+  for (int i = tid; i < 2 * NW * HB * FUSED_MAXO; i += NT) (&Yp[0][0][0])[i] = 0.f;
+
+  auto h_off = [&](int r, int c) -> int { return r * RS + (c << 4); };
+
+  // W fragments (fragment order, see prep_frag_kernel); wave w takes blocks FB w .. FB w + FB - 1.
+  // Buffer loads: the per-lane offset is one VGPR, the layer / block / K-step offset a scalar.
+  const __amdgpu_buffer_rsrc_t wrs =
+      fused_rsrc(a.Wfrag + wb * (int64_t)nh * F * F, (int64_t)nh * F * F * 2);
+  auto wfrag = [&](int l, int fb, int ks) -> bf16x8 {
+    const int soff = __builtin_amdgcn_readfirstlane((((l * 8 + FB * wave + fb) * NKS + ks) * 64) * 16);
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, soff, 0));
+  };
+  bf16x8 wreg[FB][NKS];
+#pragma unroll
+  for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) wreg[fb][ks] = wfrag(0, fb, ks);
+
+  // x tile: BM*C floats, NX per thread (rows past the end: last row)
+  constexpr int NX = (BM * C + NT - 1) / NT;
+  float xr[NX];
+  auto x_issue = [&](int64_t t) {
+#pragma unroll
+    for (int k = 0; k < NX; ++k) {
+      const int i = tid + NT * k;
+      int64_t r = t * BM + i / C;
+      r = r < rows ? r : rows - 1;
+      xr[k] = (i < BM * C) ? a.x[(batch * rows + r) * C + (i % C)] : 0.f;
+    }
+  };
+  auto x_park = [&](int xb) {
+#pragma unroll
+    for (int k = 0; k < NX; ++k) {
+      const int i = tid + NT * k;
+      if (i < BM * C) Xs[xb][i] = xr[k];
+    }
+  };
+  auto nvalid = [&](int64_t r0) -> int {
+    const int64_t n = rows - r0;
+    return (int)(n < 0 ? 0 : (n < HB ? n : HB));
+  };
+
+  // wave-local chunk tasks of a half: task i = lane + 64 k -> row i / CPW, chunk CPW w + i % CPW
+  // L0 task k of half h: phases of layer 0 for this wave's features -> (P_0) -> bf16 sin into H[h]
+  auto L0_task = [&](int64_t t, int h, int xb, int k) {
+    const int64_t r0 = t * BM + HB * h;
+    const int nval = nvalid(r0);
+    const __amdgpu_buffer_rsrc_t rs =
+        fused_rsrc(a.P[0] ? (const uint16_t*)a.P[0] + (batch * rows + r0) * F : nullptr,
+                   a.P[0] ? (int64_t)nval * F * 2 : 0);
+    const float* xs = Xs[xb] + HB * h * C;
+    const int i = lane + 64 * k;
+    const int r = i / CPW, cc = CPW * wave + (i % CPW);
+    const f32x4 ba = *(const f32x4*)(Sw0 + C * F + 8 * cc);
+    const f32x4 bb = *(const f32x4*)(Sw0 + C * F + 8 * cc + 4);
+    float z[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) z[e] = 0.f;
+#pragma unroll
+    for (int ci = 0; ci < C; ++ci) {
+      const float xv = xs[r * C + ci];
+      const f32x4 wa = *(const f32x4*)(Sw0 + ci * F + 8 * cc);
+      const f32x4 wc = *(const f32x4*)(Sw0 + ci * F + 8 * cc + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        z[e] = fmaf(xv, wa[e], z[e]);
+        z[e + 4] = fmaf(xv, wc[e], z[e + 4]);
+      }
+    }
+    u16x8 ph;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      ph[e] = PT::enc_scaled(z[e], ba[e], kph);
+      ph[e + 4] = PT::enc_scaled(z[e + 4], bb[e], kph);
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, ph), rs, (r * F + 8 * cc) * 2, 0, 0);
+    bf16x8 hv;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) hv[e] = (bf16)PT::sinp(ph[e]);
+    *(bf16x8*)(Hs[h] + h_off(r, cc)) = hv;
+  };
+
+  // EC of half h, hidden layer lh, in 16 slices: slices 0..7 write two accumulator groups each
+  // (phases, 8-byte LDS writes of 4 features), slices 8..15 take one 16-byte chunk task each
+  // (store to P_{lh+1}, then bf16 sin in place, or the output-layer partial sums if last)
+  auto EC_slice = [&](int64_t t, int h, const f32x16 (&acc)[FB][2], int lh, auto last_tag, int sl) {
+    constexpr bool last = decltype(last_tag)::value;
+    constexpr int ESL = FB * 4;  // epilogue slices (2 of the FB * 8 accumulator groups each)
+    if (sl < ESL) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int gi = 2 * sl + u;
+        const int fb = gi >> 3, g = (gi >> 1) & 3, bm = gi & 1;
+        const int f = 32 * FB * wave + 32 * fb + 8 * g + 4 * hh;
+        const f32x4 bv = *(const f32x4*)(Sb + lh * F + f);
+        u16x4 ph;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ph[e] = PT::enc_scaled(acc[fb][bm][4 * g + e], bv[e], kph);
+        *(u16x4*)(Hs[h] + h_off(32 * bm + j32, f >> 3) + 8 * hh) = ph;
+      }
+      return;
+    }
+    if (sl == ESL) asm volatile("" ::: "memory");  // this wave's phase writes precede its chunk reads
+    const int k = sl - ESL;
+    if (k >= NTASK) return;
+    const int64_t r0 = t * BM + HB * h;
+    const int nval = nvalid(r0);
+    void* Pl = a.P[lh + 1];
+    const __amdgpu_buffer_rsrc_t rs =
+        fused_rsrc(Pl ? (const uint16_t*)Pl + (batch * rows + r0) * F : nullptr, Pl ? (int64_t)nval * F * 2 : 0);
+    const int i = lane + 64 * k;
+    const int r = i / CPW, cc = CPW * wave + (i % CPW);
+    char* hp = Hs[h] + h_off(r, cc);
+    const u16x8 ph = *(const u16x8*)hp;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, ph), rs, (r * F + 8 * cc) * 2, 0, 0);
+    if constexpr (!last) {
+      bf16x8 hv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) hv[e] = (bf16)PT::sinp(ph[e]);
+      *(bf16x8*)hp = hv;
+    } else {
+      float hv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) hv[e] = PT::sinp(ph[e]);
+      for (int o = 0; o < O; ++o) {
+        const f32x4 wa = *(const f32x4*)(Swl + o * F + 8 * cc);
+        const f32x4 wc = *(const f32x4*)(Swl + o * F + 8 * cc + 4);
+        float sacc = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sacc = fmaf(hv[e], wa[e], sacc);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sacc = fmaf(hv[e + 4], wc[e], sacc);
+        // the CPW lanes of a row: DPP butterfly (quad swaps, then row_ror 4 when CPW = 8; the
+        // row's first lane, the only writer, ends with the full sum)
+        sacc += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, sacc), 0xB1, 0xF, 0xF, true));
+        sacc += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, sacc), 0x4E, 0xF, 0xF, true));
+        if constexpr (CPW == 8)
+          sacc += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, sacc), 0x124, 0xF, 0xF, true));
+        if ((i % CPW) == 0) Yp[h][wave][r * FUSED_MAXO + o] += sacc;
+      }
+    }
+  };
+
+  // K(h): acc[fb][bm] (features 64 w + 32 fb, rows 32 bm + j32 of half h) = W_l . H[h]^T, with a
+  // VALU filler(ks) issued after each K step's MFMAs (EC or L0 of the other half); with refill,
+  // each W slot is reloaded with layer `lref` right after its last use
+  auto K = [&](int h, f32x16 (&acc)[FB][2], auto refill, int lref, auto&& filler) {
+#pragma unroll
+    for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+      for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[fb][bm][e] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      bf16x8 hf[2];
+#pragma unroll
+      for (int bm = 0; bm < 2; ++bm) hf[bm] = *(const bf16x8*)(Hs[h] + h_off(32 * bm + j32, 2 * ks + hh));
+#pragma unroll
+      for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+        for (int bm = 0; bm < 2; ++bm)
+          acc[fb][bm] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wreg[fb][ks], hf[bm], acc[fb][bm], 0, 0, 0);
+      if constexpr (decltype(refill)::value) {
+#pragma unroll
+        for (int fb = 0; fb < FB; ++fb) wreg[fb][ks] = wfrag(lref, fb, ks);
+      }
+      filler(ks);
+    }
+  };
+  auto EC = [&](int64_t t, int h, const f32x16 (&acc)[FB][2], int lh, auto last_tag) {
+#pragma unroll
+    for (int sl = 0; sl < FB * 4 + NTASK; ++sl) EC_slice(t, h, acc, lh, last_tag, sl);
+  };
+  auto L0 = [&](int64_t t, int h, int xb) {
+#pragma unroll
+    for (int k = 0; k < NTASK; ++k) L0_task(t, h, xb, k);
+  };
+
+  // Y(h): y rows of half h of tile t from the partial sums; partials reset for reuse
+  auto Ypass = [&](int64_t t, int h) {
+    for (int idx = tid; idx < HB * O; idx += NT) {
+      const int r = idx / O, o = idx - r * O;
+      const int64_t row = t * BM + HB * h + r;
+      float acc = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        acc += Yp[h][w][r * FUSED_MAXO + o];
+        Yp[h][w][r * FUSED_MAXO + o] = 0.f;
+      }
+      float z = acc + Swl[FUSED_MAXO * F + o];
+      if (a.sine_out) z = PT::sinr(w0 * z);
+      if (row < rows) a.y[(batch * rows + row) * O + o] = z;
+    }
+  };
+
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  int64_t t = blockIdx.x;
+  if (t >= ntiles) return;
+  int xb = 0;  // x tile buffer of the current tile (alternates per iteration)
+  x_issue(t);
+  x_park(xb);
+  fused_barrier();
+
+  f32x16 accA[FB][2], accB[FB][2];
+  bool have_prev = false;
+  int64_t tp = -1;
+  for (; t < ntiles; t += G) {
+    const bool more = t + G < ntiles;
+    // seg 0: L0(A) + EC(nh, B) of the previous tile (+ its y rows of half A); x(t + G) issued first
+    if (more) x_issue(t + G);
+    L0(t, 0, xb);
+    if (have_prev) {
+      EC(tp, 1, accB, nh - 1, T_{});
+      Ypass(tp, 0);
+    }
+    fused_barrier();
+    // seg 1: K(1, A) + L0(B) (+ previous tile's y rows of half B); park x(t + G)
+    K(0, accA, F_{}, 0, [&](int ks) {
+      if ((ks & 1) == 0 && (ks >> 1) < NTASK) L0_task(t, 1, xb, ks >> 1);
+    });
+    if (have_prev) Ypass(tp, 1);
+    if (more) x_park(xb ^ 1);
+    fused_barrier();
+    for (int l = 0; l < nh; ++l) {
+      const int lnext = (l + 1 < nh) ? l + 1 : 0;
+      if (l + 1 < nh) {
+        // K(l, B) + EC(l, A); W slots refilled with the next layer
+        K(1, accB, T_{}, lnext, [&](int ks) { EC_slice(t, 0, accA, l, F_{}, ks); });
+        fused_barrier();
+        // K(l + 1, A) + EC(l, B)
+        K(0, accA, F_{}, 0, [&](int ks) { EC_slice(t, 1, accB, l, F_{}, ks); });
+        fused_barrier();
+      } else {
+        // last layer: K(nh, B) + EC(nh, A) with the output layer; slots refilled for the next tile
+        K(1, accB, T_{}, lnext, [&](int ks) { EC_slice(t, 0, accA, l, T_{}, ks); });
+        fused_barrier();
+      }
+    }
+    have_prev = true;
+    tp = t;
+    xb ^= 1;
+  }
+  // drain: EC(nh, B) of the last tile and its y rows
+  EC(tp, 1, accB, nh - 1, T_{});
+  Ypass(tp, 0);
+  fused_barrier();
+  Ypass(tp, 1);
 }
 
 }  // namespace siren

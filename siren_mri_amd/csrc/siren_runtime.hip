@@ -77,6 +77,7 @@ inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 bool g_fused_forward = true;
 bool g_fused_backward = true;
 bool g_fuse_top = false;
+bool g_fwd_pipe = true;  // fused forward: half-tile MFMA/VALU pipelined kernel
 bool g_dx_ring = true;  // 256x256 input-gradient layers on the 4-stage ring kernel
 bool g_dw_ring = true;  // 256x256 weight-gradient layers on the 4-stage ring kernel  // output-layer fusion: measured slower than last_bwd + plain kernels
 long long* g_fused_prof = nullptr;  // debug: per-workgroup phase cycle counters of the fused forward
@@ -462,7 +463,10 @@ int fused_forward(const siren_mlp_desc* d, const Geo& g, const Layout& lo, const
   using KernelFn = void (*)(FusedFwdArgs);
   static const KernelFn table[FUSED_MAXC] = {fused_fwd_bf16_kernel<256, 1>, fused_fwd_bf16_kernel<256, 2>,
                                              fused_fwd_bf16_kernel<256, 3>, fused_fwd_bf16_kernel<256, 4>};
-  hipLaunchKernelGGL(table[a.C - 1], grid, dim3(512), 0, st, a);
+  static const KernelFn pipe[FUSED_MAXC] = {fused_fwd_pipe_kernel<1>, fused_fwd_pipe_kernel<2>,
+                                            fused_fwd_pipe_kernel<3>, fused_fwd_pipe_kernel<4>};
+  const bool use_pipe = g_fwd_pipe && nh > 0;
+  hipLaunchKernelGGL((use_pipe ? pipe : table)[a.C - 1], grid, dim3(use_pipe ? 64 * SIREN_PIPE_NW : 512), 0, st, a);
   tmark_end(SIREN_KCLASS_FWD_FUSED, st);
   return check_launch("fused_fwd");
 }
@@ -1257,6 +1261,10 @@ int siren_config_set(const char* key, int64_t value) {
     g_fuse_top = value != 0;
     return SIREN_OK;
   }
+  if (key && strcmp(key, "fused_forward_pipe") == 0 && (value == 0 || value == 1)) {
+    g_fwd_pipe = value != 0;
+    return SIREN_OK;
+  }
   if (key && strcmp(key, "dw_ring") == 0 && (value == 0 || value == 1)) {
     g_dw_ring = value != 0;
     return SIREN_OK;
@@ -1278,6 +1286,7 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "fuse_output_layer") == 0) return g_fuse_top ? 1 : 0;
   if (key && strcmp(key, "dx_ring") == 0) return g_dx_ring ? 1 : 0;
   if (key && strcmp(key, "dw_ring") == 0) return g_dw_ring ? 1 : 0;
+  if (key && strcmp(key, "fused_forward_pipe") == 0) return g_fwd_pipe ? 1 : 0;
   return -1;
 }
 

@@ -1,0 +1,14 @@
+#!/bin/bash
+# SQ counters of one python workload: bash tools/pmc_kernel.sh TAG script.py [args]
+set -e
+TAG=$1; shift
+R=$(pwd)
+SCRIPT="$R/$1"; shift
+mkdir -p "$R/gpurun_out"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+    SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS \
+    -d "$R/gpurun_out/${TAG}_pmc1" -o run --output-format csv -- python "$SCRIPT" "$@" > "$R/gpurun_out/${TAG}_pmc1.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_WAIT_INST_LDS SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM SQ_INSTS_VALU \
+    SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_SCA \
+    -d "$R/gpurun_out/${TAG}_pmc2" -o run --output-format csv -- python "$SCRIPT" "$@" > "$R/gpurun_out/${TAG}_pmc2.log" 2>&1
