@@ -137,6 +137,28 @@ int siren_timing_collect(double* total_ms, int64_t* launches);
 void siren_timing_disable(void);
 
 /*
+ * Adam step over up to SIREN_ADAM_MAX_TENSORS fp32 parameter tensors in one launch — the
+ * optimizer of training.train (training.py:29, torch.optim.Adam with default flags). The host
+ * passes the step-dependent scalars (torch's non-capturable convention):
+ *   step_size = -lr / (1 - beta1^t),  bias_correction2_sqrt = sqrt(1 - beta2^t).
+ * exp_avg / exp_avg_sq are updated in place, then param. amsgrad is not supported here.
+ */
+#define SIREN_ADAM_MAX_TENSORS 48
+typedef struct siren_adam_desc {
+  int32_t num_tensors;
+  int32_t maximize;
+  float lr, beta1, beta2, eps, weight_decay;
+  float step_size;               /* -lr / (1 - beta1^t) */
+  float bias_correction2_sqrt;   /* sqrt(1 - beta2^t) */
+  int64_t numel[SIREN_ADAM_MAX_TENSORS];
+  float* param[SIREN_ADAM_MAX_TENSORS];
+  const float* grad[SIREN_ADAM_MAX_TENSORS];
+  float* exp_avg[SIREN_ADAM_MAX_TENSORS];
+  float* exp_avg_sq[SIREN_ADAM_MAX_TENSORS];
+} siren_adam_desc;
+int siren_adam_step(const siren_adam_desc* d, void* stream);
+
+/*
  * Process-wide execution options (no reference counterpart; used by tests and benchmarks to
  * compare code paths). Keys:
  *   "fused_forward"  1 (default): bf16 stacks of equal power-of-two hidden widths run their

@@ -38,6 +38,7 @@ EXPORTED_SYMBOLS = (
     "siren_timing_disable",
     "siren_config_set",
     "siren_config_get",
+    "siren_adam_step",
     "siren_last_error",
     "siren_version",
 )
@@ -62,6 +63,30 @@ class SirenMLPDesc(ctypes.Structure):
         ("rows_per_batch", ctypes.c_int64),
         ("weight", ctypes.c_void_p * MAX_LAYERS),
         ("bias", ctypes.c_void_p * MAX_LAYERS),
+    ]
+
+
+ADAM_MAX_TENSORS = 48
+
+
+class SirenAdamDesc(ctypes.Structure):
+    """Mirror of ``siren_adam_desc`` (include/siren_mri_amd.h)."""
+
+    _fields_ = [
+        ("num_tensors", ctypes.c_int32),
+        ("maximize", ctypes.c_int32),
+        ("lr", ctypes.c_float),
+        ("beta1", ctypes.c_float),
+        ("beta2", ctypes.c_float),
+        ("eps", ctypes.c_float),
+        ("weight_decay", ctypes.c_float),
+        ("step_size", ctypes.c_float),
+        ("bias_correction2_sqrt", ctypes.c_float),
+        ("numel", ctypes.c_int64 * ADAM_MAX_TENSORS),
+        ("param", ctypes.c_void_p * ADAM_MAX_TENSORS),
+        ("grad", ctypes.c_void_p * ADAM_MAX_TENSORS),
+        ("exp_avg", ctypes.c_void_p * ADAM_MAX_TENSORS),
+        ("exp_avg_sq", ctypes.c_void_p * ADAM_MAX_TENSORS),
     ]
 
 
@@ -108,6 +133,8 @@ def _declare(lib):
     lib.siren_config_set.restype = ctypes.c_int
     lib.siren_config_get.argtypes = [ctypes.c_char_p]
     lib.siren_config_get.restype = i64
+    lib.siren_adam_step.argtypes = [ctypes.POINTER(SirenAdamDesc), vp]
+    lib.siren_adam_step.restype = ctypes.c_int
     lib.siren_last_error.argtypes = []
     lib.siren_last_error.restype = ctypes.c_char_p
     lib.siren_version.argtypes = []

@@ -1,0 +1,49 @@
+// siren_adam.hip — the Adam update of training.py:29,95 (torch.optim.Adam defaults, non-capturable
+// foreach path on GPU) as ONE launch over every parameter tensor.
+//
+// Per element, in the order of torch's _multi_tensor_adam (fp32 "opmath", host scalars cast to
+// float): g = grad (negated if maximize) (+ wd * param); m = lerp(m, g, 1 - beta1);
+// v = v * beta2; v = v + (1 - beta2) * (g * g); d = sqrt(v) / bc2_sqrt + eps;
+// param = param + step * (m / d), step = -lr / (1 - beta1^t), bc2_sqrt = sqrt(1 - beta2^t).
+#include "siren_common.h"
+
+namespace siren {
+
+struct AdamArgs {
+  float* param[SIREN_ADAM_MAX_TENSORS];
+  const float* grad[SIREN_ADAM_MAX_TENSORS];
+  float* exp_avg[SIREN_ADAM_MAX_TENSORS];
+  float* exp_avg_sq[SIREN_ADAM_MAX_TENSORS];
+  int64_t numel[SIREN_ADAM_MAX_TENSORS];
+  float one_minus_beta1, beta2, one_minus_beta2, eps, weight_decay, step, bc2_sqrt;
+  int maximize;
+};
+
+DEV float torch_lerp(float self, float end, float w) {
+  return fabsf(w) < 0.5f ? self + w * (end - self) : end - (end - self) * (1.f - w);
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
+  const int t = blockIdx.y;
+  const int64_t n = a.numel[t];
+  float* p = a.param[t];
+  const float* gr = a.grad[t];
+  float* m = a.exp_avg[t];
+  float* v = a.exp_avg_sq[t];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float g = gr[i];
+    if (a.maximize) g = -g;
+    const float pv = p[i];
+    if (a.weight_decay != 0.f) g = g + a.weight_decay * pv;
+    const float mv = torch_lerp(m[i], g, a.one_minus_beta1);
+    float vv = v[i] * a.beta2;
+    vv = vv + a.one_minus_beta2 * (g * g);
+    float d = sqrtf(vv) / a.bc2_sqrt;
+    d = d + a.eps;
+    m[i] = mv;
+    v[i] = vv;
+    p[i] = pv + a.step * (mv / d);
+  }
+}
+
+}  // namespace siren

@@ -12,6 +12,7 @@
 #include "siren_gemm.hip"
 #include "siren_jvp.hip"
 #include "siren_fused.hip"
+#include "siren_adam.hip"
 
 using namespace siren;
 
@@ -1246,6 +1247,37 @@ void siren_timing_disable(void) {
     delete[] g_timing.ev;
   }
   g_timing = Timing();
+}
+
+int siren_adam_step(const siren_adam_desc* d, void* stream) {
+  if (!d || d->num_tensors < 0 || d->num_tensors > SIREN_ADAM_MAX_TENSORS)
+    return fail(SIREN_EINVAL, "adam: num_tensors outside [0, %d]", SIREN_ADAM_MAX_TENSORS);
+  if (d->num_tensors == 0) return SIREN_OK;
+  AdamArgs a;
+  memset(&a, 0, sizeof(a));
+  int64_t maxn = 0;
+  for (int t = 0; t < d->num_tensors; ++t) {
+    if (!d->param[t] || !d->grad[t] || !d->exp_avg[t] || !d->exp_avg_sq[t] || d->numel[t] < 0)
+      return fail(SIREN_EINVAL, "adam: tensor %d has a null pointer or negative size", t);
+    a.param[t] = d->param[t];
+    a.grad[t] = d->grad[t];
+    a.exp_avg[t] = d->exp_avg[t];
+    a.exp_avg_sq[t] = d->exp_avg_sq[t];
+    a.numel[t] = d->numel[t];
+    maxn = std::max(maxn, d->numel[t]);
+  }
+  a.one_minus_beta1 = (float)(1.0 - (double)d->beta1);
+  a.beta2 = d->beta2;
+  a.one_minus_beta2 = (float)(1.0 - (double)d->beta2);
+  a.eps = d->eps;
+  a.weight_decay = d->weight_decay;
+  a.step = d->step_size;
+  a.bc2_sqrt = d->bias_correction2_sqrt;
+  a.maximize = d->maximize;
+  if (maxn == 0) return SIREN_OK;
+  hipLaunchKernelGGL(adam_kernel, dim3(grid1d(maxn, 1024), (unsigned)d->num_tensors), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  return check_launch("adam");
 }
 
 int siren_config_set(const char* key, int64_t value) {

@@ -1,0 +1,94 @@
+"""Adam for the fitting loop (training.py:29: torch.optim.Adam(lr=lr, params=model.parameters())).
+
+`Adam` is torch.optim.Adam — same constructor, param_groups, state keys ('step', 'exp_avg',
+'exp_avg_sq') and state_dict, so checkpoints move freely between the two — whose step() runs ONE
+native launch (siren_adam_step) over all fp32 CUDA parameters of a group instead of torch's
+chain of foreach kernels, with the foreach path's arithmetic (see csrc/siren_adam.hip).
+Groups it cannot take (amsgrad, capturable/differentiable/fused flags, non-fp32 or CPU tensors,
+sparse gradients, tensor-valued lr/betas) go through torch's own step().
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from . import _native
+
+
+class Adam(torch.optim.Adam):
+    def _native_ok(self, group) -> bool:
+        if group["amsgrad"] or group.get("capturable") or group.get("differentiable") or group.get("fused"):
+            return False
+        if group.get("decoupled_weight_decay", False):
+            return False
+        if any(isinstance(group[k], torch.Tensor) for k in ("lr",)) or any(
+                isinstance(b, torch.Tensor) for b in group["betas"]):
+            return False
+        for p in group["params"]:
+            if p.grad is None:
+                continue
+            if (not p.is_cuda or p.dtype != torch.float32 or p.grad.is_sparse or p.grad.dtype != torch.float32
+                    or not p.is_contiguous() or not p.grad.is_contiguous()):
+                return False
+        return True
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        fallback = [g for g in self.param_groups if not self._native_ok(g)]
+        fallback_ids = {id(g) for g in fallback}
+        if fallback:
+            # torch's step over the groups we do not take (the native ones are skipped below)
+            saved = self.param_groups
+            self.param_groups = fallback
+            try:
+                super().step()
+            finally:
+                self.param_groups = saved
+        lib = _native.lib()
+        for group in self.param_groups:
+            if id(group) in fallback_ids:
+                continue
+            beta1, beta2 = group["betas"]
+            params = [p for p in group["params"] if p.grad is not None]
+            # lazy state init exactly as torch.optim.Adam._init_group (step on the CPU, fp32)
+            for p in params:
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            # tensors sharing a step count go together (normally: all of them)
+            by_step = {}
+            for p in params:
+                st = self.state[p]
+                st["step"] += 1
+                by_step.setdefault(float(st["step"].item()), []).append(p)
+            stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+            for t, plist in by_step.items():
+                bc1 = 1 - beta1 ** t
+                bc2 = 1 - beta2 ** t
+                for i0 in range(0, len(plist), _native.ADAM_MAX_TENSORS):
+                    chunk = plist[i0:i0 + _native.ADAM_MAX_TENSORS]
+                    d = _native.SirenAdamDesc()
+                    d.num_tensors = len(chunk)
+                    d.maximize = 1 if group["maximize"] else 0
+                    d.lr, d.beta1, d.beta2 = group["lr"], beta1, beta2
+                    d.eps, d.weight_decay = group["eps"], group["weight_decay"]
+                    d.step_size = (group["lr"] / bc1) * -1
+                    d.bias_correction2_sqrt = bc2 ** 0.5
+                    for k, p in enumerate(chunk):
+                        st = self.state[p]
+                        d.numel[k] = p.numel()
+                        d.param[k] = p.data_ptr()
+                        d.grad[k] = p.grad.data_ptr()
+                        d.exp_avg[k] = st["exp_avg"].data_ptr()
+                        d.exp_avg_sq[k] = st["exp_avg_sq"].data_ptr()
+                    if lib.siren_adam_step(ctypes.byref(d), stream) != 0:
+                        raise _native.NativeError(_native.last_error())
+        return loss

@@ -80,11 +80,10 @@ def compute_loss(losses, loss_schedules, total_steps, writer):
 
 
 def make_adam(params, lr):
-    """torch.optim.Adam as training.py:29 builds it; on GPU parameters the single-kernel (fused)
-    implementation of the same update rule, instead of the multi-launch foreach one."""
-    params = list(params)
-    fused = len(params) > 0 and all(p.is_cuda for p in params)
-    return torch.optim.Adam(lr=lr, params=params, fused=fused)
+    """The optimizer of training.py:29 (torch.optim.Adam(lr=lr, params=...)): siren_mri_amd.optim.Adam,
+    torch's Adam with the update of all fp32 CUDA parameters in one native launch."""
+    from .optim import Adam
+    return Adam(params, lr=lr)
 
 
 def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_checkpoint, model_dir, loss_fn,

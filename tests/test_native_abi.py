@@ -93,3 +93,14 @@ def test_empty_input_rejected():
     d = _desc([2, 64, 1], rows_per_batch=0)
     assert lib.siren_mlp_check(ctypes.byref(d)) != 0
     assert "empty" in _native.last_error()
+
+
+def test_adam_rejects_bad_descriptors():
+    lib = _native.load_library()
+    d = _native.SirenAdamDesc()
+    d.num_tensors = 49
+    assert lib.siren_adam_step(ctypes.byref(d), None) != 0
+    d.num_tensors = 1  # null pointers
+    assert lib.siren_adam_step(ctypes.byref(d), None) != 0
+    d.num_tensors = 0
+    assert lib.siren_adam_step(ctypes.byref(d), None) == 0
