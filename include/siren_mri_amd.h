@@ -167,6 +167,8 @@ int siren_adam_step(const siren_adam_desc* d, void* stream);
  *                    the bottom hidden layer's input-gradient kernel (when no input gradient is
  *                    requested), and the output layer into the top hidden layer's kernels when
  *                    "fuse_output_layer" is 1 (default 0); 0: separate kernels.
+ *   "ring_output_fusion"  1 (default): the output layer's backward runs inside the top 256x256
+ *                    layer's ring kernels (bf16, outermost_linear, O <= 2); 0: last_bwd kernel.
  *   "dx_ring"        1 (default): 256x256 bf16 input-gradient layers use the 4-stage
  *                    load pipeline kernel; 0: the double-buffered one.
  *   "fused_forward_pipe"  1 (default): the fused forward overlaps one half-tile's MFMA work with

@@ -850,12 +850,16 @@ DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMCNT) : "memory")
 // REC (with BOTC > 0): P_0 was not kept by the forward; the epilogue recomputes each phase from
 // the staged x tile, W_0 and b_0 with the forward's arithmetic (first layer of fused_fwd_bf16 /
 // first_fwd: fmaf chain over the inputs, then PT::encz), so cos(P_0) is bit-identical.
-template <int BOTC, bool DXOUT, bool REC = false>
+// TOPO > 0 (top hidden layer, outermost_linear, O = TOPO outputs): the A operand dZ_top is not
+// read; the ring carries P_top (in the A image) and the dy tile, and a pass forms
+// dZ_top = (dy W_L) cos(P_top) w0 in place exactly as last_bwd_kernel does.
+template <int BOTC, bool DXOUT, bool REC = false, int TOPO = 0>
 __global__ __launch_bounds__(512) void dx_ring_bf16_kernel(NTArgs a) {
   using PT = Prec<kPrecBF16>;
   constexpr int K = 256, N = 256, BM = RING_BM, S = RING_S;
   constexpr int X_BYTES = BOTC > 0 ? BM * BOTC * 4 : 0;
-  constexpr int A_BYTES = BM * K * 2, C_BYTES = BM * N * 2, STAGE = A_BYTES + C_BYTES + X_BYTES;
+  constexpr int G_BYTES = TOPO > 0 ? BM * TOPO * 4 : 0;
+  constexpr int A_BYTES = BM * K * 2, C_BYTES = BM * N * 2, STAGE = A_BYTES + C_BYTES + X_BYTES + G_BYTES;
   constexpr int NKS = K / 16;
   constexpr int A_CPR = K / 8, C_CPR = N / 8;   // 16-byte chunks per row
   constexpr int SMASK = 15;
@@ -867,8 +871,9 @@ __global__ __launch_bounds__(512) void dx_ring_bf16_kernel(NTArgs a) {
   constexpr int NST = BOT ? (DXOUT ? NQ : 0) : NQ;  // vector stores per thread per tile
   // VMEM ops issued after stage i's DMA when iteration i waits for it: the stores of the S-1
   // previous tiles and the DMAs of the S-2 stages issued in between.
-  constexpr int NX = BOT ? 1 : 0;               // x DMA instructions per wave per stage
+  constexpr int NX = (BOT ? 1 : 0) + (TOPO > 0 ? 1 : 0);  // x / dy DMA instructions per wave per stage
   constexpr int STEADY = (S - 1) * NST + (S - 2) * (NA + NP + NX);
+  static_assert(TOPO <= TOP_MAXO && !(TOPO > 0 && BOTC > 0), "output-layer fusion: top layer only");
   static_assert(!DXOUT || BOT, "dx output belongs to the first-layer fusion");
   __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
 
@@ -917,10 +922,20 @@ __global__ __launch_bounds__(512) void dx_ring_bf16_kernel(NTArgs a) {
     bcol0 = a.bot.b0[batch * a.bot.b0_bstride + col];
   }
 
+  // TOP: this thread's W_L columns for the in-place dZ_top pass (chunk tid % 32 is fixed)
+  float twl[TOPO > 0 ? TOPO : 1][8];
+  if constexpr (TOPO > 0) {
+#pragma unroll
+    for (int o = 0; o < TOPO; ++o)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) twl[o][e] = a.top.WL[batch * a.top.wl_bstride + (int64_t)o * K + 8 * (tid & 31) + e];
+  }
+
   auto a_off = [&](int r, int c) -> int { return r * K * 2 + ((c ^ (r & SMASK)) << 4); };
   auto dma = [&](int64_t t, int st) {
     char* base = smem + st * STAGE;
     const int64_t m0 = t * BM;
+    const void* asrc = TOPO > 0 ? a.top.Ptop : a.A;
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
       const int i = wave + 8 * k;
@@ -928,8 +943,16 @@ __global__ __launch_bounds__(512) void dx_ring_bf16_kernel(NTArgs a) {
       const int r = u / A_CPR, p = u - r * A_CPR;
       const int c = p ^ (r & SMASK);
       const int64_t row = min(m0 + r, rows - 1);
-      __builtin_amdgcn_global_load_lds((const void*)((const bf16*)a.A + (rowbase + row) * K + c * 8),
+      __builtin_amdgcn_global_load_lds((const void*)((const bf16*)asrc + (rowbase + row) * K + c * 8),
                                        (lds_void*)(base + i * 1024), 16, 0, 0);
+    }
+    if constexpr (TOPO > 0) {
+      // dy rows [m0, m0 + BM): BM*O floats; wave w moves bytes [16 O w, 16 O (w + 1)) (O lanes)
+      if (lane < TOPO) {
+        const int64_t el = min((m0 + rowbase) * TOPO + 4 * (TOPO * wave + lane), (rowbase + rows) * TOPO - 4);
+        __builtin_amdgcn_global_load_lds((const void*)(a.top.dy + el),
+                                         (lds_void*)(base + A_BYTES + C_BYTES + X_BYTES + 16 * TOPO * wave), 16, 0, 0);
+      }
     }
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
@@ -965,6 +988,30 @@ __global__ __launch_bounds__(512) void dx_ring_bf16_kernel(NTArgs a) {
     lds_barrier();
     if (i + S - 1 < niter) dma(t0 + (i + S - 1) * G, (int)((i + S - 1) % S));
     char* base = smem + st * STAGE;
+    if constexpr (TOPO > 0) {
+      // dZ_top = (dy W_L) cos(P_top) w0 over the staged phases, in place (last_bwd's arithmetic)
+      const float* gt = (const float*)(base + A_BYTES + C_BYTES + X_BYTES);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int u = tid + 512 * q;
+        const int r = u / A_CPR, c = u - r * A_CPR;
+        char* p = base + a_off(r, c);
+        const u16x8 ph = *(const u16x8*)p;
+        float g[TOP_MAXO];
+#pragma unroll
+        for (int o = 0; o < TOP_MAXO; ++o) g[o] = o < TOPO ? gt[r * TOPO + o] : 0.f;
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float dh = 0.f;
+#pragma unroll
+          for (int o = 0; o < TOP_MAXO; ++o) dh = fmaf(g[o], o < TOPO ? twl[o < TOPO ? o : 0][e] : 0.f, dh);
+          v[e] = (bf16)((dh * PT::cosp(ph[e])) * a.w0);
+        }
+        *(bf16x8*)p = v;
+      }
+      lds_barrier();
+    }
     f32x16 acc;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
@@ -1088,16 +1135,22 @@ namespace siren {
 // ------------------------------------------------------------------------------------------
 // RECC > 0: layer 1 with P_0 not kept by the forward: the x tile (RECC inputs) rides in the ring
 // instead of P_0, and the convert pass recomputes the phases exactly as the forward did.
-template <int RECC = 0>
+// TOPO > 0: the top hidden layer with the output layer folded in (outermost_linear, O = TOPO): the
+// ring carries P_top (in the dZ image) and the dy tile; the convert pass forms dZ_top in place
+// (last_bwd_kernel's arithmetic) and sums the output layer's dW_L = dy^T sin(P_top), db_L = sum dy
+// into per-workgroup slabs (a.top.partL).
+template <int RECC = 0, int TOPO = 0>
 __global__ __launch_bounds__(512) void dw_ring_bf16_kernel(TNArgs a) {
   using PT = Prec<kPrecBF16>;
   constexpr int M = 256, N = 256, KC = 32, S = RING_S;
   constexpr int X_BYTES = RECC > 0 ? KC * RECC * 4 : 0;
-  constexpr int D_BYTES = KC * M * 2, P_BYTES = KC * N * 2, STAGE = D_BYTES + P_BYTES + X_BYTES;
+  constexpr int G_BYTES = TOPO > 0 ? KC * TOPO * 4 : 0;
+  constexpr int D_BYTES = KC * M * 2, P_BYTES = KC * N * 2, STAGE = D_BYTES + P_BYTES + X_BYTES + G_BYTES;
   constexpr int CPR = 32;                                  // 16-byte chunks per row (both)
-  constexpr int ND = KC * CPR / 64 / 8;                    // DMA instrs per wave per stage
+  constexpr int ND = KC * CPR / 64 / 8 + (TOPO > 0 ? 1 : 0);  // DMA instrs per wave per stage
   constexpr int NP = RECC > 0 ? 1 : KC * CPR / 64 / 8;
   constexpr int STEADY = (S - 2) * (ND + NP);
+  static_assert(!(RECC > 0 && TOPO > 0), "one hidden layer: the plain output-layer path");
   __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
 
   const int tid = threadIdx.x;
@@ -1121,8 +1174,16 @@ __global__ __launch_bounds__(512) void dw_ring_bf16_kernel(TNArgs a) {
       const int r = 2 * i + (lane >> 5), p = lane & 31;
       const int64_t row = min(r0 + r, r_end - 1);
       __builtin_amdgcn_global_load_lds(
-          (const void*)((const bf16*)a.D + (rowbase + row) * M + 8 * swz(r, p)),
+          (const void*)((const bf16*)(TOPO > 0 ? a.top.Ptop : a.D) + (rowbase + row) * M + 8 * swz(r, p)),
           (lds_void*)(base + i * 1024), 16, 0, 0);
+    }
+    if constexpr (TOPO > 0) {
+      if (lane < TOPO) {
+        const int64_t el = min((r0 + rowbase) * TOPO + 4 * (TOPO * wave + lane), (rowbase + r_end) * TOPO - 4);
+        __builtin_amdgcn_global_load_lds((const void*)(a.top.dy + el),
+                                         (lds_void*)(base + D_BYTES + P_BYTES + X_BYTES + 16 * TOPO * wave), 16, 0,
+                                         0);
+      }
     }
     if constexpr (RECC > 0) {
       // x rows [r0, r0 + KC): wave w moves bytes [16 C w, 16 C (w + 1)) (C lanes)
@@ -1164,6 +1225,18 @@ __global__ __launch_bounds__(512) void dw_ring_bf16_kernel(TNArgs a) {
     b0r[e] = 0.f;
 #pragma unroll
     for (int c = 0; c < CR; ++c) w0r[e][c] = 0.f;
+  }
+  // TOPO: W_L columns of this thread's chunk, dW_L / db_L sums
+  constexpr int TO = TOPO > 0 ? TOPO : 1;
+  float twl[TO][8], tdw[TO][8], tdb[TO];
+#pragma unroll
+  for (int o = 0; o < TO; ++o) {
+    tdb[o] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      tdw[o][e] = 0.f;
+      twl[o][e] = TOPO > 0 ? a.top.WL[batch * a.top.wl_bstride + (int64_t)o * M + 8 * cth + e] : 0.f;
+    }
   }
   if constexpr (RECC > 0) {
     const float* W0 = a.rec_W0 + batch * a.rec_w0_bstride;
@@ -1211,6 +1284,35 @@ __global__ __launch_bounds__(512) void dw_ring_bf16_kernel(TNArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) hv[e] = (bf16)(valid ? PT::sinp(ph[e]) : 0.f);
       *(bf16x8*)(Pb + off) = hv;
+      if constexpr (TOPO > 0) {
+        // dZ_top in place over the staged P_top phases; output-layer sums on valid rows
+        const float* gt = (const float*)(Pb + P_BYTES + X_BYTES) + r * TOPO;
+        const u16x8 pt = *(const u16x8*)(Db + off);
+        float g[TOP_MAXO];
+#pragma unroll
+        for (int o = 0; o < TOP_MAXO; ++o) g[o] = o < TOPO ? gt[o] : 0.f;
+        bf16x8 dz;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float dh = 0.f;
+#pragma unroll
+          for (int o = 0; o < TOP_MAXO; ++o) dh = fmaf(g[o], o < TOPO ? twl[o < TOPO ? o : 0][e] : 0.f, dh);
+          dz[e] = (bf16)((dh * PT::cosp(pt[e])) * a.w0);
+        }
+        *(bf16x8*)(Db + off) = dz;
+        if (valid) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float sv = PT::sinp(pt[e]);
+#pragma unroll
+            for (int o = 0; o < TO; ++o) tdw[o][e] = fmaf(g[o], sv, tdw[o][e]);
+          }
+          if (cth == 0) {
+#pragma unroll
+            for (int o = 0; o < TO; ++o) tdb[o] += g[o];
+          }
+        }
+      }
       if (valid) {
         const bf16x8 dv = *(const bf16x8*)(Db + off);
 #pragma unroll
@@ -1267,6 +1369,27 @@ __global__ __launch_bounds__(512) void dw_ring_bf16_kernel(TNArgs a) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) sum += red[k * 256 + tid];
     part[(int64_t)M * N + tid] = sum;
+  }
+  if constexpr (TOPO > 0) {
+    // dW_L [O][M] and db_L [O] over the 16 row slots
+    __syncthreads();
+    constexpr int RS = TOPO * 256 + TOPO;
+#pragma unroll
+    for (int o = 0; o < TOPO; ++o)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[rth * RS + o * 256 + 8 * cth + e] = tdw[o][e];
+    if (cth == 0) {
+#pragma unroll
+      for (int o = 0; o < TOPO; ++o) red[rth * RS + TOPO * 256 + o] = tdb[o];
+    }
+    __syncthreads();
+    float* pl = a.top.partL + (int64_t)split * a.top.partL_stride + batch * (int64_t)RS;
+    for (int idx = tid; idx < RS; idx += 512) {
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) sum += red[k * RS + idx];
+      pl[idx] = sum;
+    }
   }
 }
 

@@ -78,6 +78,7 @@ inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 bool g_fused_forward = true;
 bool g_fused_backward = true;
 bool g_fuse_top = false;
+bool g_ring_top = true;  // output layer folded into the top 256x256 layer's ring kernels
 bool g_fwd_pipe = true;  // fused forward: half-tile MFMA/VALU pipelined kernel
 bool g_dx_ring = true;  // 256x256 input-gradient layers on the 4-stage ring kernel
 bool g_dw_ring = true;  // 256x256 weight-gradient layers on the 4-stage ring kernel  // output-layer fusion: measured slower than last_bwd + plain kernels
@@ -232,8 +233,8 @@ Layout layout_of(const siren_mlp_desc* d) {
   lo.partL_off = off;
   if (g.L >= 3) {
     const int F = d->dims[g.L - 1], O = d->dims[g.L];
-    const Split s = tn_split(g, F, d->dims[g.L - 2]);
-    off = align_up(off + s.nsplit * split_stride(g, (int64_t)O * F + O) * 4, 256);
+    const int64_t ns = std::max(tn_split(g, F, d->dims[g.L - 2]).nsplit, dw_ring_split(g).nsplit);
+    off = align_up(off + ns * split_stride(g, (int64_t)O * F + O) * 4, 256);
   }
   lo.xcopy_off = off;
   if (lo.p0_rec) off = align_up(off + g.total * d->dims[0] * 4, 256);
@@ -581,8 +582,11 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
       return fail(SIREN_ELAUNCH, "x copy: %s", hipGetErrorString(hipGetLastError()));
     x = (const float*)(ws + lo.xcopy_off);
   }
-  const bool top = fuse && g_fuse_top && d->outermost_linear && O <= TOP_MAXO && (g.rows * O) % 4 == 0 && g.rows * O >= 4 &&
-                   aligned16(dy) && d->dims[g.L - 1] <= 256 && !(rec && g.L == 3);
+  const bool top_ok = fuse && d->outermost_linear && O <= TOP_MAXO && (g.rows * O) % 4 == 0 && g.rows * O >= 4 &&
+                      aligned16(dy) && !(rec && g.L == 3);
+  // output layer folded into the top layer's ring kernels (256x256 top layer below another layer)
+  const bool ring_top = top_ok && g_ring_top && g.L >= 4 && d->dims[g.L - 1] == 256 && d->dims[g.L - 2] == 256;
+  const bool top = ring_top || (top_ok && g_fuse_top && d->dims[g.L - 1] <= 256);
   // first-layer fusion: the ring kernel (256x256 bottom layer) also produces dx; the older
   // kernel only without dx
   const bool ring_bot = rec || (fuse && g_dx_ring && !wide_input(d) && C <= BOT_MAXC && F0 == 256 &&
@@ -635,7 +639,8 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
     const bool is_top = top && l == g.L - 2;
     const bool is_bot = bot && l == 1;
     const bool rec1 = rec && l == 1;
-    const bool ring = rec1 || (PREC == kPrecBF16 && g_dw_ring && !is_top && M == 256 && N == 256);
+    const bool ring_t = ring_top && l == g.L - 2;
+    const bool ring = rec1 || ring_t || (PREC == kPrecBF16 && g_dw_ring && !is_top && M == 256 && N == 256);
     {
       const Split s = ring ? dw_ring_split(g) : tn_split(g, M, N);
       TNArgs a;
@@ -668,6 +673,9 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
             case 3: hipLaunchKernelGGL((dw_ring_bf16_kernel<3>), rg, dim3(512), 0, st, a); break;
             default: hipLaunchKernelGGL((dw_ring_bf16_kernel<4>), rg, dim3(512), 0, st, a); break;
           }
+        } else if (ring_t) {
+          if (O == 1) hipLaunchKernelGGL((dw_ring_bf16_kernel<0, 1>), rg, dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((dw_ring_bf16_kernel<0, 2>), rg, dim3(512), 0, st, a);
         } else if (ring)
           hipLaunchKernelGGL((dw_ring_bf16_kernel<0>), rg, dim3(512), 0, st, a);
         else if (is_top) hipLaunchKernelGGL((tn_dw_kernel<PREC, false, true>), grid, dim3(256), 0, st, a);
@@ -717,6 +725,12 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
         if (is_bot && ring_bot) {
           a.C = dx;  // [rows, C] f32, or not written
           rc = launch_dx_ring_bot(a, g.nb, C, dx != nullptr, rec1, SIREN_KCLASS_DX_GEMM, st);
+        } else if (ring_t) {
+          tmark_begin(SIREN_KCLASS_DX_GEMM, st);
+          if (O == 1) hipLaunchKernelGGL((dx_ring_bf16_kernel<0, false, false, 1>), ring_grid(a, g.nb), dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((dx_ring_bf16_kernel<0, false, false, 2>), ring_grid(a, g.nb), dim3(512), 0, st, a);
+          tmark_end(SIREN_KCLASS_DX_GEMM, st);
+          rc = check_launch("dx_ring top");
         } else if (is_top && is_bot) rc = launch_nt<PREC, MODE_DX, true, true>(a, g.nb, SIREN_KCLASS_DX_GEMM, st);
         else if (is_top) rc = launch_nt<PREC, MODE_DX, true, false>(a, g.nb, SIREN_KCLASS_DX_GEMM, st);
         else if (is_bot) rc = launch_nt<PREC, MODE_DX, false, true>(a, g.nb, SIREN_KCLASS_DX_GEMM, st);
@@ -1289,6 +1303,10 @@ int siren_config_set(const char* key, int64_t value) {
     g_fused_backward = value != 0;
     return SIREN_OK;
   }
+  if (key && strcmp(key, "ring_output_fusion") == 0 && (value == 0 || value == 1)) {
+    g_ring_top = value != 0;
+    return SIREN_OK;
+  }
   if (key && strcmp(key, "fuse_output_layer") == 0 && (value == 0 || value == 1)) {
     g_fuse_top = value != 0;
     return SIREN_OK;
@@ -1316,6 +1334,7 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "fused_forward") == 0) return g_fused_forward ? 1 : 0;
   if (key && strcmp(key, "fused_backward") == 0) return g_fused_backward ? 1 : 0;
   if (key && strcmp(key, "fuse_output_layer") == 0) return g_fuse_top ? 1 : 0;
+  if (key && strcmp(key, "ring_output_fusion") == 0) return g_ring_top ? 1 : 0;
   if (key && strcmp(key, "dx_ring") == 0) return g_dx_ring ? 1 : 0;
   if (key && strcmp(key, "dw_ring") == 0) return g_dw_ring ? 1 : 0;
   if (key && strcmp(key, "fused_forward_pipe") == 0) return g_fwd_pipe ? 1 : 0;

@@ -28,7 +28,7 @@ def test_adam_matches_torch_foreach(kw):
     torch.cuda.synchronize()
     for p, q in zip(ours, ref):
         torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-6, atol=1e-7)
-        torch.testing.assert_close(o1.state[p]["exp_avg"], o2.state[q]["exp_avg"], rtol=1e-6, atol=1e-8)
+        torch.testing.assert_close(o1.state[p]["exp_avg"], o2.state[q]["exp_avg"], rtol=1e-6, atol=1e-7)
         torch.testing.assert_close(o1.state[p]["exp_avg_sq"], o2.state[q]["exp_avg_sq"], rtol=1e-6, atol=1e-10)
         assert float(o1.state[p]["step"]) == float(o2.state[q]["step"])
 
