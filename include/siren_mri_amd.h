@@ -132,6 +132,7 @@ int siren_jvp_backward(const siren_mlp_desc* d, int order, const float* x, const
 #define SIREN_KCLASS_DX_GEMM 2  /* hidden-layer input-gradient GEMM + cos-weighted epilogue */
 #define SIREN_KCLASS_DW_GEMM 3  /* hidden-layer weight-gradient split-K GEMM               */
 #define SIREN_KCLASS_FWD_FUSED 4 /* whole forward in one kernel (bf16, narrow in/out layers) */
+#define SIREN_KCLASS_BWD_FUSED 5 /* a middle layer's input + weight gradients in one kernel   */
 int siren_timing_enable(int kernel_class, int max_launches);
 int siren_timing_collect(double* total_ms, int64_t* launches);
 void siren_timing_disable(void);
@@ -148,6 +149,8 @@ typedef struct siren_adam_desc {
   int32_t num_tensors;
   int32_t maximize;
   float lr, beta1, beta2, eps, weight_decay;
+  float one_minus_beta1;         /* 1 - beta1, computed in double then rounded (as torch does) */
+  float one_minus_beta2;         /* 1 - beta2, likewise */
   float step_size;               /* -lr / (1 - beta1^t) */
   float bias_correction2_sqrt;   /* sqrt(1 - beta2^t) */
   int64_t numel[SIREN_ADAM_MAX_TENSORS];
@@ -173,6 +176,8 @@ int siren_adam_step(const siren_adam_desc* d, void* stream);
  *                    load pipeline kernel; 0: the double-buffered one.
  *   "fused_forward_pipe"  1 (default): the fused forward overlaps one half-tile's MFMA work with
  *                    the other's epilogue; 0: the sequential single-kernel forward.
+ *   "bwd_ring"       0 (default), 1: middle 256x256 bf16 layers compute both gradients in one
+ *                    kernel (dZ and P read once); 0: separate input/weight-gradient kernels.
  *   "dw_ring"        1 (default): 256x256 bf16 weight-gradient layers use the ring kernel
  *                    (one full 256x256 partial per workgroup); 0: 128x128-tile split-K kernel.
  *   "debug_fused_profile"  device address of an int64 buffer [grid][4] that receives per-

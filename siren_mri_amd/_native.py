@@ -47,6 +47,7 @@ KCLASS_FWD_GEMM = 1
 KCLASS_DX_GEMM = 2
 KCLASS_DW_GEMM = 3
 KCLASS_FWD_FUSED = 4
+KCLASS_BWD_FUSED = 5
 
 
 class SirenMLPDesc(ctypes.Structure):
@@ -80,6 +81,8 @@ class SirenAdamDesc(ctypes.Structure):
         ("beta2", ctypes.c_float),
         ("eps", ctypes.c_float),
         ("weight_decay", ctypes.c_float),
+        ("one_minus_beta1", ctypes.c_float),
+        ("one_minus_beta2", ctypes.c_float),
         ("step_size", ctypes.c_float),
         ("bias_correction2_sqrt", ctypes.c_float),
         ("numel", ctypes.c_int64 * ADAM_MAX_TENSORS),

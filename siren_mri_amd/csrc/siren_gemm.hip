@@ -1394,3 +1394,216 @@ __global__ __launch_bounds__(512) void dw_ring_bf16_kernel(TNArgs a) {
 }
 
 }  // namespace siren
+
+namespace siren {
+
+// ------------------------------------------------------------------------------------------
+// bwd_ring: one 256 x 256 hidden layer's whole backward in one pass over its inputs —
+//   dZ_{l-1} = (dZ_l W_l) cos(P_{l-1}) w0          (input gradient, as dx_ring_bf16_kernel)
+//   dW_l += dZ_l^T sin(P_{l-1}), db_l += sum dZ_l   (weight gradient, as dw_ring_bf16_kernel)
+// so dZ_l and P_{l-1} are read from HBM once instead of twice.
+//
+// One wave per SIMD (4 waves, up to 512 registers): wave w holds the 64 input-gradient columns
+// [64 w, +64) (W_l^T slice, 128 VGPRs) and a 128 x 128 block of the dW partial (256 accumulator
+// registers, AGPRs). 32-row tiles of dZ_l and P_{l-1} (32 KB) stream through a 4-stage DMA ring;
+// per tile: input-gradient MFMAs -> epilogue (dZ_{l-1} to an output tile, sin(P) in place) ->
+// barrier -> weight-gradient MFMAs on transposing fragment reads -> coalesced dZ_{l-1} stores.
+// Each workgroup owns a contiguous row range (a.rows_per_split) and writes one dW/db slab.
+// ------------------------------------------------------------------------------------------
+struct BwdArgs {
+  const bf16* dZ;        // [rows, 256] grad_t (dZ_l)
+  const uint16_t* P;     // [rows, 256] phase (P_{l-1})
+  const bf16* Wt;        // [nb_w][256 (out cols), 256 (K)] op_t = W_l^T rows
+  bf16* dZo;             // [rows, 256] grad_t (dZ_{l-1})
+  float* part;           // [split][nb][256*256 + 256] dW / db partials
+  int64_t rows_per_batch;
+  int64_t rows_per_split;
+  int64_t split_stride;
+  int64_t w_bstride;
+  float w0;
+};
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void bwd_ring_bf16_kernel(BwdArgs a) {
+  using PT = Prec<kPrecBF16>;
+  constexpr int F = 256, BM = 32, S = RING_S, NT = 256;
+  // rows padded to 544 B: every LDS address is a per-lane base plus a compile-time offset, and
+  // the 4-row transposing reads hit 4 disjoint bank groups. Each DMA instruction moves one row
+  // (the 32 low lanes; the high half is masked off).
+  constexpr int RS = F * 2 + 32;
+  constexpr int T_BYTES = BM * RS;                     // one padded 32 x 256 2-byte tile
+  constexpr int STAGE = 2 * T_BYTES;                   // dZ_l tile, P tile
+  constexpr int O_BYTES = BM * F * 2;                  // output tile (linear rows)
+  constexpr int NKS = F / 16;
+  constexpr int NDMA = BM / 4;                         // DMA instructions per wave per tile and operand (8)
+  constexpr int NST = O_BYTES / 16 / NT;               // 16-byte stores per thread per tile (4)
+  constexpr int STEADY = (S - 1) * NST + (S - 2) * 2 * NDMA;
+  static_assert(STEADY == 44, "counted wait below");
+  __shared__ __attribute__((aligned(16))) char smem[S * STAGE + O_BYTES];
+  char* const Obuf = smem + S * STAGE;                 // dZ_{l-1} output tile
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int split = blockIdx.x;
+  const int64_t batch = blockIdx.y;
+  const int64_t rows = a.rows_per_batch;
+  const int64_t rowbase = batch * rows;
+  const int64_t r_begin = (int64_t)split * a.rows_per_split;
+  int64_t r_end = r_begin + a.rows_per_split;
+  if (r_end > rows) r_end = rows;
+  const int64_t ntile = r_end > r_begin ? (r_end - r_begin + BM - 1) / BM : 0;
+
+  auto off = [&](int r, int c) -> int { return r * RS + (c << 4); };
+
+  // input-gradient B operand: W_l^T rows of this wave's 64 columns
+  bf16x8 wf[2][NKS];
+  {
+    const bf16* Wb = a.Wt + batch * a.w_bstride;
+#pragma unroll
+    for (int fb = 0; fb < 2; ++fb)
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+        wf[fb][ks] = *(const bf16x8*)(Wb + (int64_t)(64 * wave + 32 * fb + r32) * F + 16 * ks + 8 * h);
+  }
+
+  auto dma = [&](int64_t k, int st) {
+    char* base = smem + st * STAGE;
+    const int64_t r0 = r_begin + k * BM;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const uint16_t* src = t == 0 ? (const uint16_t*)a.dZ : a.P;
+#pragma unroll
+      for (int j = 0; j < NDMA; ++j) {
+        const int r = wave + 4 * j;                  // one row per instruction
+        const int64_t row = min(r0 + r, r_end - 1);
+        if (lane < 32)
+          __builtin_amdgcn_global_load_lds((const void*)(src + (rowbase + row) * F + 8 * lane),
+                                           (lds_void*)(base + t * T_BYTES + r * RS), 16, 0, 0);
+      }
+    }
+  };
+
+  f32x16 dw[4][4];  // wave (wm, wn): dW rows [128 wm + 32 i, +32), cols [128 wn + 32 j, +32)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) dw[i][j][e] = 0.f;
+  const int wm = wave & 1, wn = wave >> 1;
+  float dbacc[8];  // db: thread's chunk column cth, summed over its rows 4 rth .. 4 rth + 3
+  const int cth = tid & 31, rth = tid >> 5;  // 8 row groups of 4 rows
+#pragma unroll
+  for (int e = 0; e < 8; ++e) dbacc[e] = 0.f;
+
+  for (int s = 0; s < S - 1; ++s)
+    if (s < ntile) dma(s, s);
+
+  const int g = lane >> 4, t16 = lane & 15, q4 = t16 >> 2, p4 = t16 & 3;
+  for (int64_t k = 0; k < ntile; ++k) {
+    const int st = (int)(k % S);
+    if (k + S - 2 < ntile && k >= S - 1) vm_wait<STEADY>();
+    else vm_drain();
+    lds_barrier();
+    if (k + S - 1 < ntile) dma(k + S - 1, (int)((k + S - 1) % S));
+    char* Ab = smem + st * STAGE;
+    char* Pb = Ab + T_BYTES;
+    const int64_t r0 = r_begin + k * BM;
+    const int nval = (int)(r_end - r0 < BM ? r_end - r0 : BM);
+
+    // db over the valid rows of the dZ_l tile (chunk task: rows 4 rth + q, chunk cth)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 4 * rth + q;
+      if (r < nval) {
+        const bf16x8 dv = *(const bf16x8*)(Ab + off(r, cth));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dbacc[e] += (float)dv[e];
+      }
+    }
+    // input gradient, one 32-column block at a time (16 accumulator registers live):
+    // acc = dZ_l tile (32 rows) . W_l^T cols [64 w + 32 fb, +32); epilogue: dZ_{l-1} = acc cos(P) w0
+    // -> output tile, P -> bf16 sin(P) in place (0 past the end)
+#pragma unroll
+    for (int fb = 0; fb < 2; ++fb) {
+      f32x16 acc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8 af = *(const bf16x8*)(Ab + off(r32, 2 * ks + h));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, wf[fb][ks], acc, 0, 0, 0);
+      }
+      const int col = 64 * wave + 32 * fb + r32;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int rl = (e & 3) + 8 * (e >> 2) + 4 * h;
+        uint16_t* pp = (uint16_t*)(Pb + off(rl, col >> 3)) + (col & 7);
+        const uint16_t ph = *pp;
+        const float c = PT::cosp(ph);
+        ((uint16_t*)Obuf)[rl * F + col] = __builtin_bit_cast(uint16_t, (bf16)((acc[e] * c) * a.w0));
+        *pp = __builtin_bit_cast(uint16_t, (bf16)(rl < nval ? PT::sinp(ph) : 0.f));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    lds_barrier();
+    // weight gradient: dW[m][n] += sum_r dZ_l[r][m] sin(P)[r][n] (transposing fragment reads)
+#pragma unroll
+    for (int ks = 0; ks < BM / 16; ++ks) {
+      const int nb = 16 * ks + 8 * (g >> 1) + q4;
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = 128 * wm + 32 * i + 16 * (g & 1) + 4 * p4;
+        af[i] = lds_read_tr16_pair(Ab + off(nb, c >> 3) + (c & 7) * 2, Ab + off(nb + 4, c >> 3) + (c & 7) * 2);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = 128 * wn + 32 * j + 16 * (g & 1) + 4 * p4;
+        bfr[j] = lds_read_tr16_pair(Pb + off(nb, c >> 3) + (c & 7) * 2, Pb + off(nb + 4, c >> 3) + (c & 7) * 2);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          dw[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], dw[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // one K step's fragments live at a time
+    }
+    // coalesced dZ_{l-1} stores (rows past the range skipped)
+#pragma unroll
+    for (int q = 0; q < NST; ++q) {
+      const int u = tid + NT * q;
+      const int r = u >> 5, c = u & 31;
+      const u16x8 v = *(const u16x8*)(Obuf + (r * F + 8 * c) * 2);
+      if (r < nval) *(u16x8*)((uint16_t*)a.dZo + (rowbase + r0 + r) * F + 8 * c) = v;
+    }
+  }
+
+  // partial slab: dW (row-major 256 x 256) then db (256)
+  float* part = a.part + (int64_t)split * a.split_stride + batch * ((int64_t)F * F + F);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = 128 * wn + 32 * j + r32;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = 128 * wm + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+        part[(int64_t)row * F + col] = dw[i][j][e];
+      }
+    }
+  __syncthreads();
+  float* red = (float*)smem;  // [8 row groups][256]
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rth * 256 + 8 * cth + e] = dbacc[e];
+  __syncthreads();
+  {
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sum += red[k * 256 + tid];
+    part[(int64_t)F * F + tid] = sum;
+  }
+}
+
+}  // namespace siren

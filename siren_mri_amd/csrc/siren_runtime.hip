@@ -77,11 +77,12 @@ inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // every hidden width 256, up to FUSED_MAXH hidden MFMA layers.
 bool g_fused_forward = true;
 bool g_fused_backward = true;
-bool g_fuse_top = false;
-bool g_ring_top = true;  // output layer folded into the top 256x256 layer's ring kernels
-bool g_fwd_pipe = true;  // fused forward: half-tile MFMA/VALU pipelined kernel
-bool g_dx_ring = true;  // 256x256 input-gradient layers on the 4-stage ring kernel
-bool g_dw_ring = true;  // 256x256 weight-gradient layers on the 4-stage ring kernel  // output-layer fusion: measured slower than last_bwd + plain kernels
+bool g_fuse_top = false;   // output-layer fusion into the tiled kernels: slower than last_bwd, off
+bool g_ring_top = true;    // output layer folded into the top 256x256 layer's ring kernels
+bool g_bwd_ring = false;   // middle 256x256 layers in one ring kernel: measured slower (179 vs 145 us)
+bool g_fwd_pipe = true;    // fused forward: half-tile MFMA/VALU pipelined kernel
+bool g_dx_ring = true;     // 256x256 input-gradient layers on the 4-stage ring kernel
+bool g_dw_ring = true;     // 256x256 weight-gradient layers on the 4-stage ring kernel
 long long* g_fused_prof = nullptr;  // debug: per-workgroup phase cycle counters of the fused forward
 bool fused_shape(const siren_mlp_desc* d) {
   if (d->prec != SIREN_PREC_BF16) return false;
@@ -640,6 +641,31 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
     const bool is_bot = bot && l == 1;
     const bool rec1 = rec && l == 1;
     const bool ring_t = ring_top && l == g.L - 2;
+    if (PREC == kPrecBF16 && g_bwd_ring && !is_top && !is_bot && !rec1 && M == 256 && N == 256) {
+      // both gradients of a middle layer in one pass (bwd_ring_bf16_kernel)
+      const Split s = dw_ring_split(g);
+      BwdArgs b;
+      memset(&b, 0, sizeof(b));
+      b.dZ = (const bf16*)(ws + lo.dz_off[cur]);
+      b.P = (const uint16_t*)P(l - 1);
+      b.Wt = (const bf16*)(saved + lo.wt_op_off[l]);
+      b.dZo = (bf16*)(ws + lo.dz_off[cur ^ 1]);
+      b.part = part;
+      b.rows_per_batch = g.rows;
+      b.rows_per_split = s.rows_per_split;
+      b.split_stride = split_stride(g, (int64_t)M * N + M);
+      b.w_bstride = d->weights_batched ? (int64_t)M * N : 0;
+      b.w0 = d->w0;
+      tmark_begin(SIREN_KCLASS_BWD_FUSED, st);
+      hipLaunchKernelGGL(bwd_ring_bf16_kernel, dim3((unsigned)s.nsplit, (unsigned)g.nb), dim3(256), 0, st, b);
+      tmark_end(SIREN_KCLASS_BWD_FUSED, st);
+      if ((rc = check_launch("bwd_ring"))) return rc;
+      if ((rc = launch_reduce(part, s.nsplit, b.split_stride, g.nb, (int64_t)M * N + M, (int64_t)M * N, dW[l],
+                              db[l], st)))
+        return rc;
+      cur ^= 1;
+      continue;
+    }
     const bool ring = rec1 || ring_t || (PREC == kPrecBF16 && g_dw_ring && !is_top && M == 256 && N == 256);
     {
       const Split s = ring ? dw_ring_split(g) : tn_split(g, M, N);
@@ -1280,9 +1306,9 @@ int siren_adam_step(const siren_adam_desc* d, void* stream) {
     a.numel[t] = d->numel[t];
     maxn = std::max(maxn, d->numel[t]);
   }
-  a.one_minus_beta1 = (float)(1.0 - (double)d->beta1);
+  a.one_minus_beta1 = d->one_minus_beta1;
   a.beta2 = d->beta2;
-  a.one_minus_beta2 = (float)(1.0 - (double)d->beta2);
+  a.one_minus_beta2 = d->one_minus_beta2;
   a.eps = d->eps;
   a.weight_decay = d->weight_decay;
   a.step = d->step_size;
@@ -1315,6 +1341,10 @@ int siren_config_set(const char* key, int64_t value) {
     g_fwd_pipe = value != 0;
     return SIREN_OK;
   }
+  if (key && strcmp(key, "bwd_ring") == 0 && (value == 0 || value == 1)) {
+    g_bwd_ring = value != 0;
+    return SIREN_OK;
+  }
   if (key && strcmp(key, "dw_ring") == 0 && (value == 0 || value == 1)) {
     g_dw_ring = value != 0;
     return SIREN_OK;
@@ -1337,6 +1367,7 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "ring_output_fusion") == 0) return g_ring_top ? 1 : 0;
   if (key && strcmp(key, "dx_ring") == 0) return g_dx_ring ? 1 : 0;
   if (key && strcmp(key, "dw_ring") == 0) return g_dw_ring ? 1 : 0;
+  if (key && strcmp(key, "bwd_ring") == 0) return g_bwd_ring ? 1 : 0;
   if (key && strcmp(key, "fused_forward_pipe") == 0) return g_fwd_pipe ? 1 : 0;
   return -1;
 }

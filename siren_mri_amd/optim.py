@@ -80,6 +80,7 @@ class Adam(torch.optim.Adam):
                     d.maximize = 1 if group["maximize"] else 0
                     d.lr, d.beta1, d.beta2 = group["lr"], beta1, beta2
                     d.eps, d.weight_decay = group["eps"], group["weight_decay"]
+                    d.one_minus_beta1, d.one_minus_beta2 = 1 - beta1, 1 - beta2
                     d.step_size = (group["lr"] / bc1) * -1
                     d.bias_correction2_sqrt = bc2 ** 0.5
                     for k, p in enumerate(chunk):
