@@ -112,9 +112,12 @@ int siren_jvp_forward(const siren_mlp_desc* d, int order, const float* x, float*
                       void* stream);
 
 /*
- * Backward of a loss on the gradient (order 1): from dgrad = dL/dgrad [rows, in_features] writes
- * dweight/dbias (overwrite) and, if dx != NULL, dx. This is the double backward that
- * loss_functions.gradients_mse (loss_functions.py:330-335) runs through autograd.
+ * Backward of a loss on the gradient (order 1) or on the Laplacian (order 2): from
+ * dgrad = dL/dgrad [rows, in_features] (order 1) or dL/dlap [rows] (order 2) writes
+ * dweight/dbias (overwrite; the output bias gets zeros: it does not reach either derivative)
+ * and, if dx != NULL, dx. These are the double / triple backward passes that
+ * loss_functions.gradients_mse (loss_functions.py:330-335) and laplace_mse (:350-355) run
+ * through autograd. `saved` must come from siren_jvp_forward with the same order.
  */
 int siren_jvp_backward(const siren_mlp_desc* d, int order, const float* x, const float* dgrad,
                        const void* saved, int64_t saved_bytes, void* workspace,

@@ -15,10 +15,14 @@
 // streams with the same W_l; the prologue builds each stream's operand from the stored primal
 // phase P and the stored pre-activation tangents U, the epilogue stores P (stream 0) or U.
 //
-// Backward of a loss on the gradient (adjoints, stream-stacked D = [a_bar; u_bar^1..C]):
-//   u_bar^k = w0 cos(p) t_bar^k ;  a_bar = w0 (cos(p) h_bar - w0 sin(p) sum_k t_bar^k u^k)
-//   W_bar_l = D^T [h_{l-1}; t_{l-1}^k] ; b_bar_l = sum a_bar ; [h_bar; t_bar^k]_{l-1} = D W_l
-//   first layer: W_bar_0 = a_bar^T x + [sum_n u_bar^k as column k] ; x_bar = a_bar W_0
+// Backward of a loss on the gradient / the Laplacian (adjoints, stream-stacked
+// D = [a_bar; u_bar^1..C (; V_bar)] with Q = sum_k (u^k)^2, c = cos(p), s = sin(p)):
+//   u_bar^k = w0 c t_bar^k - 2 w0^2 s S_bar u^k          V_bar = w0 c S_bar
+//   a_bar   = w0 (c h_bar - w0 s sum_k t_bar^k u^k - w0 S_bar (s V + w0 c Q))
+//   W_bar_l = D^T [h_{l-1}; t_{l-1}^k; S_{l-1}] ; b_bar_l = sum a_bar ;
+//   [h_bar; t_bar^k; S_bar]_{l-1} = D W_l
+//   first layer: W_bar_0 = a_bar^T x + [sum_n u_bar^k as column k] ; x_bar = a_bar W_0 (V_0 = 0)
+// (order 1 has no S stream: S_bar = 0; the Laplacian loss has no gradient stream at the top)
 #include "siren_common.h"
 
 namespace siren {
@@ -239,7 +243,7 @@ struct JTNArgs {
   int64_t N;
   int64_t rows_per_split;
   int64_t split_stride;
-  int S, Su;          // S' = 1 + C adjoint streams
+  int S, Su, C;       // S' adjoint streams (1 + C, + 1 with the Laplacian stream)
   int M, Kin;
   float w0;
 };
@@ -291,8 +295,16 @@ __global__ __launch_bounds__(256) void jvp_tn_kernel(JTNArgs a) {
         if (i0 + c < a.M) dv = to_f32(((const grad_t*)a.D)[(b * rows + row) * a.M + i0 + c]);
         if (j0 + c < a.Kin) {
           const phase_t p = ((const phase_t*)a.P)[(b * a.N + n) * a.Kin + j0 + c];
-          xv = (s == 0) ? PT::sinp(p)
-                        : a.w0 * PT::cosp(p) * a.U[(b * a.Su + (s - 1)) * plane + n * a.Kin + j0 + c];
+          const float* Ue = a.U + b * a.Su * plane + n * a.Kin + j0 + c;
+          if (s == 0) {
+            xv = PT::sinp(p);
+          } else if (s <= a.C) {
+            xv = a.w0 * PT::cosp(p) * Ue[(s - 1) * plane];
+          } else {  // Laplacian stream: S = w0 c V - w0^2 s Q
+            float q = 0.f;
+            for (int j = 0; j < a.C; ++j) q = fmaf(Ue[j * plane], Ue[j * plane], q);
+            xv = a.w0 * PT::cosp(p) * Ue[a.C * plane] - a.w0 * a.w0 * PT::sinp(p) * q;
+          }
         }
         if (s == 0) dbacc[q] += dv;
       }
@@ -454,22 +466,24 @@ __global__ __launch_bounds__(256) void jvp_last_kernel(JLastArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Adjoint combine for a sine layer: from t_bar^k (and h_bar) to D = [a_bar; u_bar^k] (grad_t).
-// top = 1: the output layer's adjoint, t_bar^k[f] = gbar[n][k] * sum_o W_L[o][f], h_bar = 0,
-//          and also the output-layer weight-gradient partials dW_L[o][f] = sum_n sum_k gbar t^k[f].
-// top = 0: raw = [h_bar; t_bar^1..C] (fp32, [B][S'][N][F]) from the previous adjoint GEMM.
+// Adjoint combine for a sine layer: from [h_bar; t_bar^k; S_bar] to D = [a_bar; u_bar^k; V_bar].
+// top = 1: the output layer's adjoint, t_bar^k[f] = gbar[n][k] ws[f], S_bar[f] = lbar[n] ws[f]
+//          (ws = sum_o W_L[o][f]), h_bar = 0, and also the output-layer weight-gradient
+//          partials dW_L[o][f] = sum_n (sum_k gbar t^k[f] + lbar S[f]).
+// top = 0: raw = [h_bar; t_bar^1..C (; S_bar)] (fp32, [B][S'][N][F]) from the adjoint GEMM.
 struct JCombArgs {
   const void* P;      // [B][N][F] phase_t of this layer
   const float* U;     // [B][Su][N][F] tangents of this layer
   const float* raw;   // top=0
-  const float* gbar;  // top=1: [B][N][C]
+  const float* gbar;  // top=1: [B][N][C] or null (Laplacian loss)
+  const float* lbar;  // top=1: [B][N] (lap = 1)
   const float* WL;    // top=1: [nb_w][O][F]
   void* D;            // [B][S'][N][F] grad_t
   float* part;        // top=1: dW_L partial slabs (split s, batch b at s*split_stride + b*(O*F + O))
   int64_t N;
   int64_t rows_per_split;
   int64_t split_stride;
-  int C, F, O, Su, top;
+  int C, F, O, Su, S, top, lap;
   int64_t w_bstride;
   float w0;
 };
@@ -479,11 +493,12 @@ __global__ __launch_bounds__(256) void jvp_combine_kernel(JCombArgs a) {
   using PT = Prec<PREC>;
   using phase_t = typename PT::phase_t;
   using grad_t = typename PT::grad_t;
-  __shared__ float red[256];
   const int64_t b = blockIdx.y;
-  const int S = 1 + a.C;
+  const int S = a.S;
   const int64_t plane = a.N * (int64_t)a.F;
   const float* WL = a.top ? a.WL + b * a.w_bstride : nullptr;
+  const float w0 = a.w0, w02 = a.w0 * a.w0;
+  grad_t* D = (grad_t*)a.D;
   // thread owns feature column f = threadIdx.x (+256 k) for rows of its split
   const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_split;
   const int64_t r_end = min(r_begin + a.rows_per_split, a.N);
@@ -496,17 +511,35 @@ __global__ __launch_bounds__(256) void jvp_combine_kernel(JCombArgs a) {
       const phase_t p = ((const phase_t*)a.P)[(b * a.N + n) * a.F + f];
       const float c = PT::cosp(p), s = PT::sinp(p);
       const float* Ub = a.U + b * (int64_t)a.Su * plane + n * a.F + f;
-      float hbar = 0.f, cross = 0.f;
-      if (!a.top) hbar = a.raw[(b * S * a.N + n) * a.F + f];
+      const float* rw = a.top ? nullptr : a.raw + (b * S * a.N + n) * a.F + f;  // stream j: rw[j * plane]
+      const float hbar = a.top ? 0.f : rw[0];
+      float sbar = 0.f;
+      if (a.lap) sbar = a.top ? a.lbar[b * a.N + n] * ws : rw[(int64_t)(1 + a.C) * plane];
+      float cross = 0.f, q = 0.f;
       for (int k = 0; k < a.C; ++k) {
         const float u = Ub[(int64_t)k * plane];
-        const float tbar = a.top ? a.gbar[(b * a.N + n) * a.C + k] * ws
-                                 : a.raw[((b * S + 1 + k) * a.N + n) * a.F + f];
-        if (a.top) dwl = fmaf(a.gbar[(b * a.N + n) * a.C + k], a.w0 * c * u, dwl);
+        float tbar = 0.f;
+        if (a.top) {
+          if (a.gbar) {
+            const float gk = a.gbar[(b * a.N + n) * a.C + k];
+            tbar = gk * ws;
+            dwl = fmaf(gk, w0 * c * u, dwl);
+          }
+        } else {
+          tbar = rw[(int64_t)(1 + k) * plane];
+        }
         cross = fmaf(tbar, u, cross);
-        ((grad_t*)a.D)[((b * S + 1 + k) * a.N + n) * a.F + f] = from_f32<grad_t>(a.w0 * c * tbar);
+        q = fmaf(u, u, q);
+        D[((b * S + 1 + k) * a.N + n) * a.F + f] = from_f32<grad_t>(w0 * c * tbar - 2.f * w02 * s * sbar * u);
       }
-      ((grad_t*)a.D)[(b * S * a.N + n) * a.F + f] = from_f32<grad_t>(a.w0 * (c * hbar - a.w0 * s * cross));
+      float abar = c * hbar - w0 * s * cross;
+      if (a.lap) {
+        const float v = Ub[(int64_t)a.C * plane];
+        abar -= w0 * sbar * (s * v + w0 * c * q);
+        D[((b * S + 1 + a.C) * a.N + n) * a.F + f] = from_f32<grad_t>(w0 * c * sbar);
+        if (a.top) dwl = fmaf(a.lbar[b * a.N + n], w0 * c * v - w02 * s * q, dwl);
+      }
+      D[(b * S * a.N + n) * a.F + f] = from_f32<grad_t>(w0 * abar);
     }
     if (a.top) {
       float* part = a.part + (int64_t)blockIdx.x * a.split_stride + b * (int64_t)(a.O * a.F + a.O);
@@ -514,7 +547,6 @@ __global__ __launch_bounds__(256) void jvp_combine_kernel(JCombArgs a) {
       if (f < a.O) part[a.O * a.F + f] = 0.f;
     }
   }
-  (void)red;
 }
 
 // First layer adjoint: dW0[f][c] = sum_n a_bar[n][f] x[n][c] + sum_n u_bar^c[n][f] (c < C),
@@ -529,7 +561,7 @@ struct JFirstBwdArgs {
   int64_t N;
   int64_t rows_per_split;
   int64_t split_stride;
-  int C, F;
+  int C, F, S;        // S = adjoint streams (stride of D)
   int64_t w_bstride;
 };
 
@@ -538,7 +570,7 @@ __global__ __launch_bounds__(256) void jvp_first_bwd_kernel(JFirstBwdArgs a) {
   using PT = Prec<PREC>;
   using grad_t = typename PT::grad_t;
   const int64_t b = blockIdx.y;
-  const int S = 1 + a.C;
+  const int S = a.S;
   const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_split;
   const int64_t r_end = min(r_begin + a.rows_per_split, a.N);
   float* part = a.part + (int64_t)blockIdx.x * a.split_stride + b * (int64_t)(a.F * a.C + a.F);
@@ -567,7 +599,7 @@ __global__ __launch_bounds__(256) void jvp_first_dx_kernel(JFirstBwdArgs a) {
   using PT = Prec<PREC>;
   using grad_t = typename PT::grad_t;
   const int64_t b = blockIdx.y;
-  const int S = 1 + a.C;
+  const int S = a.S;
   const float* W = a.W + b * a.w_bstride;
   const int l32 = threadIdx.x & 31;
   for (int64_t n = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5); n < a.N; n += (int64_t)gridDim.x * 8) {

@@ -860,7 +860,7 @@ JLayout jlayout_of(const siren_mlp_desc* d, int order) {
   jl.C = d->dims[0];
   jl.Su = jl.C + (order >= 2 ? 1 : 0);
   jl.S = 1 + jl.Su;
-  jl.Sb = 1 + jl.C;
+  jl.Sb = 1 + jl.Su;  // adjoints [a_bar; u_bar^k (; V_bar)] mirror the forward streams
   int64_t off = jl.base.weights_bytes;
   for (int l = 0; l + 1 < g.L; ++l) {
     jl.p_off[l] = off;
@@ -981,10 +981,11 @@ int jvp_forward_impl(const siren_mlp_desc* d, int order, const float* x, float* 
 }
 
 template <int PREC>
-int jvp_backward_impl(const siren_mlp_desc* d, const float* x, const float* gbar, const char* saved,
-                      char* ws, float* const* dW, float* const* db, float* dx, hipStream_t st) {
+int jvp_backward_impl(const siren_mlp_desc* d, int order, const float* x, const float* dout,
+                      const char* saved, char* ws, float* const* dW, float* const* db, float* dx, hipStream_t st) {
   const Geo g = geo_of(d);
-  const JLayout jl = jlayout_of(d, 1);
+  const JLayout jl = jlayout_of(d, order);
+  const int lapmode = order >= 2;
   float* part = (float*)(ws + jl.part_off);
   int rc = SIREN_OK;
   int cur = 0;
@@ -995,7 +996,8 @@ int jvp_backward_impl(const siren_mlp_desc* d, const float* x, const float* gbar
     a.P = saved + jl.p_off[l - 1];
     a.U = (const float*)(saved + jl.u_off[l - 1]);
     a.raw = nullptr;
-    a.gbar = gbar;
+    a.gbar = lapmode ? nullptr : dout;
+    a.lbar = lapmode ? dout : nullptr;
     a.WL = d->weight[l];
     a.D = ws + jl.d_off[cur];
     a.part = part;
@@ -1005,7 +1007,9 @@ int jvp_backward_impl(const siren_mlp_desc* d, const float* x, const float* gbar
     a.F = d->dims[l];
     a.O = d->dims[l + 1];
     a.Su = jl.Su;
+    a.S = jl.Sb;
     a.top = 1;
+    a.lap = lapmode;
     a.split_stride = split_stride(g, (int64_t)a.O * a.F + a.O);
     a.w_bstride = d->weights_batched ? (int64_t)d->dims[l + 1] * d->dims[l] : 0;
     a.w0 = d->w0;
@@ -1029,6 +1033,7 @@ int jvp_backward_impl(const siren_mlp_desc* d, const float* x, const float* gbar
       a.split_stride = split_stride(g, (int64_t)M * N + M);
       a.S = jl.Sb;
       a.Su = jl.Su;
+      a.C = jl.C;
       a.M = M;
       a.Kin = N;
       a.w0 = d->w0;
@@ -1069,7 +1074,9 @@ int jvp_backward_impl(const siren_mlp_desc* d, const float* x, const float* gbar
       a.C = jl.C;
       a.F = N;
       a.Su = jl.Su;
+      a.S = jl.Sb;
       a.top = 0;
+      a.lap = lapmode;
       a.w0 = d->w0;
       hipLaunchKernelGGL(jvp_combine_kernel<PREC>, dim3((unsigned)s.nsplit, (unsigned)g.nb), dim3(256), 0, st, a);
       if ((rc = check_launch("jvp_combine"))) return rc;
@@ -1088,6 +1095,7 @@ int jvp_backward_impl(const siren_mlp_desc* d, const float* x, const float* gbar
     a.rows_per_split = s.rows_per_split;
     a.C = d->dims[0];
     a.F = d->dims[1];
+    a.S = jl.Sb;
     a.split_stride = split_stride(g, (int64_t)a.F * a.C + a.F);
     a.w_bstride = d->weights_batched ? (int64_t)d->dims[1] * d->dims[0] : 0;
     hipLaunchKernelGGL(jvp_first_bwd_kernel<PREC>, dim3((unsigned)s.nsplit, (unsigned)g.nb), dim3(256), 0, st, a);
@@ -1229,8 +1237,6 @@ int siren_jvp_backward(const siren_mlp_desc* d, int order, const float* x, const
                        float* const* dweight, float* const* dbias, float* dx, void* stream) {
   int rc = jvp_check(d, order);
   if (rc) return rc;
-  if (order != 1)
-    return fail(SIREN_EINVAL, "backward through the analytic Laplacian is not implemented (order 2)");
   const JLayout jl = jlayout_of(d, order);
   if (!saved || saved_bytes < jl.saved_bytes)
     return fail(SIREN_ENOSPACE, "saved buffer %lld < %lld bytes", (long long)saved_bytes, (long long)jl.saved_bytes);
@@ -1242,8 +1248,8 @@ int siren_jvp_backward(const siren_mlp_desc* d, int order, const float* x, const
   g_err.clear();
   hipStream_t st = (hipStream_t)stream;
   if (d->prec == SIREN_PREC_BF16)
-    return jvp_backward_impl<kPrecBF16>(d, x, dgrad, (const char*)saved, (char*)workspace, dweight, dbias, dx, st);
-  return jvp_backward_impl<kPrecF32>(d, x, dgrad, (const char*)saved, (char*)workspace, dweight, dbias, dx, st);
+    return jvp_backward_impl<kPrecBF16>(d, order, x, dgrad, (const char*)saved, (char*)workspace, dweight, dbias, dx, st);
+  return jvp_backward_impl<kPrecF32>(d, order, x, dgrad, (const char*)saved, (char*)workspace, dweight, dbias, dx, st);
 }
 
 const char* siren_last_error(void) { return g_err.c_str(); }

@@ -5,7 +5,8 @@ siren_gradient(x, fcblock, params) == diff_operators.gradient(y, x) for y = fcbl
     its backward is siren_jvp_backward, the hand-derived adjoint of the tangent streams (what
     loss_functions.gradients_mse's double backward computes through autograd in the reference).
 siren_laplace(x, fcblock, params) == diff_operators.laplace(y, x) (diff_operators.py:27-36):
-    sum over outputs and input dims of d2y/dx2. Forward only (its backward raises).
+    sum over outputs and input dims of d2y/dx2. Differentiable: its backward adds the Laplacian
+    adjoint stream (what laplace_mse's triple backward computes through autograd).
 """
 from __future__ import annotations
 
@@ -35,7 +36,7 @@ class _SirenJVP(torch.autograd.Function):
         dev = x.device
         desc = _desc(geo, ws, bs, fcblock, prec)
         L = _native.lib()
-        keep = grad_on and order == 1 and any(ctx.needs_input_grad)
+        keep = grad_on and any(ctx.needs_input_grad)
         saved_bytes = L.siren_jvp_saved_bytes(ctypes.byref(desc), order)
         if saved_bytes < 0:
             raise _native.NativeError(f"siren_jvp: {_native.last_error()}")
@@ -57,21 +58,19 @@ class _SirenJVP(torch.autograd.Function):
     @once_differentiable
     def backward(ctx, dout):
         fcblock, prec, order, n_layers, _ = ctx.cfg
-        if order != 1:
-            raise RuntimeError("siren_mri_amd: backward through the analytic laplace is not implemented")
         geo = ctx.geo
         t = ctx.saved_tensors
         xc, ws, bs = t[0], list(t[1:1 + n_layers]), list(t[1 + n_layers:])
         dev = xc.device
         desc = _desc(geo, ws, bs, fcblock, prec)
         L = _native.lib()
-        ws_bytes = L.siren_jvp_workspace_bytes(ctypes.byref(desc), 1)
+        ws_bytes = L.siren_jvp_workspace_bytes(ctypes.byref(desc), order)
         work = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         dW = [torch.empty_like(w) for w in ws]
         db = [torch.empty_like(b) for b in bs]
         dx = torch.empty_like(xc) if ctx.needs_input_grad[1] else None
         VP = ctypes.c_void_p * n_layers
-        rc = L.siren_jvp_backward(ctypes.byref(desc), 1, xc.data_ptr(), dout.contiguous().float().data_ptr(),
+        rc = L.siren_jvp_backward(ctypes.byref(desc), order, xc.data_ptr(), dout.contiguous().float().data_ptr(),
                                   ctx.saved_buf.data_ptr(), ctx.saved_bytes, work.data_ptr(), ws_bytes,
                                   VP(*[g.data_ptr() for g in dW]), VP(*[g.data_ptr() for g in db]),
                                   dx.data_ptr() if dx is not None else None, _native.stream_handle(dev))
@@ -80,7 +79,7 @@ class _SirenJVP(torch.autograd.Function):
         if geo.squeeze_w:
             dW = [g.unsqueeze(0) for g in dW]
             db = [g.unsqueeze(0) for g in db]
-        # the output bias does not reach dy/dx: autograd leaves its .grad as None in the reference
+        # the output bias does not reach dy/dx or the Laplacian: autograd leaves its .grad as None in the reference
         db[-1] = None
         return (None, dx, *dW, *db)
 

@@ -3,9 +3,13 @@
   gradient  == diff_operators.gradient (diff_operators.py:39-43)
   laplace   == diff_operators.laplace  (diff_operators.py:27-36)
   backward of gradients_mse == the reference's double backward (loss_functions.py:330-335)
+  backward of laplace_mse   == the reference's triple backward (loss_functions.py:350-355)
 Tolerance (fp32 path): 1e-5 norm-relative for values, 1e-4 for parameter gradients of the
 gradient loss (second-order adjoints through 2^10..2^12 rows). bf16 path: 5e-2.
-Also: 10 Adam steps of gradients_mse with the reference's own trajectory (train_c3.npz).
+Also: 10 Adam steps of gradients_mse with the reference's own trajectory (train_c3.npz), and 10
+Adam steps of laplace_mse against the oracle's loop (training.py:19-146 restated, float64) —
+the Laplacian training trajectory has no reference fixture: parity pinned through the oracle's
+autograd, whose forward laplace/laplace_mse values are pinned by forward.npz / losses.npz.
 """
 import os
 
@@ -116,3 +120,83 @@ def test_gradient_loss_training_matches_reference(tmp_path):
     sd = m.state_dict()
     for k in sd:
         assert orc.norm_rel(sd[k].cpu(), torch.from_numpy(d["final/" + k])) < 1e-4, k
+
+
+def _oracle_check_grads(m, ps, tg):
+    for i, (W, b) in enumerate(ps):
+        lw = m.net.net[i][0]
+        assert orc.norm_rel(lw.weight.grad.cpu(), W.grad) < tg, f"layer {i} dW"
+        if b.grad is None:  # output bias: no path to the derivative
+            assert lw.bias.grad is None
+        else:
+            assert orc.norm_rel(lw.bias.grad.cpu(), b.grad) < tg, f"layer {i} db"
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("side,hidden,nh,out", [(24, 64, 2, 1), (16, 256, 3, 1), (20, 128, 1, 2)])
+def test_laplace_mse_backward(precision, side, hidden, nh, out):
+    from siren_mri_amd import loss_functions
+    m = _model(hidden, nh, 7, precision, out=out)
+    coords = orc.get_mgrid(side)[None]
+    gt = torch.randn(1, side * side, 1, generator=torch.Generator().manual_seed(3)) * 100.0
+    o = m({"coords": coords.to(DEV)})
+    loss = loss_functions.laplace_mse(o, {"laplace": gt.to(DEV)})["laplace_loss"]
+    loss.backward()
+    ps = _oracle_params(m)
+    x = coords.double().clone().requires_grad_(True)
+    outd = {"model_in": x, "model_out": orc.siren_forward(x, ps)}
+    ref = orc.laplace_mse(outd, {"laplace": gt.double()})["laplace_loss"]
+    ref.backward()
+    tv, tg = TOL[precision]
+    assert loss.item() == pytest.approx(ref.item(), rel=max(tv, 1e-5) * 4)
+    _oracle_check_grads(m, ps, tg)
+
+
+def test_laplace_backward_input_grad_and_batched_weights():
+    """dL/dx through the analytic Laplacian and per-sample (hypernetwork) weights."""
+    from siren_mri_amd import diff_operators, modules
+    torch.manual_seed(11)
+    m = modules.SingleBVPNet(type="sine", hidden_features=64, num_hidden_layers=1, precision="fp32").to(DEV)
+    B = 2
+    params = {k: torch.stack([v * (1 + 0.03 * i) for i in range(B)]).requires_grad_(True)
+              for k, v in m.state_dict().items()}
+    coords = orc.get_mgrid(10)[None].repeat(B, 1, 1)
+    o = m({"coords": coords.to(DEV)}, params=params)
+    xin = o["model_in"]  # SingleBVPNet's detached leaf copy of the coordinates (modules.py:151)
+    lap = diff_operators.laplace(o["model_out"], o["model_in"])
+    wts = torch.randn(lap.shape, generator=torch.Generator().manual_seed(4))
+    (lap * wts.to(DEV)).sum().backward()
+    for bi in range(B):
+        ps = [(params[f"net.net.{i}.0.weight"][bi].detach().double().cpu().requires_grad_(True),
+               params[f"net.net.{i}.0.bias"][bi].detach().double().cpu().requires_grad_(True)) for i in range(3)]
+        x = coords[bi:bi + 1].double().clone().requires_grad_(True)
+        ref = orc.laplace(orc.siren_forward(x, ps), x)
+        (ref * wts[bi:bi + 1].double()).sum().backward()
+        for i, (W, b) in enumerate(ps):
+            gW = params[f"net.net.{i}.0.weight"].grad[bi].cpu()
+            assert orc.norm_rel(gW, W.grad) < 1e-4, f"sample {bi} layer {i} dW"
+            if i < 2:
+                assert orc.norm_rel(params[f"net.net.{i}.0.bias"].grad[bi].cpu(), b.grad) < 1e-4
+        assert orc.norm_rel(xin.grad[bi:bi + 1].cpu(), x.grad) < 1e-4, f"sample {bi} dx"
+
+
+def test_laplace_loss_training_matches_oracle(tmp_path):
+    """training.train + laplace_mse (Poisson-style fit, 32^2, 2x64): 10 Adam steps vs the oracle."""
+    from siren_mri_amd import dataio, loss_functions, modules, training
+    torch.manual_seed(5)
+    m = modules.SingleBVPNet(type="sine", hidden_features=64, num_hidden_layers=2, precision="fp32")
+    init = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.to(DEV)
+    coords = dataio.get_mgrid(32)[None]
+    gt = torch.sin(3 * coords[..., :1]) * torch.cos(2 * coords[..., 1:]) * 50.0
+    loader = [({"coords": coords}, {"laplace": gt})]
+    training.train(m, loader, epochs=10, lr=1e-4, steps_til_summary=1000, epochs_til_checkpoint=1000,
+                   model_dir=str(tmp_path / "run"), loss_fn=loss_functions.laplace_mse,
+                   summary_fn=lambda *a, **k: None)
+    losses = np.loadtxt(tmp_path / "run" / "checkpoints" / "train_losses_final.txt")
+    ps = [(init[f"net.net.{i}.0.weight"].double(), init[f"net.net.{i}.0.bias"].double()) for i in range(4)]
+    ref_losses, ref_ps, _ = orc.train_steps(ps, coords.double(), {"laplace": gt.double()}, orc.laplace_mse,
+                                            steps=10, lr=1e-4)
+    np.testing.assert_allclose(losses, ref_losses, rtol=1e-4)
+    for i, (W, b) in enumerate(ref_ps):
+        assert orc.norm_rel(m.net.net[i][0].weight.detach().cpu(), W) < 1e-4, f"layer {i} W"
