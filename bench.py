@@ -12,8 +12,8 @@ target: a smooth random image (sum of 32 sinusoids). Multi-GPU is weak scaling: 
 its own 512^2 block of coordinates (a 512 x 512N image), one gradient all-reduce per step.
 
 Prints ONE JSON line on rank 0 with: value (coord-samples/s, whole job), roofline of the
-dominant kernel (HIP events around each of its launches inside the timed region; FLOPs per
-launch = 2*rows*in*out), cpu_baseline (the CPU oracle timed on this host, rank 0, N=1 only),
+dominant kernel (HIP events around each of its launches inside the timed region; algorithmic
+FLOPs / bytes per launch from kernel_model), cpu_baseline (the CPU oracle timed on this host, rank 0, N=1 only),
 and psnr (64^2 cameraman, 500 steps, this path vs the reference's golden trajectory).
 """
 from __future__ import annotations
@@ -33,10 +33,19 @@ sys.path.insert(0, ROOT)
 
 PEAK = {"bf16": (2.5e15, "TFLOP/s"), "fp32": (157.3e12, "TFLOP/s")}
 HBM_PEAK = 8.0e12
-KCLASS_NAMES = {1: "nt_bf16_kernel<fwd> (hidden-layer forward GEMM + bias/w0/sin-phase epilogue)",
-                2: "nt_bf16_kernel<dx> (hidden-layer input-gradient GEMM + cos epilogue)",
-                3: "tn_dw_kernel (hidden-layer weight-gradient split-K GEMM)",
-                4: "fused_fwd_bf16_kernel (whole forward: layer 0, hidden MFMA layers, output layer)"}
+KCLASS_NAMES = {
+    1: "nt_bf16_kernel<fwd> (per-layer forward GEMM + bias/w0/phase epilogue)",
+    2: "nt_*_kernel<dx> (per-layer input-gradient GEMM + cos epilogue)",
+    3: "tn_dw_kernel (per-layer weight-gradient split-K GEMM)",
+    4: "fused_fwd_pipe_kernel (whole forward: layer 0, hidden MFMA layers, output layer)",
+    5: "bwd_ring_bf16_kernel (middle layer dX + dW)",
+    6: "dx_ring_bf16_kernel<0,false,false,0> (middle-layer input gradient)",
+    7: "dw_ring_bf16_kernel<0,0> (middle-layer weight gradient)",
+    8: "dx_ring_bf16_kernel<C,dx,rec,0> (layer-1 input gradient with layer 0 folded in)",
+    9: "dw_ring_bf16_kernel<C,0> (layer-1 weight gradient, P_0 rebuilt from x)",
+    10: "dx_ring_bf16_kernel<0,false,false,O> (top hidden layer with the output layer folded in)",
+    11: "dw_ring_bf16_kernel<0,O> (top hidden layer weight gradient + output-layer dW/db)",
+}
 
 
 def parse():
@@ -91,23 +100,38 @@ def build_step(args, dev, rank, world):
     return step, model
 
 
-def kernel_model(args, kclass):
+def kernel_model(args, kclass, p0_recompute):
     """Algorithmic FLOPs and HBM bytes of ONE launch of a kernel class at the bench workload
-    (DESIGN.md §5): F = hidden width, e = bytes per stored activation element (2 in bf16 mode:
-    16-bit phases / bf16 gradients; 4 in fp32 mode), C = 2 inputs, O = 1 output."""
-    rows = args.side * args.side
+    (DESIGN.md §5): R rows, F = hidden width, e = bytes per stored activation element (2 in bf16
+    mode: 16-bit phases / bf16 gradients; 4 in fp32 mode), C = 2 inputs, O = 1 output. Bytes are
+    the kernel's essential inputs and outputs once each (split-K partial slabs are not counted:
+    they are an implementation choice, visible in the PMC traffic)."""
+    R = args.side * args.side
     F, nh = args.hidden, args.num_hidden_layers
     e = 2 if args.precision == "bf16" else 4
     C, O = 2, 1
-    if kclass == 1:    # P_l = enc(w0 (sin(P_{l-1}) W^T + b)): read P_{l-1}, write P_l
-        return 2.0 * rows * F * F, rows * F * 2 * e
-    if kclass == 2:    # dZ_{l-1} = (dZ_l W) cos(P_{l-1}) w0: read dZ_l, P_{l-1}; write dZ_{l-1}
-        return 2.0 * rows * F * F, rows * F * 3 * e
-    if kclass == 3:    # dW_l = dZ_l^T sin(P_{l-1}): read dZ_l, P_{l-1}
-        return 2.0 * rows * F * F, rows * F * 2 * e
-    if kclass == 4:    # x in, every sine layer's phases out (kept for backward), y out
-        flops = 2.0 * rows * (C * F + nh * F * F + F * O)
-        return flops, rows * (4 * C + (nh + 1) * F * e + 4 * O)
+    gemm = 2.0 * R * F * F
+    dw_out = 4 * (F * F + F)
+    if kclass == 1:            # P_l = enc(w0 (sin(P_{l-1}) W^T + b)): read P_{l-1}, write P_l
+        return gemm, R * F * 2 * e
+    if kclass in (2, 6):       # dZ_{l-1} = (dZ_l W) cos(P_{l-1}) w0: read dZ_l, P_{l-1}; write dZ_{l-1}
+        return gemm, R * F * 3 * e
+    if kclass in (3, 7):       # dW_l = dZ_l^T sin(P_{l-1}), db_l: read dZ_l, P_{l-1}; write dW_l, db_l
+        return gemm, R * F * 2 * e + dw_out
+    if kclass == 4:            # x in, the kept sine layers' phases out, y out
+        planes = nh if p0_recompute else nh + 1
+        return 2.0 * R * (C * F + nh * F * F + F * O), R * (4 * C + planes * F * e + 4 * O)
+    if kclass == 5:            # 6 + 7 in one pass
+        return 2 * gemm, R * F * 3 * e + dw_out
+    if kclass == 8:            # read dZ_1, x (P_0 rebuilt from x, or read); write dx, dW_0/db_0
+        return (gemm + 3 * 2.0 * R * C * F,
+                R * (F * e + 4 * C + 4 * C + (0 if p0_recompute else F * e)) + 4 * (F * C + F))
+    if kclass == 9:            # read dZ_1, x; write dW_1, db_1
+        return gemm + 2.0 * R * C * F, R * (F * e + 4 * C) + dw_out
+    if kclass == 10:           # read P_top, dy, P_{top-1}; write dZ_{top-1}
+        return gemm + 2.0 * R * F * O, R * (3 * F * e + 4 * O)
+    if kclass == 11:           # read P_top, dy, P_{top-1}; write dW, db, dW_L, db_L
+        return gemm + 4.0 * R * F * O, R * (2 * F * e + 4 * O) + dw_out + 4 * (F * O + O)
     raise ValueError(kclass)
 
 
@@ -187,16 +211,32 @@ def psnr_check(args, dev):
             "config": "64x64 cameraman, SingleBVPNet 3 hidden x 256, Adam 1e-4, seed 0"}
 
 
+# kernel symbol of each class at the bench shape (C = 2 inputs, O = 1 output), as rocprofv3 names it
+KCLASS_SYMBOL = {
+    "bf16": {1: "siren::nt_bf16_kernel<0, 256, false, false>", 2: "siren::nt_bf16_kernel<1, 256, false, false>",
+             3: "siren::tn_dw_kernel<1, false, false>", 4: "siren::fused_fwd_pipe_kernel<2>",
+             5: "siren::bwd_ring_bf16_kernel", 6: "siren::dx_ring_bf16_kernel<0, false, false, 0>",
+             7: "siren::dw_ring_bf16_kernel<0, 0>", 8: "siren::dx_ring_bf16_kernel<2, true, true, 0>",
+             9: "siren::dw_ring_bf16_kernel<2, 0>", 10: "siren::dx_ring_bf16_kernel<0, false, false, 1>",
+             11: "siren::dw_ring_bf16_kernel<0, 1>"},
+    "fp32": {1: "siren::nt_f32_kernel<0>", 2: "siren::nt_f32_kernel<1>", 3: "siren::tn_dw_kernel<0, false, false>"},
+}
+
+
 def traffic_from_profile(kclass, args):
+    """HBM bytes per launch of the kernel from the committed PMC pass (profiles/pmc_traffic.json,
+    written by tools/pmc_bench.sh + tools/pmc_summary.py: FETCH_SIZE x2 (gfx950 correction) +
+    WRITE_SIZE, KB -> bytes), or None when this workload/kernel was not profiled."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
+    sym = KCLASS_SYMBOL.get(args.precision, {}).get(kclass)
+    if sym is None or not os.path.exists(path):
         return None
     try:
         with open(path) as f:
             d = json.load(f)
-        key = f"{args.precision}:{args.side}:{args.hidden}:{kclass}"
-        return d.get(key)
-    except Exception:
+        ent = d.get(f"{args.precision}:{args.side}:{args.hidden}:{args.num_hidden_layers}", {}).get(sym)
+        return None if ent is None else round(ent["bytes"] / 1e9, 4)
+    except (OSError, ValueError, KeyError):
         return None
 
 
@@ -213,15 +253,18 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    # pick the dominant kernel class from a short untimed probe (3 steps per class)
+    # pick the dominant kernel (largest time per step) from a short untimed probe (3 steps per
+    # class; every class is one kernel template instantiation, so its average launch duration is
+    # the rocprofv3 row of that kernel)
     totals = {}
-    for kc in (_native.KCLASS_FWD_GEMM, _native.KCLASS_DX_GEMM, _native.KCLASS_DW_GEMM,
-               _native.KCLASS_FWD_FUSED):
+    for kc in sorted(KCLASS_NAMES):
         with _native.KernelTimer(kc) as t:
             for _ in range(3):
                 step()
-        totals[kc] = t.total_ms
+        if t.launches:
+            totals[kc] = t.total_ms
     dom = max(totals, key=totals.get)
+    p0_recompute = args.precision == "bf16" and bool(_native.get_option("fused_forward"))
 
     with _native.KernelTimer(dom, max_launches=max(64, 8 * args.steps)) as kt:
         elapsed = timed_region(step, args.steps, world)
@@ -233,7 +276,7 @@ def main():
     coords_per_rank = args.side * args.side
     value = world * coords_per_rank * args.steps / elapsed
     avg_s = kt.avg_ms * 1e-3
-    flops, nbytes = kernel_model(args, dom)
+    flops, nbytes = kernel_model(args, dom, p0_recompute)
     mfma_peak, _ = PEAK[args.precision]
     # the binding roofline: whichever resource the algorithmic work needs longer on at peak
     if nbytes / HBM_PEAK >= flops / mfma_peak:
@@ -241,14 +284,16 @@ def main():
     else:
         bound, work, peak, unit, scale = "mfma", flops, mfma_peak, "TFLOP/s", 1e12
     achieved = work / avg_s if avg_s > 0 else float("nan")
-    roofline = {"bound": bound, "kernel": KCLASS_NAMES[dom], "achieved": round(achieved / scale, 2),
+    roofline = {"bound": bound, "kernel": KCLASS_NAMES[dom], "kernel_symbol": KCLASS_SYMBOL.get(args.precision, {}).get(dom),
+                "achieved": round(achieved / scale, 2),
                 "peak": round(peak / scale, 1), "unit": unit, "frac": round(achieved / peak, 4),
                 "traffic": traffic_from_profile(dom, args),
+                "traffic_unit": "GB per launch (HBM, PMC)",
                 "algorithmic_bytes_per_launch": nbytes, "flops_per_launch": flops,
                 "achieved_tflops": round(flops / avg_s / 1e12, 2) if avg_s > 0 else None,
                 "avg_launch_ms": round(kt.avg_ms, 4), "launches": kt.launches,
-                "kernel_class_ms_per_3_steps": {KCLASS_NAMES[k].split(" ")[0] + f"[{k}]": round(v, 3)
-                                                for k, v in totals.items()}}
+                "kernel_ms_per_step": {KCLASS_NAMES[k].split(" ")[0] + f"[{k}]": round(v / 3, 4)
+                                       for k, v in totals.items()}}
     result = {
         "metric": "coord-samples/sec/step, 5x256 SIREN on 512^2 grid; PSNR vs ref",
         "value": value,

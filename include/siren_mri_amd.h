@@ -136,6 +136,12 @@ int siren_jvp_backward(const siren_mlp_desc* d, int order, const float* x, const
 #define SIREN_KCLASS_DW_GEMM 3  /* hidden-layer weight-gradient split-K GEMM               */
 #define SIREN_KCLASS_FWD_FUSED 4 /* whole forward in one kernel (bf16, narrow in/out layers) */
 #define SIREN_KCLASS_BWD_FUSED 5 /* a middle layer's input + weight gradients in one kernel   */
+#define SIREN_KCLASS_DX_RING 6   /* dx_ring_bf16_kernel, middle layer                         */
+#define SIREN_KCLASS_DW_RING 7   /* dw_ring_bf16_kernel, middle layer                         */
+#define SIREN_KCLASS_DX_RING_BOT 8 /* dx_ring_bf16_kernel with the first layer folded in      */
+#define SIREN_KCLASS_DW_RING_REC 9 /* dw_ring_bf16_kernel of layer 1 (P_0 rebuilt from x)     */
+#define SIREN_KCLASS_DX_RING_TOP 10 /* dx_ring_bf16_kernel with the output layer folded in    */
+#define SIREN_KCLASS_DW_RING_TOP 11 /* dw_ring_bf16_kernel with the output layer folded in    */
 int siren_timing_enable(int kernel_class, int max_launches);
 int siren_timing_collect(double* total_ms, int64_t* launches);
 void siren_timing_disable(void);

@@ -48,6 +48,12 @@ KCLASS_DX_GEMM = 2
 KCLASS_DW_GEMM = 3
 KCLASS_FWD_FUSED = 4
 KCLASS_BWD_FUSED = 5
+KCLASS_DX_RING = 6
+KCLASS_DW_RING = 7
+KCLASS_DX_RING_BOT = 8
+KCLASS_DW_RING_REC = 9
+KCLASS_DX_RING_TOP = 10
+KCLASS_DW_RING_TOP = 11
 
 
 class SirenMLPDesc(ctypes.Structure):

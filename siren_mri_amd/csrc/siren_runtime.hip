@@ -403,9 +403,9 @@ int launch_nt(const NTArgs& a, int64_t nb, int kclass, hipStream_t st) {
   const int kmax = a.K <= 256 ? 256 : 512;
   if constexpr (PREC == kPrecBF16 && MODE == MODE_DX && !TOP && !BOT) {
     if (g_dx_ring && a.K == 256 && a.N == 256) {
-      tmark_begin(kclass, st);
+      tmark_begin(SIREN_KCLASS_DX_RING, st);
       hipLaunchKernelGGL((dx_ring_bf16_kernel<0, false>), ring_grid(a, nb), dim3(512), 0, st, a);
-      tmark_end(kclass, st);
+      tmark_end(SIREN_KCLASS_DX_RING, st);
       return check_launch("dx_ring");
     }
   }
@@ -689,7 +689,11 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
       a.w0 = d->w0;
       a.top = ta;
       dim3 grid((unsigned)(cdiv(M, TN_BM) * cdiv(N, TN_BN)), (unsigned)s.nsplit, (unsigned)g.nb);
-      tmark_begin(SIREN_KCLASS_DW_GEMM, st);
+      const int kcls = PREC != kPrecBF16 || !ring ? SIREN_KCLASS_DW_GEMM
+                       : rec1                     ? SIREN_KCLASS_DW_RING_REC
+                       : ring_t                   ? SIREN_KCLASS_DW_RING_TOP
+                                                  : SIREN_KCLASS_DW_RING;
+      tmark_begin(kcls, st);
       if constexpr (PREC == kPrecBF16) {
         const dim3 rg((unsigned)s.nsplit, (unsigned)g.nb);
         if (rec1) {
@@ -709,7 +713,7 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
       } else {
         hipLaunchKernelGGL((tn_dw_kernel<PREC, false>), grid, dim3(256), 0, st, a);
       }
-      tmark_end(SIREN_KCLASS_DW_GEMM, st);
+      tmark_end(kcls, st);
       if ((rc = check_launch("tn_dw"))) return rc;
       if ((rc = launch_reduce(part, s.nsplit, a.split_stride, g.nb, (int64_t)M * N + M,
                               (int64_t)M * N, dW[l], db[l], st)))
@@ -750,12 +754,12 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
       if constexpr (PREC == kPrecBF16) {
         if (is_bot && ring_bot) {
           a.C = dx;  // [rows, C] f32, or not written
-          rc = launch_dx_ring_bot(a, g.nb, C, dx != nullptr, rec1, SIREN_KCLASS_DX_GEMM, st);
+          rc = launch_dx_ring_bot(a, g.nb, C, dx != nullptr, rec1, SIREN_KCLASS_DX_RING_BOT, st);
         } else if (ring_t) {
-          tmark_begin(SIREN_KCLASS_DX_GEMM, st);
+          tmark_begin(SIREN_KCLASS_DX_RING_TOP, st);
           if (O == 1) hipLaunchKernelGGL((dx_ring_bf16_kernel<0, false, false, 1>), ring_grid(a, g.nb), dim3(512), 0, st, a);
           else hipLaunchKernelGGL((dx_ring_bf16_kernel<0, false, false, 2>), ring_grid(a, g.nb), dim3(512), 0, st, a);
-          tmark_end(SIREN_KCLASS_DX_GEMM, st);
+          tmark_end(SIREN_KCLASS_DX_RING_TOP, st);
           rc = check_launch("dx_ring top");
         } else if (is_top && is_bot) rc = launch_nt<PREC, MODE_DX, true, true>(a, g.nb, SIREN_KCLASS_DX_GEMM, st);
         else if (is_top) rc = launch_nt<PREC, MODE_DX, true, false>(a, g.nb, SIREN_KCLASS_DX_GEMM, st);

@@ -15,4 +15,4 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ
     -d "$R/gpurun_out/${TAG}_pmc3" -o run --output-format csv -- \
     python "$R/bench.py" "$@" > "$R/gpurun_out/${TAG}_pmc3.log" 2>&1
 cd "$R"
-python tools/pmc_summary.py "$R/gpurun_out/${TAG}" > "$R/gpurun_out/${TAG}_pmc.md"
+python tools/pmc_summary.py "$R/gpurun_out/${TAG}" "$R/gpurun_out/${TAG}_pmc.json" > "$R/gpurun_out/${TAG}_pmc.md"

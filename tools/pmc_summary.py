@@ -24,7 +24,7 @@ def load(pattern):
     return out
 
 
-def main(prefix):
+def main(prefix, json_out=None):
     merged = defaultdict(dict)
     for k in (1, 2, 3):
         data = load(f"{prefix}_pmc{k}/**/*counter_collection.csv")
@@ -51,6 +51,15 @@ def main(prefix):
     for _, name, short, rd, wr, mfma, valu, wait, wc, c in rows:
         print(f"| `{short}` | {rd:.1f} | {wr:.1f} | {mfma:.3g} | {100 * valu / wc if wc else float('nan'):.1f} | "
               f"{100 * wait / wc if wc else float('nan'):.1f} |")
+    if json_out:
+        # per-kernel HBM bytes per launch, keyed by the kernel symbol without `void ` and arguments
+        d = {}
+        for _, name, short, rd, wr, *_r in rows:
+            sym = name.split("(")[0].replace("void ", "").strip()
+            d[sym] = {"read_bytes": rd * 1e6, "write_bytes": wr * 1e6, "bytes": (rd + wr) * 1e6}
+        import json
+        with open(json_out, "w") as f:
+            json.dump(d, f, indent=1)
     print()
     print("raw means per dispatch:")
     for _, name, short, *_r, c in rows:
@@ -58,4 +67,4 @@ def main(prefix):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)

@@ -13,5 +13,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof
 cd "$R"
 STATS=$(find "$R/gpurun_out/${TAG}_prof" -name 'run_kernel_stats.csv' | head -1)
 cp "$STATS" "$R/gpurun_out/${TAG}_kernel_stats.csv"
-# steps run by bench.py: warmup + 4 probe classes x 3 + timed steps
-python tools/rocprof_summary.py "$STATS" "${STEPS_TOTAL:-37}" "$R/gpurun_out/${TAG}_summary.md" > /dev/null
+python tools/rocprof_summary.py "$STATS" auto "$R/gpurun_out/${TAG}_summary.md" > /dev/null
