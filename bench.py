@@ -45,6 +45,9 @@ KCLASS_NAMES = {
     9: "dw_ring_bf16_kernel<C,0> (layer-1 weight gradient, P_0 rebuilt from x)",
     10: "dx_ring_bf16_kernel<0,false,false,O> (top hidden layer with the output layer folded in)",
     11: "dw_ring_bf16_kernel<0,O> (top hidden layer weight gradient + output-layer dW/db)",
+    12: "pair_ring_bf16_kernel<middle> (middle layer: dX and dW roles on XCD-paired workgroups)",
+    13: "pair_ring_bf16_kernel<top> (top hidden layer + output layer: dX and dW roles)",
+    14: "pair_ring_bf16_kernel<bottom> (layer 1 + first layer, P_0 rebuilt: dX and dW roles)",
 }
 
 
@@ -132,6 +135,14 @@ def kernel_model(args, kclass, p0_recompute):
         return gemm + 2.0 * R * F * O, R * (3 * F * e + 4 * O)
     if kclass == 11:           # read P_top, dy, P_{top-1}; write dW, db, dW_L, db_L
         return gemm + 4.0 * R * F * O, R * (2 * F * e + 4 * O) + dw_out + 4 * (F * O + O)
+    if kclass == 12:           # 6 + 7 with dZ_l and P_{l-1} read once per pair
+        return 2 * gemm, R * F * 3 * e + dw_out
+    if kclass == 13:           # 10 + 11: read P_top, dy, P_{top-1} once; write dZ_{top-1}, dW, dW_L
+        return (2 * gemm + 6.0 * R * F * O,
+                R * (3 * F * e + 4 * O) + dw_out + 4 * (F * O + O))
+    if kclass == 14:           # 8 + 9: read dZ_1, x once; write dx, dW_1, dW_0
+        return (2 * gemm + 4 * 2.0 * R * C * F,
+                R * (F * e + 4 * C + 4 * C) + dw_out + 4 * (F * C + F))
     raise ValueError(kclass)
 
 
@@ -218,7 +229,10 @@ KCLASS_SYMBOL = {
              5: "siren::bwd_ring_bf16_kernel", 6: "siren::dx_ring_bf16_kernel<0, false, false, 0>",
              7: "siren::dw_ring_bf16_kernel<0, 0>", 8: "siren::dx_ring_bf16_kernel<2, true, true, 0>",
              9: "siren::dw_ring_bf16_kernel<2, 0>", 10: "siren::dx_ring_bf16_kernel<0, false, false, 1>",
-             11: "siren::dw_ring_bf16_kernel<0, 1>"},
+             11: "siren::dw_ring_bf16_kernel<0, 1>",
+             12: "siren::pair_ring_bf16_kernel<0, false, false, 0, 0>",
+             13: "siren::pair_ring_bf16_kernel<0, false, false, 1, 0>",
+             14: "siren::pair_ring_bf16_kernel<2, true, true, 0, 2>"},
     "fp32": {1: "siren::nt_f32_kernel<0>", 2: "siren::nt_f32_kernel<1>", 3: "siren::tn_dw_kernel<0, false, false>"},
 }
 

@@ -142,6 +142,9 @@ int siren_jvp_backward(const siren_mlp_desc* d, int order, const float* x, const
 #define SIREN_KCLASS_DW_RING_REC 9 /* dw_ring_bf16_kernel of layer 1 (P_0 rebuilt from x)     */
 #define SIREN_KCLASS_DX_RING_TOP 10 /* dx_ring_bf16_kernel with the output layer folded in    */
 #define SIREN_KCLASS_DW_RING_TOP 11 /* dw_ring_bf16_kernel with the output layer folded in    */
+#define SIREN_KCLASS_PAIR_RING 12     /* pair_ring_bf16_kernel, middle layer (dx + dw roles)   */
+#define SIREN_KCLASS_PAIR_RING_TOP 13 /* pair_ring_bf16_kernel, top layer + output layer        */
+#define SIREN_KCLASS_PAIR_RING_BOT 14 /* pair_ring_bf16_kernel, layer 1 + first layer, P_0 rebuilt */
 int siren_timing_enable(int kernel_class, int max_launches);
 int siren_timing_collect(double* total_ms, int64_t* launches);
 void siren_timing_disable(void);
@@ -189,6 +192,9 @@ int siren_adam_step(const siren_adam_desc* d, void* stream);
  *                    kernel (dZ and P read once); 0: separate input/weight-gradient kernels.
  *   "dw_ring"        1 (default): 256x256 bf16 weight-gradient layers use the ring kernel
  *                    (one full 256x256 partial per workgroup); 0: 128x128-tile split-K kernel.
+ *   "pair_ring"      1 (default): a 256x256 bf16 layer whose two gradients both run on the ring
+ *                    kernels computes them in ONE launch, on co-scheduled workgroup pairs that
+ *                    stream the same tiles (one HBM read of dZ and P per pair); 0: two launches.
  *   "debug_fused_profile"  device address of an int64 buffer [grid][4] that receives per-
  *                    workgroup cycle counts of the fused forward's phases, or 0 (off).
  * Returns SIREN_OK, or SIREN_EINVAL for an unknown key / value. Not thread-safe.

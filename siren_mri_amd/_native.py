@@ -54,6 +54,9 @@ KCLASS_DX_RING_BOT = 8
 KCLASS_DW_RING_REC = 9
 KCLASS_DX_RING_TOP = 10
 KCLASS_DW_RING_TOP = 11
+KCLASS_PAIR_RING = 12
+KCLASS_PAIR_RING_TOP = 13
+KCLASS_PAIR_RING_BOT = 14
 
 
 class SirenMLPDesc(ctypes.Structure):

@@ -853,13 +853,22 @@ DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMCNT) : "memory")
 // TOPO > 0 (top hidden layer, outermost_linear, O = TOPO outputs): the A operand dZ_top is not
 // read; the ring carries P_top (in the A image) and the dy tile, and a pass forms
 // dZ_top = (dy W_L) cos(P_top) w0 in place exactly as last_bwd_kernel does.
+template <int BOTC, int TOPO>
+constexpr int dx_ring_lds_bytes() {
+  return RING_S * (RING_BM * 256 * 2 * 2 + (BOTC > 0 ? RING_BM * BOTC * 4 : 0) + (TOPO > 0 ? RING_BM * TOPO * 4 : 0));
+}
+
+// The tiles of one workgroup: t = t0 + i * G for i < niter; `slab` indexes the BOTC first-layer
+// partial slab it writes.
 template <int BOTC, bool DXOUT, bool REC = false, int TOPO = 0>
-__global__ __launch_bounds__(512) void dx_ring_bf16_kernel(NTArgs a) {
+DEV void dx_ring_body(const NTArgs& a, char* smem, const int64_t t0, const int64_t G, const int64_t niter,
+                      const int64_t slab) {
   using PT = Prec<kPrecBF16>;
   constexpr int K = 256, N = 256, BM = RING_BM, S = RING_S;
   constexpr int X_BYTES = BOTC > 0 ? BM * BOTC * 4 : 0;
   constexpr int G_BYTES = TOPO > 0 ? BM * TOPO * 4 : 0;
   constexpr int A_BYTES = BM * K * 2, C_BYTES = BM * N * 2, STAGE = A_BYTES + C_BYTES + X_BYTES + G_BYTES;
+  static_assert(S * STAGE == dx_ring_lds_bytes<BOTC, TOPO>(), "dx_ring LDS size");
   constexpr int NKS = K / 16;
   constexpr int A_CPR = K / 8, C_CPR = N / 8;   // 16-byte chunks per row
   constexpr int SMASK = 15;
@@ -875,7 +884,6 @@ __global__ __launch_bounds__(512) void dx_ring_bf16_kernel(NTArgs a) {
   constexpr int STEADY = (S - 1) * NST + (S - 2) * (NA + NP + NX);
   static_assert(TOPO <= TOP_MAXO && !(TOPO > 0 && BOTC > 0), "output-layer fusion: top layer only");
   static_assert(!DXOUT || BOT, "dx output belongs to the first-layer fusion");
-  __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -883,7 +891,6 @@ __global__ __launch_bounds__(512) void dx_ring_bf16_kernel(NTArgs a) {
   const int64_t batch = blockIdx.y;
   const int64_t rows = a.rows_per_batch;
   const int64_t rowbase = batch * rows;
-  const int64_t ntiles = (rows + BM - 1) / BM;
   const int col = 32 * wave + r32;
 
   const bf16* Wb = (const bf16*)a.W + batch * a.w_bstride + (int64_t)col * K;
@@ -973,8 +980,6 @@ __global__ __launch_bounds__(512) void dx_ring_bf16_kernel(NTArgs a) {
     }
   };
 
-  const int64_t t0 = blockIdx.x, G = gridDim.x;
-  const int64_t niter = t0 < ntiles ? (ntiles - t0 + G - 1) / G : 0;
   for (int s = 0; s < S - 1; ++s)
     if (s < niter) dma(t0 + s * G, s);
 
@@ -1110,7 +1115,7 @@ __global__ __launch_bounds__(512) void dx_ring_bf16_kernel(NTArgs a) {
       red[rth * RS + 256 * BOTC + f] = bdb[e];
     }
     __syncthreads();
-    float* part = a.bot.part + (int64_t)blockIdx.x * a.bot.split_stride + batch * (int64_t)RS;
+    float* part = a.bot.part + slab * a.bot.split_stride + batch * (int64_t)RS;
     for (int idx = tid; idx < RS; idx += 512) {
       float sum = 0.f;
 #pragma unroll
@@ -1118,6 +1123,15 @@ __global__ __launch_bounds__(512) void dx_ring_bf16_kernel(NTArgs a) {
       part[idx] = sum;
     }
   }
+}
+
+template <int BOTC, bool DXOUT, bool REC = false, int TOPO = 0>
+__global__ __launch_bounds__(512) void dx_ring_bf16_kernel(NTArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[dx_ring_lds_bytes<BOTC, TOPO>()];
+  const int64_t ntiles = (a.rows_per_batch + RING_BM - 1) / RING_BM;
+  const int64_t t0 = blockIdx.x, G = gridDim.x;
+  const int64_t niter = t0 < ntiles ? (ntiles - t0 + G - 1) / G : 0;
+  dx_ring_body<BOTC, DXOUT, REC, TOPO>(a, smem, t0, G, niter, blockIdx.x);
 }
 
 }  // namespace siren
@@ -1139,29 +1153,32 @@ namespace siren {
 // ring carries P_top (in the dZ image) and the dy tile; the convert pass forms dZ_top in place
 // (last_bwd_kernel's arithmetic) and sums the output layer's dW_L = dy^T sin(P_top), db_L = sum dy
 // into per-workgroup slabs (a.top.partL).
+template <int RECC, int TOPO>
+constexpr int dw_ring_lds_bytes() {
+  return RING_S * (32 * 256 * 2 * 2 + (RECC > 0 ? 32 * RECC * 4 : 0) + (TOPO > 0 ? 32 * TOPO * 4 : 0));
+}
+
+// Rows [r_begin, r_end) of weight set blockIdx.y into partial slab `split`.
 template <int RECC = 0, int TOPO = 0>
-__global__ __launch_bounds__(512) void dw_ring_bf16_kernel(TNArgs a) {
+DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const int64_t r_end_in, const int64_t split) {
   using PT = Prec<kPrecBF16>;
   constexpr int M = 256, N = 256, KC = 32, S = RING_S;
   constexpr int X_BYTES = RECC > 0 ? KC * RECC * 4 : 0;
   constexpr int G_BYTES = TOPO > 0 ? KC * TOPO * 4 : 0;
   constexpr int D_BYTES = KC * M * 2, P_BYTES = KC * N * 2, STAGE = D_BYTES + P_BYTES + X_BYTES + G_BYTES;
+  static_assert(S * STAGE == dw_ring_lds_bytes<RECC, TOPO>(), "dw_ring LDS size");
   constexpr int CPR = 32;                                  // 16-byte chunks per row (both)
   constexpr int ND = KC * CPR / 64 / 8 + (TOPO > 0 ? 1 : 0);  // DMA instrs per wave per stage
   constexpr int NP = RECC > 0 ? 1 : KC * CPR / 64 / 8;
   constexpr int STEADY = (S - 2) * (ND + NP);
   static_assert(!(RECC > 0 && TOPO > 0), "one hidden layer: the plain output-layer path");
-  __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 3, wn = wave >> 2;
-  const int split = blockIdx.x;
   const int64_t batch = blockIdx.y;
   const int64_t rowbase = batch * a.rows_per_batch;
-  const int64_t r_begin = (int64_t)split * a.rows_per_split;
-  int64_t r_end = r_begin + a.rows_per_split;
-  if (r_end > a.rows_per_batch) r_end = a.rows_per_batch;
+  const int64_t r_end = r_end_in;
   const int64_t nchunk = r_end > r_begin ? (r_end - r_begin + KC - 1) / KC : 0;
 
   auto swz = [](int r, int c) -> int { return c ^ (2 * (r & 7)); };
@@ -1390,6 +1407,43 @@ __global__ __launch_bounds__(512) void dw_ring_bf16_kernel(TNArgs a) {
       for (int k = 0; k < 16; ++k) sum += red[k * RS + idx];
       pl[idx] = sum;
     }
+  }
+}
+
+template <int RECC = 0, int TOPO = 0>
+__global__ __launch_bounds__(512) void dw_ring_bf16_kernel(TNArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[dw_ring_lds_bytes<RECC, TOPO>()];
+  const int64_t split = blockIdx.x;
+  const int64_t r_begin = split * a.rows_per_split;
+  const int64_t r_end = r_begin + a.rows_per_split < a.rows_per_batch ? r_begin + a.rows_per_split : a.rows_per_batch;
+  dw_ring_body<RECC, TOPO>(a, smem, r_begin, r_end, split);
+}
+
+// ------------------------------------------------------------------------------------------
+// pair_ring: one 256 x 256 layer's two gradients in ONE launch, on two co-scheduled roles.
+// Workgroups b and b + 8 land on the same XCD under round-robin dispatch (speed only, never
+// correctness); pair p = the two workgroups (b & 7) + 16 k and (b & 7) + 16 k + 8. Both walk the
+// same contiguous range of 32-row tiles in the same order — the first as dx_ring (input
+// gradient), the second as dw_ring (weight gradient, one partial slab per pair) — so the tile one
+// of them streams from HBM is, most of the time, still in the XCD's L2 when the other asks for
+// it: dZ_l and P_{l-1} leave HBM about once instead of twice, and there are half as many slabs.
+// gridDim.x = 2 * npair, a multiple of 16.
+// ------------------------------------------------------------------------------------------
+template <int BOTC, bool DXOUT, bool REC, int TOPO, int RECC>
+__global__ __launch_bounds__(512) void pair_ring_bf16_kernel(NTArgs ax, TNArgs aw) {
+  constexpr int LX = dx_ring_lds_bytes<BOTC, TOPO>(), LW = dw_ring_lds_bytes<RECC, TOPO>();
+  __shared__ __attribute__((aligned(16))) char smem[LX > LW ? LX : LW];
+  const int b = blockIdx.x;
+  const int64_t pair = (b & 7) | ((b >> 4) << 3);
+  const int64_t npair = gridDim.x >> 1;
+  const int64_t rows = ax.rows_per_batch;
+  const int64_t ntiles = (rows + RING_BM - 1) / RING_BM;
+  const int64_t tb = ntiles * pair / npair, te = ntiles * (pair + 1) / npair;
+  if (((b >> 3) & 1) == 0) {
+    dx_ring_body<BOTC, DXOUT, REC, TOPO>(ax, smem, tb, 1, te - tb, pair);
+  } else {
+    const int64_t r_end = te * RING_BM < rows ? te * RING_BM : rows;
+    dw_ring_body<RECC, TOPO>(aw, smem, tb * RING_BM, r_end, pair);
   }
 }
 

@@ -83,6 +83,7 @@ bool g_bwd_ring = false;   // middle 256x256 layers in one ring kernel: measured
 bool g_fwd_pipe = true;    // fused forward: half-tile MFMA/VALU pipelined kernel
 bool g_dx_ring = true;     // 256x256 input-gradient layers on the 4-stage ring kernel
 bool g_dw_ring = true;     // 256x256 weight-gradient layers on the 4-stage ring kernel
+bool g_pair_ring = true;   // both gradients of a ring layer in one launch (pair_ring_bf16_kernel)
 long long* g_fused_prof = nullptr;  // debug: per-workgroup phase cycle counters of the fused forward
 bool fused_shape(const siren_mlp_desc* d) {
   if (d->prec != SIREN_PREC_BF16) return false;
@@ -142,6 +143,17 @@ Split dw_ring_split(const Geo& g) {
 // Distance between consecutive split slabs (all weight sets of one split), padded to float4.
 int64_t split_stride(const Geo& g, int64_t slab) { return align_up(g.nb * slab, 4); }
 
+// pair_ring_bf16_kernel: npair input-gradient / weight-gradient workgroup pairs per weight set
+// (a multiple of 8, so the grid is a multiple of 16 and every pair shares an XCD); with nb <= 16
+// weight sets all 2 * npair * nb workgroups are resident together (one per CU).
+constexpr int64_t kMaxPairs = 128;
+bool pair_ok(const Geo& g) { return g.nb <= 16; }
+int64_t pair_count(const Geo& g) {
+  const int64_t ntiles = cdiv(g.rows, 32);
+  const int64_t np = std::max<int64_t>(8, (kMaxPairs / g.nb) / 8 * 8);
+  return std::min<int64_t>(np, align_up(ntiles, 8));
+}
+
 struct Layout {
   // saved
   int64_t saved_off[SIREN_MAX_LAYERS];
@@ -153,6 +165,7 @@ struct Layout {
   int64_t dz_off[2];     // dZ ping-pong
   int64_t part_off;
   int64_t partL_off;      // output-layer partial slabs of the fused top backward layer
+  int64_t partB_off;      // first-layer partial slabs of the paired bottom layer (P_0 recompute)
   int64_t xcopy_off;      // 16-byte aligned copy of x (P_0 recompute with a misaligned x)
   bool p0_rec;
   int64_t ws_bytes;
@@ -218,6 +231,7 @@ Layout layout_of(const siren_mlp_desc* d) {
     const Split s = tn_split(g, M, N);
     part = std::max(part, s.nsplit * split_stride(g, (int64_t)M * N + M));
     part = std::max(part, dw_ring_split(g).nsplit * split_stride(g, (int64_t)M * N + M));
+    part = std::max(part, pair_count(g) * split_stride(g, (int64_t)M * N + M));
   }
   {
     const Split s = valu_split(g);
@@ -234,9 +248,12 @@ Layout layout_of(const siren_mlp_desc* d) {
   lo.partL_off = off;
   if (g.L >= 3) {
     const int F = d->dims[g.L - 1], O = d->dims[g.L];
-    const int64_t ns = std::max(tn_split(g, F, d->dims[g.L - 2]).nsplit, dw_ring_split(g).nsplit);
+    const int64_t ns = std::max(std::max(tn_split(g, F, d->dims[g.L - 2]).nsplit, dw_ring_split(g).nsplit),
+                                pair_count(g));
     off = align_up(off + ns * split_stride(g, (int64_t)O * F + O) * 4, 256);
   }
+  lo.partB_off = off;
+  if (lo.p0_rec) off = align_up(off + kMaxPairs * split_stride(g, (int64_t)d->dims[1] * d->dims[0] + d->dims[1]) * 4, 256);
   lo.xcopy_off = off;
   if (lo.p0_rec) off = align_up(off + g.total * d->dims[0] * 4, 256);
   lo.ws_bytes = off;
@@ -563,6 +580,90 @@ int forward_impl(const siren_mlp_desc* d, const float* x, float* y, char* saved,
   return SIREN_OK;
 }
 
+// One pair_ring_bf16_kernel launch for hidden layer l (kind: see backward_impl) and the
+// reductions of its partial slabs.
+template <int PREC>
+int launch_pair(const siren_mlp_desc* d, const Geo& g, const Layout& lo, int kind, int l, const float* x,
+                const TopArgs& ta, char* ws, const char* saved, float* part, float* const* dW, float* const* db,
+                float* dx, int cur, hipStream_t st) {
+  const int M = d->dims[l + 1], N = d->dims[l], C = d->dims[0], F0 = d->dims[1], O = d->dims[g.L];
+  const int64_t npair = pair_count(g);
+  TNArgs w;
+  memset(&w, 0, sizeof(w));
+  w.D = ws + lo.dz_off[cur];
+  w.P = kind == 3 ? (const void*)x : (const void*)(saved + lo.saved_off[l - 1]);
+  w.part = part;
+  w.rows_per_batch = g.rows;
+  w.rows_per_split = 0;  // ranges come from the pair index
+  w.split_stride = split_stride(g, (int64_t)M * N + M);
+  w.M = M;
+  w.N = N;
+  w.w0 = d->w0;
+  w.top = ta;
+  NTArgs a;
+  memset(&a, 0, sizeof(a));
+  a.A = ws + lo.dz_off[cur];
+  a.W = saved + lo.wt_op_off[l];
+  a.Paux = kind == 3 ? nullptr : (const void*)(saved + lo.saved_off[l - 1]);
+  a.C = ws + lo.dz_off[cur ^ 1];
+  a.rows_per_batch = g.rows;
+  a.w_bstride = d->weights_batched ? (int64_t)M * N : 0;
+  a.K = M;
+  a.N = N;
+  a.lda = M;
+  a.w0 = d->w0;
+  a.top = ta;
+  const int64_t bot_stride = split_stride(g, (int64_t)F0 * C + F0);
+  if (kind == 3) {
+    w.rec_W0 = d->weight[0];
+    w.rec_w0_bstride = d->weights_batched ? (int64_t)F0 * C : 0;
+    w.rec_b0 = d->bias[0];
+    w.rec_b0_bstride = d->weights_batched ? F0 : 0;
+    a.C = dx;
+    a.bot.x = x;
+    a.bot.W0 = d->weight[0];
+    a.bot.w0_bstride = w.rec_w0_bstride;
+    a.bot.b0 = d->bias[0];
+    a.bot.b0_bstride = w.rec_b0_bstride;
+    a.bot.part = (float*)(ws + lo.partB_off);
+    a.bot.split_stride = bot_stride;
+    a.bot.C = C;
+  }
+  const dim3 grid((unsigned)(2 * npair), (unsigned)g.nb);
+  const int kcls = kind == 1 ? SIREN_KCLASS_PAIR_RING : kind == 2 ? SIREN_KCLASS_PAIR_RING_TOP : SIREN_KCLASS_PAIR_RING_BOT;
+  tmark_begin(kcls, st);
+  if (kind == 1) {
+    hipLaunchKernelGGL((pair_ring_bf16_kernel<0, false, false, 0, 0>), grid, dim3(512), 0, st, a, w);
+  } else if (kind == 2) {
+    if (O == 1) hipLaunchKernelGGL((pair_ring_bf16_kernel<0, false, false, 1, 0>), grid, dim3(512), 0, st, a, w);
+    else hipLaunchKernelGGL((pair_ring_bf16_kernel<0, false, false, 2, 0>), grid, dim3(512), 0, st, a, w);
+  } else {
+#define SIREN_PAIR_BOT(CC)                                                                                   \
+  if (dx) hipLaunchKernelGGL((pair_ring_bf16_kernel<CC, true, true, 0, CC>), grid, dim3(512), 0, st, a, w);   \
+  else hipLaunchKernelGGL((pair_ring_bf16_kernel<CC, false, true, 0, CC>), grid, dim3(512), 0, st, a, w);
+    switch (C) {
+      case 1: SIREN_PAIR_BOT(1) break;
+      case 2: SIREN_PAIR_BOT(2) break;
+      case 3: SIREN_PAIR_BOT(3) break;
+      default: SIREN_PAIR_BOT(4) break;
+    }
+#undef SIREN_PAIR_BOT
+  }
+  tmark_end(kcls, st);
+  int rc = check_launch("pair_ring");
+  if (rc) return rc;
+  if ((rc = launch_reduce(part, npair, w.split_stride, g.nb, (int64_t)M * N + M, (int64_t)M * N, dW[l], db[l], st)))
+    return rc;
+  if (kind == 2 &&
+      (rc = launch_reduce(ta.partL, npair, ta.partL_stride, g.nb, (int64_t)O * M + O, (int64_t)O * M, dW[g.L - 1],
+                          db[g.L - 1], st)))
+    return rc;
+  if (kind == 3 && (rc = launch_reduce(a.bot.part, npair, bot_stride, g.nb, (int64_t)F0 * C + F0, (int64_t)F0 * C,
+                                       dW[0], db[0], st)))
+    return rc;
+  return SIREN_OK;
+}
+
 template <int PREC>
 int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, const char* saved,
                   char* ws, float* const* dW, float* const* db, float* dx, hipStream_t st) {
@@ -665,6 +766,21 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
         return rc;
       cur ^= 1;
       continue;
+    }
+    if (PREC == kPrecBF16 && g_pair_ring && pair_ok(g) && M == 256 && N == 256) {
+      // both gradients in one launch on co-scheduled workgroup pairs (pair_ring_bf16_kernel):
+      // 1 = middle layer, 2 = top layer with the output layer folded in, 3 = bottom layer with the
+      // first layer folded in and P_0 rebuilt from x
+      const int kind = (rec1 && !is_top)                                   ? 3
+                       : (ring_t && !is_bot)                               ? 2
+                       : (!is_top && !is_bot && !rec1 && g_dw_ring && g_dx_ring) ? 1
+                                                                           : 0;
+      if (kind) {
+        if ((rc = launch_pair<PREC>(d, g, lo, kind, l, x, ta, ws, saved, part, dW, db, dx, cur, st))) return rc;
+        if (kind == 3) return SIREN_OK;  // first layer done
+        cur ^= 1;
+        continue;
+      }
     }
     const bool ring = rec1 || ring_t || (PREC == kPrecBF16 && g_dw_ring && !is_top && M == 256 && N == 256);
     {
@@ -1363,6 +1479,10 @@ int siren_config_set(const char* key, int64_t value) {
     g_dx_ring = value != 0;
     return SIREN_OK;
   }
+  if (key && strcmp(key, "pair_ring") == 0 && (value == 0 || value == 1)) {
+    g_pair_ring = value != 0;
+    return SIREN_OK;
+  }
   if (key && strcmp(key, "debug_fused_profile") == 0) {  // device pointer or 0
     g_fused_prof = (long long*)(intptr_t)value;
     return SIREN_OK;
@@ -1378,6 +1498,7 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "dx_ring") == 0) return g_dx_ring ? 1 : 0;
   if (key && strcmp(key, "dw_ring") == 0) return g_dw_ring ? 1 : 0;
   if (key && strcmp(key, "bwd_ring") == 0) return g_bwd_ring ? 1 : 0;
+  if (key && strcmp(key, "pair_ring") == 0) return g_pair_ring ? 1 : 0;
   if (key && strcmp(key, "fused_forward_pipe") == 0) return g_fwd_pipe ? 1 : 0;
   return -1;
 }
