@@ -195,6 +195,8 @@ int siren_adam_step(const siren_adam_desc* d, void* stream);
  *   "pair_ring"      1 (default): a 256x256 bf16 layer whose two gradients both run on the ring
  *                    kernels computes them in ONE launch, on co-scheduled workgroup pairs that
  *                    stream the same tiles (one HBM read of dZ and P per pair); 0: two launches.
+ *   "debug_pair_roles"  3 (default); 1 / 2 run only the input- / weight-gradient role of
+ *                    pair_ring_bf16_kernel (timing experiments only: the gradients are then wrong).
  *   "debug_fused_profile"  device address of an int64 buffer [grid][4] that receives per-
  *                    workgroup cycle counts of the fused forward's phases, or 0 (off).
  * Returns SIREN_OK, or SIREN_EINVAL for an unknown key / value. Not thread-safe.

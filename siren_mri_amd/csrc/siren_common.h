@@ -66,8 +66,13 @@ template <> struct Prec<kPrecBF16> {
     return (uint16_t)(int)__builtin_rintf(fmaf(z, k, bk));
   }
   static DEV float rev(phase_t v) { return (float)v * (1.0f / 65536.0f); }
-  static DEV float sinp(phase_t v) { return __builtin_amdgcn_sinf(rev(v)); }
-  static DEV float cosp(phase_t v) { return __builtin_amdgcn_cosf(rev(v)); }
+  // v_sin_f32 / v_cos_f32 take revolutions and reduce them exactly: the float with bits
+  // 0x4300_0000 | v is 128 + v * 2^-16 (exact), one OR (or byte permute) instead of a convert and a
+  // multiply. Measured on gfx950 over all 65536 phases: cos bit-identical to cos(rev(v)); sin
+  // differs in 22 phases by less than 2^-24 absolute (tools/probe_sin.hip).
+  static DEV float rev128(phase_t v) { return __builtin_bit_cast(float, 0x43000000u | (uint32_t)v); }
+  static DEV float sinp(phase_t v) { return __builtin_amdgcn_sinf(rev128(v)); }
+  static DEV float cosp(phase_t v) { return __builtin_amdgcn_cosf(rev128(v)); }
   static DEV float sinr(float x) {
     const float r = x * kInv2Pi;
     return __builtin_amdgcn_sinf(r - floorf(r));
@@ -106,6 +111,38 @@ DEV bf16x8 lds_read_tr16_pair(const void* lo_ptr, const void* hi_ptr) {
   const s16x4 lo = lds_read_tr16(lo_ptr);
   const s16x4 hi = lds_read_tr16(hi_ptr);
   const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Raw buffer resource over [base, base + bytes): loads past the end return 0, stores past it are
+// dropped (the ragged-tile handling of the ring and fused kernels).
+DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                           (int)(bytes > 0x7fffffff ? 0x7fffffff : bytes), 0x00020000);
+}
+
+// The same transposing reads as inline asm, for kernels that also fill LDS by DMA
+// (global_load_lds): hipcc 7.2's wait-count pass treats the ds_read_b64_tr_b16 builtin as possibly
+// aliasing every LDS-DMA still in flight and puts an s_waitcnt vmcnt(0) in front of it, which
+// drains the prefetch ring every iteration. The asm form is invisible to that pass, so the caller
+// owns the LDS wait: issue the reads (tr16_issue), then tr16_wait(...) on every fragment (one
+// s_waitcnt lgkmcnt(0) whose operands tie the fragments to it), then tr16_value.
+struct TrFrag {
+  s16x4 lo, hi;
+};
+DEV uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+DEV void tr16_issue(TrFrag& f, const void* lo_ptr, const void* hi_ptr) {
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f.lo) : "v"(lds_addr(lo_ptr)));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f.hi) : "v"(lds_addr(hi_ptr)));
+}
+template <int OFF>
+DEV void tr16_read(s16x4& out, uint32_t vaddr) {
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(out) : "v"(vaddr), "n"(OFF));
+}
+DEV bf16x8 tr16_value(const TrFrag& f) {
+  const s16x8 v = __builtin_shufflevector(f.lo, f.hi, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(bf16x8, v);
 }
 

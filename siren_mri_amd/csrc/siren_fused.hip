@@ -353,10 +353,7 @@ namespace siren {
 // ------------------------------------------------------------------------------------------
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
-DEV __amdgpu_buffer_rsrc_t fused_rsrc(const void* base, int64_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
-                                           (int)(bytes > 0x7fffffff ? 0x7fffffff : bytes), 0x00020000);
-}
+DEV __amdgpu_buffer_rsrc_t fused_rsrc(const void* base, int64_t bytes) { return make_rsrc(base, bytes); }
 
 // SIREN_PIPE_NW waves (8: two per SIMD, 256 registers each; 4: one per SIMD, 512): wave w owns
 // FB = 8 / NW blocks of 32 features, holds their W_l fragments and the accumulators of both

@@ -69,6 +69,7 @@ struct NTArgs {
   float w0;
   TopArgs top;         // DX with TOP
   BotArgs bot;         // DX with BOT
+  long long* prof;     // debug: [grid.x][8 waves][RING_NPROF] segment cycle counters (null: off)
 };
 
 // Largest power-of-two divisor of the 16-byte chunks per row, capped at 16, minus one: the XOR
@@ -91,6 +92,8 @@ struct TNArgs {
   const float* rec_b0;
   int64_t rec_b0_bstride;
   TopArgs top;         // TOP: D = dZ_top formed from P_top, dy and W_L; also dW_L / db_L partials
+  int pair_roles;      // pair_ring (debug timing only): bit 0 runs the dx role, bit 1 the dw role
+  long long* prof;     // debug: [grid.x][8 waves][RING_NPROF] segment cycle counters (null: off)
 };
 
 // ------------------------------------------------------------------------------------------
@@ -838,6 +841,29 @@ namespace siren {
 // ------------------------------------------------------------------------------------------
 constexpr int RING_S = 4;
 constexpr int RING_BM = 32;
+constexpr int RING_NPROF = 6;
+
+// debug segment timer of the ring kernels (s_memtime; perturbs timing by ~10 %)
+struct RingProf {
+  long long* out;
+  long long acc[RING_NPROF];
+  long long mark;
+  DEV RingProf(long long* p) : out(p), mark(0) {
+    for (int i = 0; i < RING_NPROF; ++i) acc[i] = 0;
+    if (out) mark = clock64();
+  }
+  DEV void tick(int k) {
+    if (out) {
+      const long long now = clock64();
+      acc[k] += now - mark;
+      mark = now;
+    }
+  }
+  DEV void flush(int64_t slot) {
+    if (out && (threadIdx.x & 63) == 0)
+      for (int i = 0; i < RING_NPROF; ++i) out[(slot * 8 + (threadIdx.x >> 6)) * RING_NPROF + i] = acc[i];
+  }
+};
 
 template <int VMCNT>
 DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMCNT) : "memory"); }
@@ -983,6 +1009,7 @@ DEV void dx_ring_body(const NTArgs& a, char* smem, const int64_t t0, const int64
   for (int s = 0; s < S - 1; ++s)
     if (s < niter) dma(t0 + s * G, s);
 
+  RingProf prof(a.prof);
   for (int64_t i = 0; i < niter; ++i) {
     const int st = (int)(i % S);
     const int64_t t = t0 + i * G;
@@ -990,8 +1017,11 @@ DEV void dx_ring_body(const NTArgs& a, char* smem, const int64_t t0, const int64
     // wave to be done with the stage the next DMA overwrites (consumed in iteration i - 1)
     if (i + S - 2 < niter && i >= S - 1) vm_wait<STEADY>();
     else vm_drain();
+    prof.tick(0);
     lds_barrier();
+    prof.tick(1);
     if (i + S - 1 < niter) dma(t0 + (i + S - 1) * G, (int)((i + S - 1) % S));
+    prof.tick(2);
     char* base = smem + st * STAGE;
     if constexpr (TOPO > 0) {
       // dZ_top = (dy W_L) cos(P_top) w0 over the staged phases, in place (last_bwd's arithmetic)
@@ -1044,7 +1074,9 @@ DEV void dx_ring_body(const NTArgs& a, char* smem, const int64_t t0, const int64
       const float c = PT::cosp(ph);
       *dst = __builtin_bit_cast(uint16_t, (bf16)((acc[e] * c) * a.w0));
     }
+    prof.tick(3);
     lds_barrier();
+    prof.tick(4);
     const int64_t m0 = t * BM;
     if constexpr (!BOT) {
       // epilogue 2: coalesced 16-byte stores
@@ -1101,7 +1133,9 @@ DEV void dx_ring_body(const NTArgs& a, char* smem, const int64_t t0, const int64
         }
       }
     }
+    prof.tick(5);
   }
+  prof.flush(blockIdx.x);
   if constexpr (BOT) {
     // per-workgroup slab: dW_0 [F0][C] then db_0 [F0], summed over the 16 row slots
     __syncthreads();
@@ -1143,7 +1177,7 @@ namespace siren {
 // one 256 x 256 fp32 partial per workgroup over a contiguous row range (split-K; 128 accumulator
 // registers per lane: wave w owns dW rows [64 (w & 3), +64) x cols [128 (w >> 2), +128)).
 // 32-row chunks of dZ and P stream through a 4-stage LDS ring by DMA (16-byte chunks XOR-
-// swizzled by 2 (row & 7), which keeps the transposing ds_read_b64_tr_b16 fragment reads
+// swizzled by 4 (row & 3), which keeps the transposing ds_read_b64_tr_b16 fragment reads
 // conflict-free); each stage's phases are turned into bf16 sin(P) in place, then 16 MFMAs per
 // wave per stage. Counted waits keep three stages (96 KB per CU) in flight.
 // ------------------------------------------------------------------------------------------
@@ -1159,66 +1193,73 @@ constexpr int dw_ring_lds_bytes() {
 }
 
 // Rows [r_begin, r_end) of weight set blockIdx.y into partial slab `split`.
+//
+// Loads are LDS-DMA through raw buffer resources that span exactly this row range, so rows past
+// r_end arrive as zeros (dZ = 0: no contribution to dW, db or the output-layer sums) and no lane
+// ever tests a row bound. Per chunk and lane, VALU work is the convert pass alone: every LDS
+// address is a per-lane base fixed at entry plus the stage base plus an immediate offset.
 template <int RECC = 0, int TOPO = 0>
-DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const int64_t r_end_in, const int64_t split) {
+DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const int64_t r_end, const int64_t split) {
   using PT = Prec<kPrecBF16>;
   constexpr int M = 256, N = 256, KC = 32, S = RING_S;
   constexpr int X_BYTES = RECC > 0 ? KC * RECC * 4 : 0;
   constexpr int G_BYTES = TOPO > 0 ? KC * TOPO * 4 : 0;
   constexpr int D_BYTES = KC * M * 2, P_BYTES = KC * N * 2, STAGE = D_BYTES + P_BYTES + X_BYTES + G_BYTES;
   static_assert(S * STAGE == dw_ring_lds_bytes<RECC, TOPO>(), "dw_ring LDS size");
-  constexpr int CPR = 32;                                  // 16-byte chunks per row (both)
-  constexpr int ND = KC * CPR / 64 / 8 + (TOPO > 0 ? 1 : 0);  // DMA instrs per wave per stage
-  constexpr int NP = RECC > 0 ? 1 : KC * CPR / 64 / 8;
-  constexpr int STEADY = (S - 2) * (ND + NP);
+  constexpr int ND = 2 + (TOPO > 0 ? 1 : 0);   // DMA instructions per wave per stage: dZ (or P_top) (+ dy)
+  constexpr int NP = RECC > 0 ? 1 : 2;         // P_{l-1} (or x)
+  constexpr int NDMA = ND + NP;
   static_assert(!(RECC > 0 && TOPO > 0), "one hidden layer: the plain output-layer path");
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 3, wn = wave >> 2;
   const int64_t batch = blockIdx.y;
-  const int64_t rowbase = batch * a.rows_per_batch;
-  const int64_t r_end = r_end_in;
-  const int64_t nchunk = r_end > r_begin ? (r_end - r_begin + KC - 1) / KC : 0;
+  const int64_t row0 = batch * a.rows_per_batch + r_begin;
+  const int64_t nrows = r_end > r_begin ? r_end - r_begin : 0;
+  const int64_t nchunk = (nrows + KC - 1) / KC;
 
-  auto swz = [](int r, int c) -> int { return c ^ (2 * (r & 7)); };
+  const __amdgpu_buffer_rsrc_t rD =
+      make_rsrc((const bf16*)(TOPO > 0 ? a.top.Ptop : a.D) + row0 * M, nrows * M * 2);
+  const __amdgpu_buffer_rsrc_t rP =
+      RECC > 0 ? make_rsrc((const float*)a.P + row0 * (RECC > 0 ? RECC : 1), nrows * (RECC > 0 ? RECC : 1) * 4)
+               : make_rsrc((const uint16_t*)a.P + row0 * N, nrows * N * 2);
+  const __amdgpu_buffer_rsrc_t rG =
+      TOPO > 0 ? make_rsrc(a.top.dy + row0 * (TOPO > 0 ? TOPO : 1), nrows * (TOPO > 0 ? TOPO : 1) * 4) : rD;
+
+  // 16-byte chunk c of row r sits at chunk c ^ 4 (r & 3): the four rows of a transposing read
+  // (4 consecutive chunks each) then fall on four disjoint bank groups
+  auto swz = [](int r, int c) -> int { return c ^ (4 * (r & 3)); };
+  // DMA piece j of a 32-row image: rows 2 i, 2 i + 1 (i = wave + 8 j), lane -> (row, chunk)
+  uint32_t dvoff[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int i = wave + 8 * j;
+    const int r = 2 * i + (lane >> 5), p = lane & 31;
+    dvoff[j] = r * 512 + 16 * swz(r, p);
+  }
   auto dma = [&](int64_t k, int st) {
     char* base = smem + st * STAGE;
-    const int64_t r0 = r_begin + k * KC;
+    const uint32_t cb = (uint32_t)(k * KC * 512);  // the chunk's first byte in a 512-byte-row tensor
 #pragma unroll
-    for (int j = 0; j < ND; ++j) {
-      const int i = wave + 8 * j;                 // 1 KB = 2 rows
-      const int r = 2 * i + (lane >> 5), p = lane & 31;
-      const int64_t row = min(r0 + r, r_end - 1);
-      __builtin_amdgcn_global_load_lds(
-          (const void*)((const bf16*)(TOPO > 0 ? a.top.Ptop : a.D) + (rowbase + row) * M + 8 * swz(r, p)),
-          (lds_void*)(base + i * 1024), 16, 0, 0);
-    }
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rD, (lds_void*)(base + (wave + 8 * j) * 1024), 16, dvoff[j] + cb, 0,
+                                               0, 0);
     if constexpr (TOPO > 0) {
-      if (lane < TOPO) {
-        const int64_t el = min((r0 + rowbase) * TOPO + 4 * (TOPO * wave + lane), (rowbase + r_end) * TOPO - 4);
-        __builtin_amdgcn_global_load_lds((const void*)(a.top.dy + el),
-                                         (lds_void*)(base + D_BYTES + P_BYTES + X_BYTES + 16 * TOPO * wave), 16, 0,
-                                         0);
-      }
+      // dy rows of the chunk: KC * O floats; wave w moves bytes [16 O w, 16 O (w + 1)) (O lanes)
+      if (lane < TOPO)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rG, (lds_void*)(base + D_BYTES + P_BYTES + X_BYTES + 16 * TOPO * wave),
+                                                 16, (uint32_t)(k * KC * TOPO * 4) + 16 * (TOPO * wave + lane), 0, 0, 0);
     }
     if constexpr (RECC > 0) {
-      // x rows [r0, r0 + KC): wave w moves bytes [16 C w, 16 C (w + 1)) (C lanes)
-      if (lane < RECC) {
-        const int64_t el = min((r0 + rowbase) * RECC + 4 * (RECC * wave + lane), (rowbase + r_end) * RECC - 4);
-        __builtin_amdgcn_global_load_lds((const void*)((const float*)a.P + el),
-                                         (lds_void*)(base + D_BYTES + P_BYTES + 16 * RECC * wave), 16, 0, 0);
-      }
+      if (lane < RECC)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (lds_void*)(base + D_BYTES + P_BYTES + 16 * RECC * wave), 16,
+                                                 (uint32_t)(k * KC * RECC * 4) + 16 * (RECC * wave + lane), 0, 0, 0);
     } else {
 #pragma unroll
-      for (int j = 0; j < NP; ++j) {
-        const int i = wave + 8 * j;
-        const int r = 2 * i + (lane >> 5), p = lane & 31;
-        const int64_t row = min(r0 + r, r_end - 1);
-        __builtin_amdgcn_global_load_lds(
-            (const void*)((const uint16_t*)a.P + (rowbase + row) * N + 8 * swz(r, p)),
-            (lds_void*)(base + D_BYTES + i * 1024), 16, 0, 0);
-      }
+      for (int j = 0; j < 2; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (lds_void*)(base + D_BYTES + (wave + 8 * j) * 1024), 16,
+                                                 dvoff[j] + cb, 0, 0, 0);
     }
   };
 
@@ -1266,102 +1307,152 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
     }
   }
 
+  // convert pass, piece qq of the chunk in slot st: P -> bf16 sin(P) in place; db from the same
+  // rows; TOPO: dZ_top in place and the output-layer sums (rows past the range are all zeros)
+  const int coff = rth * 512 + swz(rth, cth) * 16;  // piece 1: + 16 rows = + 8192
+  auto convert = [&](int st, int qq) {
+    char* Db = smem + st * STAGE;
+    char* Pb = Db + D_BYTES;
+    const int r = rth + 16 * qq;
+    const int off = coff + 8192 * qq;
+    u16x8 ph;
+    if constexpr (RECC > 0) {
+      const float* xr = (const float*)(Pb + P_BYTES) + r * RECC;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float z = 0.f;
+#pragma unroll
+        for (int c = 0; c < CR; ++c) z = fmaf(xr[c], w0r[e][c], z);
+        ph[e] = PT::encz(z, b0r[e], a.w0);
+      }
+    } else {
+      ph = *(const u16x8*)(Pb + off);
+    }
+    bf16x8 hv;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) hv[e] = (bf16)PT::sinp(ph[e]);
+    *(bf16x8*)(Pb + off) = hv;
+    if constexpr (TOPO > 0) {
+      const float* gt = (const float*)(Pb + P_BYTES + X_BYTES) + r * TOPO;
+      const u16x8 pt = *(const u16x8*)(Db + off);
+      float gg[TOP_MAXO];
+#pragma unroll
+      for (int o = 0; o < TOP_MAXO; ++o) gg[o] = o < TOPO ? gt[o] : 0.f;
+      bf16x8 dz;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float dh = 0.f;
+#pragma unroll
+        for (int o = 0; o < TOP_MAXO; ++o) dh = fmaf(gg[o], o < TOPO ? twl[o < TOPO ? o : 0][e] : 0.f, dh);
+        dz[e] = (bf16)((dh * PT::cosp(pt[e])) * a.w0);
+        const float sv = PT::sinp(pt[e]);
+#pragma unroll
+        for (int o = 0; o < TO; ++o) tdw[o][e] = fmaf(gg[o], sv, tdw[o][e]);
+      }
+      *(bf16x8*)(Db + off) = dz;
+      if (cth == 0) {
+#pragma unroll
+        for (int o = 0; o < TO; ++o) tdb[o] += gg[o];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dbacc[e] += (float)dz[e];
+    } else {
+      const bf16x8 dv = *(const bf16x8*)(Db + off);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dbacc[e] += (float)dv[e];
+    }
+  };
+
+  // per-lane bases of the transposing fragment reads (bytes within a stage): K step 1 = + 16 rows
+  // (+ 8192), the upper 4 rows of a read pair = + 2048
+  const int g = lane >> 4, t = lane & 15, q = t >> 2, p = t & 3;
+  uint32_t abase[2], bbase[4];
+  {
+    const int nb = 8 * (g >> 1) + q;
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm) {
+      const int c = 64 * wm + 32 * bm + 16 * (g & 1) + 4 * p;
+      abase[bm] = nb * 512 + swz(nb, c >> 3) * 16 + (c & 7) * 2;
+    }
+#pragma unroll
+    for (int bn = 0; bn < 4; ++bn) {
+      const int c = 128 * wn + 32 * bn + 16 * (g & 1) + 4 * p;
+      bbase[bn] = D_BYTES + nb * 512 + swz(nb, c >> 3) * 16 + (c & 7) * 2;
+    }
+  }
+  const uint32_t smem_lds = lds_addr(smem);
+
   for (int s = 0; s < S - 1; ++s)
     if (s < nchunk) dma(s, s);
 
-  const int g = lane >> 4, t = lane & 15, q = t >> 2, p = t & 3;
-  for (int64_t k = 0; k < nchunk; ++k) {
-    const int st = (int)(k % S);
-    if (k + S - 2 < nchunk && k >= S - 1) vm_wait<STEADY>();
+  // The convert pass of chunk k + 1 runs beside the MFMAs of chunk k (different slots); one
+  // barrier per chunk. Slots in use at iteration k: k (MFMA), k + 1 (convert); DMAs k + 2, k + 3
+  // in flight (issued two iterations ahead).
+  if (nchunk > 0) {
+    if (nchunk >= 3) vm_wait<2 * NDMA>();
+    else if (nchunk == 2) vm_wait<NDMA>();
     else vm_drain();
     lds_barrier();
-    if (k + S - 1 < nchunk) dma(k + S - 1, (int)((k + S - 1) % S));
-    char* Db = smem + st * STAGE;
-    char* Pb = Db + D_BYTES;
-    // convert pass: P -> bf16 sin(P) in place (rows past the range -> 0); db from the same rows
-#pragma unroll
-    for (int qq = 0; qq < KC * CPR / 512; ++qq) {
-      const int r = rth + 16 * qq;
-      const bool valid = r_begin + k * KC + r < r_end;
-      const int off = r * 512 + swz(r, cth) * 16;
-      u16x8 ph;
-      if constexpr (RECC > 0) {
-        const float* xr = (const float*)(Pb + P_BYTES) + r * RECC;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float z = 0.f;
-#pragma unroll
-          for (int c = 0; c < CR; ++c) z = fmaf(xr[c], w0r[e][c], z);
-          ph[e] = PT::encz(z, b0r[e], a.w0);
-        }
-      } else {
-        ph = *(const u16x8*)(Pb + off);
-      }
-      bf16x8 hv;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) hv[e] = (bf16)(valid ? PT::sinp(ph[e]) : 0.f);
-      *(bf16x8*)(Pb + off) = hv;
-      if constexpr (TOPO > 0) {
-        // dZ_top in place over the staged P_top phases; output-layer sums on valid rows
-        const float* gt = (const float*)(Pb + P_BYTES + X_BYTES) + r * TOPO;
-        const u16x8 pt = *(const u16x8*)(Db + off);
-        float g[TOP_MAXO];
-#pragma unroll
-        for (int o = 0; o < TOP_MAXO; ++o) g[o] = o < TOPO ? gt[o] : 0.f;
-        bf16x8 dz;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float dh = 0.f;
-#pragma unroll
-          for (int o = 0; o < TOP_MAXO; ++o) dh = fmaf(g[o], o < TOPO ? twl[o < TOPO ? o : 0][e] : 0.f, dh);
-          dz[e] = (bf16)((dh * PT::cosp(pt[e])) * a.w0);
-        }
-        *(bf16x8*)(Db + off) = dz;
-        if (valid) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float sv = PT::sinp(pt[e]);
-#pragma unroll
-            for (int o = 0; o < TO; ++o) tdw[o][e] = fmaf(g[o], sv, tdw[o][e]);
-          }
-          if (cth == 0) {
-#pragma unroll
-            for (int o = 0; o < TO; ++o) tdb[o] += g[o];
-          }
-        }
-      }
-      if (valid) {
-        const bf16x8 dv = *(const bf16x8*)(Db + off);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) dbacc[e] += (float)dv[e];
-      }
-    }
-    lds_barrier();
-#pragma unroll
-    for (int ks = 0; ks < KC / 16; ++ks) {
-      const int nb = 16 * ks + 8 * (g >> 1) + q;
-      bf16x8 af[2], bfr[4];
-#pragma unroll
-      for (int bm = 0; bm < 2; ++bm) {
-        const int c = 64 * wm + 32 * bm + 16 * (g & 1) + 4 * p;
-        const int o0 = nb * 512 + swz(nb, c >> 3) * 16 + (c & 7) * 2;
-        const int o1 = (nb + 4) * 512 + swz(nb + 4, c >> 3) * 16 + (c & 7) * 2;
-        af[bm] = lds_read_tr16_pair(Db + o0, Db + o1);
-      }
-#pragma unroll
-      for (int bn = 0; bn < 4; ++bn) {
-        const int c = 128 * wn + 32 * bn + 16 * (g & 1) + 4 * p;
-        const int o0 = nb * 512 + swz(nb, c >> 3) * 16 + (c & 7) * 2;
-        const int o1 = (nb + 4) * 512 + swz(nb + 4, c >> 3) * 16 + (c & 7) * 2;
-        bfr[bn] = lds_read_tr16_pair(Pb + o0, Pb + o1);
-      }
-#pragma unroll
-      for (int bm = 0; bm < 2; ++bm)
-#pragma unroll
-        for (int bn = 0; bn < 4; ++bn)
-          acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[bm], bfr[bn], acc[bm][bn], 0, 0, 0);
-    }
+    convert(0, 0);
+    convert(0, 1);
   }
+  RingProf prof(a.prof);
+  for (int64_t k = 0; k < nchunk; ++k) {
+    const int st = (int)(k % S);
+    const bool next = k + 1 < nchunk;
+    // DMA(k + 1) landed (issued after it: DMA(k + 2), if any)
+    if (next) {
+      if (k + 2 < nchunk) vm_wait<NDMA>();
+      else vm_drain();
+    }
+    prof.tick(0);
+    lds_barrier();  // convert(k) visible, DMA(k + 1) visible, MFMA(k - 1) done with slot k - 1
+    prof.tick(1);
+    if (k + S - 1 < nchunk) dma(k + S - 1, (int)((k + S - 1) % S));
+    prof.tick(2);
+    const int stn = (int)((k + 1) % S);
+    const uint32_t sb = smem_lds + st * STAGE;
+    const uint32_t va0 = sb + abase[0], va1 = sb + abase[1];
+    const uint32_t vb0 = sb + bbase[0], vb1 = sb + bbase[1], vb2 = sb + bbase[2], vb3 = sb + bbase[3];
+    // both K steps' fragment reads up front (24 transposing reads), counted waits per step
+    TrFrag fa[2][2], fb[2][4];
+#define SIREN_TR(F, V, OFF)          \
+  tr16_read<(OFF)>((F).lo, V);       \
+  tr16_read<(OFF) + 2048>((F).hi, V);
+    SIREN_TR(fa[0][0], va0, 0) SIREN_TR(fa[0][1], va1, 0)
+    SIREN_TR(fb[0][0], vb0, 0) SIREN_TR(fb[0][1], vb1, 0) SIREN_TR(fb[0][2], vb2, 0) SIREN_TR(fb[0][3], vb3, 0)
+    SIREN_TR(fa[1][0], va0, 8192) SIREN_TR(fa[1][1], va1, 8192)
+    SIREN_TR(fb[1][0], vb0, 8192) SIREN_TR(fb[1][1], vb1, 8192) SIREN_TR(fb[1][2], vb2, 8192) SIREN_TR(fb[1][3], vb3, 8192)
+#undef SIREN_TR
+    static_assert(KC / 16 == 2, "two K steps per chunk");
+    asm volatile("s_waitcnt lgkmcnt(12)"
+                 : "+v"(fa[0][0].lo), "+v"(fa[0][0].hi), "+v"(fa[0][1].lo), "+v"(fa[0][1].hi), "+v"(fb[0][0].lo),
+                   "+v"(fb[0][0].hi), "+v"(fb[0][1].lo), "+v"(fb[0][1].hi), "+v"(fb[0][2].lo), "+v"(fb[0][2].hi),
+                   "+v"(fb[0][3].lo), "+v"(fb[0][3].hi));
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+      for (int bn = 0; bn < 4; ++bn)
+        acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr16_value(fa[0][bm]), tr16_value(fb[0][bn]),
+                                                              acc[bm][bn], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (next) convert(stn, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(fa[1][0].lo), "+v"(fa[1][0].hi), "+v"(fa[1][1].lo), "+v"(fa[1][1].hi), "+v"(fb[1][0].lo),
+                   "+v"(fb[1][0].hi), "+v"(fb[1][1].lo), "+v"(fb[1][1].hi), "+v"(fb[1][2].lo), "+v"(fb[1][2].hi),
+                   "+v"(fb[1][3].lo), "+v"(fb[1][3].hi));
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+      for (int bn = 0; bn < 4; ++bn)
+        acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr16_value(fa[1][bm]), tr16_value(fb[1][bn]),
+                                                              acc[bm][bn], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (next) convert(stn, 1);
+    prof.tick(3);
+  }
+  prof.flush(blockIdx.x);
 
   // partial slab: dW (row-major M x N) then db (M)
   float* part = a.part + (int64_t)split * a.split_stride + batch * ((int64_t)M * N + M);
@@ -1440,8 +1531,10 @@ __global__ __launch_bounds__(512) void pair_ring_bf16_kernel(NTArgs ax, TNArgs a
   const int64_t ntiles = (rows + RING_BM - 1) / RING_BM;
   const int64_t tb = ntiles * pair / npair, te = ntiles * (pair + 1) / npair;
   if (((b >> 3) & 1) == 0) {
+    if (!(aw.pair_roles & 1)) return;
     dx_ring_body<BOTC, DXOUT, REC, TOPO>(ax, smem, tb, 1, te - tb, pair);
   } else {
+    if (!(aw.pair_roles & 2)) return;
     const int64_t r_end = te * RING_BM < rows ? te * RING_BM : rows;
     dw_ring_body<RECC, TOPO>(aw, smem, tb * RING_BM, r_end, pair);
   }

@@ -84,6 +84,9 @@ bool g_fwd_pipe = true;    // fused forward: half-tile MFMA/VALU pipelined kerne
 bool g_dx_ring = true;     // 256x256 input-gradient layers on the 4-stage ring kernel
 bool g_dw_ring = true;     // 256x256 weight-gradient layers on the 4-stage ring kernel
 bool g_pair_ring = true;   // both gradients of a ring layer in one launch (pair_ring_bf16_kernel)
+int g_pair_roles = 3;      // debug timing: which pair_ring roles run (results are wrong unless 3)
+long long* g_ring_prof = nullptr;   // debug: pair_ring segment cycle counters, one block per launch
+int g_ring_prof_n = 0;
 long long* g_fused_prof = nullptr;  // debug: per-workgroup phase cycle counters of the fused forward
 bool fused_shape(const siren_mlp_desc* d) {
   if (d->prec != SIREN_PREC_BF16) return false;
@@ -600,6 +603,8 @@ int launch_pair(const siren_mlp_desc* d, const Geo& g, const Layout& lo, int kin
   w.N = N;
   w.w0 = d->w0;
   w.top = ta;
+  w.pair_roles = g_pair_roles;
+  w.prof = g_ring_prof ? g_ring_prof + (int64_t)(g_ring_prof_n++) * 256 * 8 * RING_NPROF : nullptr;
   NTArgs a;
   memset(&a, 0, sizeof(a));
   a.A = ws + lo.dz_off[cur];
@@ -613,6 +618,7 @@ int launch_pair(const siren_mlp_desc* d, const Geo& g, const Layout& lo, int kin
   a.lda = M;
   a.w0 = d->w0;
   a.top = ta;
+  a.prof = w.prof;
   const int64_t bot_stride = split_stride(g, (int64_t)F0 * C + F0);
   if (kind == 3) {
     w.rec_W0 = d->weight[0];
@@ -1479,8 +1485,17 @@ int siren_config_set(const char* key, int64_t value) {
     g_dx_ring = value != 0;
     return SIREN_OK;
   }
+  if (key && strcmp(key, "debug_pair_roles") == 0 && value >= 0 && value <= 3) {
+    g_pair_roles = (int)value;
+    return SIREN_OK;
+  }
   if (key && strcmp(key, "pair_ring") == 0 && (value == 0 || value == 1)) {
     g_pair_ring = value != 0;
+    return SIREN_OK;
+  }
+  if (key && strcmp(key, "debug_ring_profile") == 0) {  // device pointer or 0
+    g_ring_prof = (long long*)(intptr_t)value;
+    g_ring_prof_n = 0;
     return SIREN_OK;
   }
   if (key && strcmp(key, "debug_fused_profile") == 0) {  // device pointer or 0
