@@ -351,7 +351,6 @@ namespace siren {
 // (ds_add_f32) and a small pass writes y after the next barrier. x comes in one tile ahead and
 // is parked in LDS so no vector-memory wait ever covers the stores.
 // ------------------------------------------------------------------------------------------
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 DEV __amdgpu_buffer_rsrc_t fused_rsrc(const void* base, int64_t bytes) { return make_rsrc(base, bytes); }
 

@@ -887,8 +887,8 @@ constexpr int dx_ring_lds_bytes() {
 // The tiles of one workgroup: t = t0 + i * G for i < niter; `slab` indexes the BOTC first-layer
 // partial slab it writes.
 template <int BOTC, bool DXOUT, bool REC = false, int TOPO = 0>
-DEV void dx_ring_body(const NTArgs& a, char* smem, const int64_t t0, const int64_t G, const int64_t niter,
-                      const int64_t slab) {
+DEV void dx_ring_body_v1(const NTArgs& a, char* smem, const int64_t t0, const int64_t G, const int64_t niter,
+                         const int64_t slab) {
   using PT = Prec<kPrecBF16>;
   constexpr int K = 256, N = 256, BM = RING_BM, S = RING_S;
   constexpr int X_BYTES = BOTC > 0 ? BM * BOTC * 4 : 0;
@@ -1157,6 +1157,367 @@ DEV void dx_ring_body(const NTArgs& a, char* smem, const int64_t t0, const int64
       part[idx] = sum;
     }
   }
+}
+
+// dx_ring body for the layers without the first-layer fusion (middle and top). The MFMA runs
+// transposed, dZ_{l-1}^T = W_l^T . dZ_l^T, so each lane holds one row's 4 consecutive output
+// features per accumulator group: the cos(P) epilogue reads the phases and writes the result as
+// 8-byte LDS accesses in place over the staged P tile, and the wave stores its own 32 columns of
+// the tile from there (wave-local: no barrier between the MFMAs and the stores). Loads are LDS-DMA
+// through buffer resources bounded by the tile's valid rows (rows past the end arrive as zeros),
+// stores are buffer stores bounded the same way. One barrier per tile (two with TOPO).
+template <int TOPO>
+DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const int64_t G, const int64_t niter) {
+  using PT = Prec<kPrecBF16>;
+  constexpr int K = 256, N = 256, BM = RING_BM, S = RING_S;
+  constexpr int G_BYTES = TOPO > 0 ? BM * TOPO * 4 : 0;
+  constexpr int A_BYTES = BM * K * 2, C_BYTES = BM * N * 2, STAGE = A_BYTES + C_BYTES + G_BYTES;
+  static_assert(S * STAGE == dx_ring_lds_bytes<0, TOPO>(), "dx_ring LDS size");
+  constexpr int NKS = K / 16;
+  constexpr int NDMA = 4 + (TOPO > 0 ? 1 : 0);  // VMEM instructions per wave per stage (loads)
+  constexpr int NST = 2;                        // buffer stores per wave per tile
+  // VMEM ops issued after DMA(i) when iteration i waits for it: stores of tiles i-3..i-1 and the
+  // DMAs of tiles i+1, i+2
+  constexpr int STEADY = 3 * NST + 2 * NDMA;
+  static_assert(TOPO <= TOP_MAXO, "output-layer fusion: O <= 2");
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int64_t batch = blockIdx.y;
+  const int64_t rows = a.rows_per_batch;
+  const int64_t rowbase = batch * rows;
+
+  // W_l^T slice of this wave's 32 output features: the MFMA A operand, in registers
+  const bf16* Wb = (const bf16*)a.W + batch * a.w_bstride + (int64_t)(32 * wave + r32) * K;
+  bf16x8 wf[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) wf[ks] = *(const bf16x8*)(Wb + 16 * ks + 8 * h);
+
+  // TOPO: this thread's W_L columns for the in-place dZ_top pass (chunk tid % 32 is fixed)
+  float twl[TOPO > 0 ? TOPO : 1][8];
+  if constexpr (TOPO > 0) {
+#pragma unroll
+    for (int o = 0; o < TOPO; ++o)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) twl[o][e] = a.top.WL[batch * a.top.wl_bstride + (int64_t)o * K + 8 * (tid & 31) + e];
+  }
+
+  // both images: row r (512 B), 16-byte chunk c stored at chunk c ^ (r & 15)
+  auto img_off = [](int r, int c) -> int { return r * 512 + ((c ^ (r & 15)) << 4); };
+  uint32_t dvoff[2];  // DMA piece j: rows 2 i, 2 i + 1 (i = wave + 8 j)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int i = wave + 8 * j;
+    const int r = 2 * i + (lane >> 5), p = lane & 31;
+    dvoff[j] = r * 512 + 16 * (p ^ (r & 15));
+  }
+  // epilogue: group g = this lane's row r32, features 32 w + 8 g + 4 h .. +4 (chunk 4 w + g, half h)
+  int eoff[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) eoff[g] = A_BYTES + img_off(r32, 4 * wave + g) + 8 * h;
+  // store pass: lane's 16-byte pieces q = lane + 64 j -> row q / 4, chunk 4 w + q % 4
+  int soff[2], goff[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int qd = lane + 64 * j, r = qd >> 2, c = 4 * wave + (qd & 3);
+    soff[j] = A_BYTES + img_off(r, c);
+    goff[j] = r * 512 + 16 * c;
+  }
+
+  auto nval = [&](int64_t t) -> int64_t {
+    const int64_t n = rows - t * BM;
+    return n < BM ? n : BM;
+  };
+  auto dma = [&](int64_t t, int st) {
+    char* base = smem + st * STAGE;
+    const int64_t m0 = rowbase + t * BM, nv = nval(t);
+    const __amdgpu_buffer_rsrc_t rA = make_rsrc((const bf16*)(TOPO > 0 ? a.top.Ptop : a.A) + m0 * K, nv * K * 2);
+    const __amdgpu_buffer_rsrc_t rP = make_rsrc((const uint16_t*)a.Paux + m0 * N, nv * N * 2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(base + (wave + 8 * j) * 1024), 16, dvoff[j], 0, 0, 0);
+    if constexpr (TOPO > 0) {
+      const __amdgpu_buffer_rsrc_t rG = make_rsrc(a.top.dy + m0 * TOPO, nv * TOPO * 4);
+      if (lane < TOPO)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rG, (lds_void*)(base + A_BYTES + C_BYTES + 16 * TOPO * wave), 16,
+                                                 16 * (TOPO * wave + lane), 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (lds_void*)(base + A_BYTES + (wave + 8 * j) * 1024), 16, dvoff[j],
+                                               0, 0, 0);
+  };
+
+  // epilogue of tile t held in slot st with accumulator acc: dZ_{l-1} = acc cos(P) w0 (4 features
+  // per group, in place over the staged P tile), then the wave's 32 columns to dZ_{l-1} rows
+  auto epilogue = [&](int64_t t, int st, const f32x16& acc) {
+    char* base = smem + st * STAGE;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      char* pp = base + eoff[g];
+      const u16x4 ph = *(const u16x4*)pp;
+      bf16x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (bf16)((acc[4 * g + e] * PT::cosp(ph[e])) * a.w0);
+      *(bf16x4*)pp = v;
+    }
+    const __amdgpu_buffer_rsrc_t rC = make_rsrc((const bf16*)a.C + (rowbase + t * BM) * N, nval(t) * N * 2);
+#pragma unroll
+    for (int j = 0; j < NST; ++j) {
+      const u32x4_t v = *(const u32x4_t*)(base + soff[j]);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rC, goff[j], 0, 0);
+    }
+  };
+
+  // (An in-wave software pipeline — tile i's MFMAs beside tile i - 1's epilogue — measured
+  // slower: the two waves of a SIMD already overlap one's MFMAs with the other's epilogue.)
+  for (int s = 0; s < S - 1; ++s)
+    if (s < niter) dma(t0 + s * G, s);
+
+  RingProf prof(a.prof);
+  for (int64_t i = 0; i < niter; ++i) {
+    const int st = (int)(i % S);
+    const int64_t t = t0 + i * G;
+    // this stage's DMA (this wave's part) landed; then every wave's part, and every wave is done
+    // with the stage the next DMA overwrites (tile i - 1: MFMA reads and its store pass)
+    if (i >= S - 1 && i + S - 2 < niter) vm_wait<STEADY>();
+    else vm_drain();
+    prof.tick(0);
+    lds_barrier();
+    prof.tick(1);
+    if (i + S - 1 < niter) dma(t0 + (i + S - 1) * G, (int)((i + S - 1) % S));
+    prof.tick(2);
+    char* base = smem + st * STAGE;
+    if constexpr (TOPO > 0) {
+      // dZ_top = (dy W_L) cos(P_top) w0 over the staged phases, in place (last_bwd's arithmetic)
+      const float* gt = (const float*)(base + A_BYTES + C_BYTES);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int u = tid + 512 * q;
+        const int r = u >> 5, c = u & 31;
+        char* pp = base + img_off(r, c);
+        const u16x8 ph = *(const u16x8*)pp;
+        float gg[TOP_MAXO];
+#pragma unroll
+        for (int o = 0; o < TOP_MAXO; ++o) gg[o] = o < TOPO ? gt[r * TOPO + o] : 0.f;
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float dh = 0.f;
+#pragma unroll
+          for (int o = 0; o < TOP_MAXO; ++o) dh = fmaf(gg[o], o < TOPO ? twl[o < TOPO ? o : 0][e] : 0.f, dh);
+          v[e] = (bf16)((dh * PT::cosp(ph[e])) * a.w0);
+        }
+        *(bf16x8*)pp = v;
+      }
+      lds_barrier();
+    }
+    // dZ_{l-1}^T (32 features x 32 rows) = W^T slice . dZ_l^T: B fragments = dZ rows from LDS
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const bf16x8 bfr = *(const bf16x8*)(base + img_off(r32, 2 * ks + h));
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], bfr, acc, 0, 0, 0);
+    }
+    prof.tick(3);
+    epilogue(t, st, acc);
+    prof.tick(5);
+  }
+  prof.flush(blockIdx.x);
+}
+
+// dx_ring body of the bottom hidden layer with the first layer folded in and P_0 rebuilt from x
+// (C = BOTC <= 4 inputs). Transposed MFMA as dx_ring_body_v2; the epilogue keeps dZ_0 in
+// registers (rounded to bf16 exactly like the stored-and-reloaded value of the v1 kernel) and
+// accumulates per lane: db_0 and dW_0 = dZ_0^T x for its 16 features (reduced over the lanes once,
+// at the end), and dx = dZ_0 W_0 partials over its features, summed over the 8 waves in wave
+// order through LDS after the next barrier. The ring carries dZ_1 and x only (no P image).
+template <int BOTC, bool DXOUT>
+DEV void dx_ring_body_v2bot(const NTArgs& a, char* smem, const int64_t t0, const int64_t G, const int64_t niter,
+                            const int64_t slab) {
+  using PT = Prec<kPrecBF16>;
+  constexpr int K = 256, F0 = 256, BM = RING_BM, S = RING_S, C = BOTC;
+  constexpr int A_BYTES = BM * K * 2, X_BYTES = BM * C * 4, STAGE = A_BYTES + X_BYTES;
+  constexpr int YP_BYTES = 2 * 8 * BM * C * 4;  // dx partials [2][wave][row][C]
+  constexpr int W0_BYTES = F0 * C * 4 + F0 * 4;  // W_0 [F0][C] and k * b_0 [F0], staged once
+  static_assert(S * STAGE + YP_BYTES + W0_BYTES <= dx_ring_lds_bytes<BOTC, 0>(), "dx_ring LDS size");
+  constexpr int NKS = K / 16;
+  constexpr int NDMA = 2 + 1;              // dZ_1 pieces + the x piece
+  constexpr int NST = DXOUT ? 1 : 0;       // dx stores per wave per tile
+  constexpr int STEADY = (S - 1) * NST + (S - 2) * NDMA;
+  float* Yp = (float*)(smem + S * STAGE);
+  float* W0s = (float*)(smem + S * STAGE + YP_BYTES);
+  float* b0ks = W0s + F0 * C;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int64_t batch = blockIdx.y;
+  const int64_t rows = a.rows_per_batch;
+  const int64_t rowbase = batch * rows;
+  const float kph = PT::enck(a.w0);
+
+  const bf16* Wb = (const bf16*)a.W + batch * a.w_bstride + (int64_t)(32 * wave + r32) * K;
+  bf16x8 wf[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) wf[ks] = *(const bf16x8*)(Wb + 16 * ks + 8 * h);
+  // W_0 and k * b_0 staged in LDS (visible after the first barrier); the lane's 16 first-layer
+  // features are f = 32 w + 8 g + 4 h + e, u = 4 g + e
+  {
+    const float* W0 = a.bot.W0 + batch * a.bot.w0_bstride;
+    const float* b0 = a.bot.b0 + batch * a.bot.b0_bstride;
+    for (int idx = tid; idx < F0 * C; idx += 512) W0s[idx] = W0[idx];
+    for (int f = tid; f < F0; f += 512) b0ks[f] = b0[f] * kph;
+  }
+  float dwacc[16][C], dbacc[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    dbacc[u] = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) dwacc[u][c] = 0.f;
+  }
+
+  auto img_off = [](int r, int c) -> int { return r * 512 + ((c ^ (r & 15)) << 4); };
+  uint32_t dvoff[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int i = wave + 8 * j;
+    const int r = 2 * i + (lane >> 5), p = lane & 31;
+    dvoff[j] = r * 512 + 16 * (p ^ (r & 15));
+  }
+  auto nval = [&](int64_t t) -> int64_t {
+    const int64_t n = rows - t * BM;
+    return n < BM ? n : BM;
+  };
+  auto dma = [&](int64_t t, int st) {
+    char* base = smem + st * STAGE;
+    const int64_t m0 = rowbase + t * BM, nv = nval(t);
+    const __amdgpu_buffer_rsrc_t rA = make_rsrc((const bf16*)a.A + m0 * K, nv * K * 2);
+    const __amdgpu_buffer_rsrc_t rX = make_rsrc(a.bot.x + m0 * C, nv * C * 4);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(base + (wave + 8 * j) * 1024), 16, dvoff[j], 0, 0, 0);
+    // x rows of the tile: BM * C floats; wave w moves bytes [16 C w, 16 C (w + 1)) (C lanes)
+    if (lane < C)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)(base + A_BYTES + 16 * C * wave), 16,
+                                               16 * (C * wave + lane), 0, 0, 0);
+  };
+  // dx of tile t from the wave partials in Yp[buf]: wave w stores rows 4 w .. 4 w + 3 (lanes < 4 C)
+  auto dx_store = [&](int64_t t, int buf) {
+    if constexpr (DXOUT) {
+      const int idx = 4 * C * wave + lane;  // (row, c) element of the tile, row-major
+      float v = 0.f;
+      if (lane < 4 * C) {
+#pragma unroll
+        for (int w = 0; w < 8; ++w) v += Yp[(buf * 8 + w) * BM * C + idx];
+      }
+      const __amdgpu_buffer_rsrc_t rD = make_rsrc(a.C ? (float*)a.C + (rowbase + t * BM) * C : nullptr,
+                                                  a.C ? nval(t) * C * 4 : 0);
+      if (lane < 4 * C) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rD, idx * 4, 0, 0);
+    }
+  };
+
+  for (int s = 0; s < S - 1; ++s)
+    if (s < niter) dma(t0 + s * G, s);
+
+  for (int64_t i = 0; i < niter; ++i) {
+    const int st = (int)(i % S);
+    const int64_t t = t0 + i * G;
+    if (i >= S - 1 && i + S - 2 < niter) vm_wait<STEADY>();
+    else vm_drain();
+    lds_barrier();  // also publishes tile i - 1's dx partials
+    if (i + S - 1 < niter) dma(t0 + (i + S - 1) * G, (int)((i + S - 1) % S));
+    if (i > 0) dx_store(t - G, (int)((i - 1) & 1));
+    char* base = smem + st * STAGE;
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const bf16x8 bfr = *(const bf16x8*)(base + img_off(r32, 2 * ks + h));
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], bfr, acc, 0, 0, 0);
+    }
+    // epilogue: P_0 rebuilt from x (the forward's arithmetic), dZ_0 = bf16(acc cos(P_0) w0)
+    const float* xr = (const float*)(base + A_BYTES) + r32 * C;
+    float xv[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) xv[c] = xr[c];
+    float dxp[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) dxp[c] = 0.f;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int f0 = 32 * wave + 8 * g + 4 * h;
+      float wv[4 * C];
+#pragma unroll
+      for (int k4 = 0; k4 < C; ++k4) {
+        const f32x4 v = *(const f32x4*)(W0s + f0 * C + 4 * k4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) wv[4 * k4 + e] = v[e];
+      }
+      const f32x4 bk = *(const f32x4*)(b0ks + f0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int u = 4 * g + e;
+        float z = 0.f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) z = fmaf(xv[c], wv[e * C + c], z);
+        const uint16_t ph = PT::enc_scaled(z, bk[e], kph);
+        const float dz = (float)(bf16)((acc[u] * PT::cosp(ph)) * a.w0);
+        dbacc[u] += dz;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          dwacc[u][c] = fmaf(dz, xv[c], dwacc[u][c]);
+          dxp[c] = fmaf(dz, wv[e * C + c], dxp[c]);
+        }
+      }
+    }
+    if constexpr (DXOUT) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) dxp[c] += __shfl_xor(dxp[c], 32, 64);
+      if (h == 0) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) Yp[((i & 1) * 8 + wave) * BM * C + r32 * C + c] = dxp[c];
+      }
+    }
+  }
+  if (niter > 0) {
+    lds_barrier();
+    dx_store(t0 + (niter - 1) * G, (int)((niter - 1) & 1));
+  }
+  // per-workgroup slab: dW_0 [F0][C] then db_0 [F0]: sums over the 32 lanes of each half-wave
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+#pragma unroll
+    for (int off = 16; off >= 1; off >>= 1) {
+      dbacc[u] += __shfl_xor(dbacc[u], off, 32);
+#pragma unroll
+      for (int c = 0; c < C; ++c) dwacc[u][c] += __shfl_xor(dwacc[u][c], off, 32);
+    }
+  }
+  if (r32 == 0) {
+    float* part = a.bot.part + slab * a.bot.split_stride + batch * (int64_t)(F0 * (C + 1));
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int f = 32 * wave + 8 * g + 4 * h + e, u = 4 * g + e;
+#pragma unroll
+        for (int c = 0; c < C; ++c) part[f * C + c] = dwacc[u][c];
+        part[F0 * C + f] = dbacc[u];
+      }
+  }
+}
+
+template <int BOTC, bool DXOUT, bool REC = false, int TOPO = 0>
+DEV void dx_ring_body(const NTArgs& a, char* smem, const int64_t t0, const int64_t G, const int64_t niter,
+                      const int64_t slab) {
+  if constexpr (BOTC == 0) dx_ring_body_v2<TOPO>(a, smem, t0, G, niter);
+  else if constexpr (REC) dx_ring_body_v2bot<BOTC, DXOUT>(a, smem, t0, G, niter, slab);
+  else dx_ring_body_v1<BOTC, DXOUT, REC, TOPO>(a, smem, t0, G, niter, slab);
 }
 
 template <int BOTC, bool DXOUT, bool REC = false, int TOPO = 0>
