@@ -174,6 +174,23 @@ typedef struct siren_adam_desc {
 int siren_adam_step(const siren_adam_desc* d, void* stream);
 
 /*
+ * Weighted sum of squared errors of image_mse (replaces loss_functions.py:66-101's
+ *   diff = mask * (pred - gt); (diff.abs() ** 2).sum() * weight   and its autograd backward).
+ * forward : d[e] = m[e % mask_n] (pred[e] - tgt[e]); *loss = weight * sum_e d[e]^2 (device
+ *           scalar; deterministic summation order). mask may be NULL (no mask). `workspace` holds
+ *           siren_sse_workspace_bytes() bytes, zero-filled before its first use and left zeroed by
+ *           every call; one call at a time per workspace.
+ * backward: out[e] = m[e % mask_n] (d[e] (g[0] scale)) with scale = 2 weight and g the upstream
+ *           gradient (device scalar).
+ * All pointers are device pointers of float32 data; stream is a hipStream_t (NULL = default).
+ */
+int64_t siren_sse_workspace_bytes(void);
+int siren_sse_forward(const float* pred, const float* tgt, const float* mask, int64_t n, int64_t mask_n,
+                      float weight, float* d, float* loss, void* workspace, int64_t ws_bytes, void* stream);
+int siren_sse_backward(const float* d, const float* mask, int64_t n, int64_t mask_n, const float* g, float scale,
+                       float* out, void* stream);
+
+/*
  * Process-wide execution options (no reference counterpart; used by tests and benchmarks to
  * compare code paths). Keys:
  *   "fused_forward"  1 (default): bf16 stacks of equal power-of-two hidden widths run their

@@ -39,6 +39,9 @@ EXPORTED_SYMBOLS = (
     "siren_config_set",
     "siren_config_get",
     "siren_adam_step",
+    "siren_sse_workspace_bytes",
+    "siren_sse_forward",
+    "siren_sse_backward",
     "siren_last_error",
     "siren_version",
 )
@@ -147,6 +150,13 @@ def _declare(lib):
     lib.siren_config_get.restype = i64
     lib.siren_adam_step.argtypes = [ctypes.POINTER(SirenAdamDesc), vp]
     lib.siren_adam_step.restype = ctypes.c_int
+    f32 = ctypes.c_float
+    lib.siren_sse_workspace_bytes.argtypes = []
+    lib.siren_sse_workspace_bytes.restype = i64
+    lib.siren_sse_forward.argtypes = [vp, vp, vp, i64, i64, f32, vp, vp, vp, i64, vp]
+    lib.siren_sse_forward.restype = ctypes.c_int
+    lib.siren_sse_backward.argtypes = [vp, vp, i64, i64, vp, f32, vp, vp]
+    lib.siren_sse_backward.restype = ctypes.c_int
     lib.siren_last_error.argtypes = []
     lib.siren_last_error.restype = ctypes.c_char_p
     lib.siren_version.argtypes = []

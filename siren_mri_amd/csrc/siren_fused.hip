@@ -301,6 +301,7 @@ __global__ __launch_bounds__(512) void fused_fwd_bf16_kernel(FusedFwdArgs a) {
 //   Wfrag[b][l][fb][ks][lane][j] = W_l[b][32 fb + (lane & 31)][16 ks + 8 (lane >> 5) + j]
 struct FragPrepArgs {
   const float* W[FUSED_MAXH];  // hidden layer weights [nb_w][F, F] fp32
+  bf16* Wt[FUSED_MAXH];        // optional: the backward's transposed bf16 copy [nb_w][F (in), F (out)]
   bf16* out;
   int64_t nb;
   int F, nh;
@@ -327,6 +328,11 @@ __global__ __launch_bounds__(256) void prep_frag_kernel(FragPrepArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = (bf16)src[j];
     *(bf16x8*)(a.out + idx * 8) = v;
+    if (a.Wt[l]) {  // W^T[i][o] for the 8 inputs i of this slice, o = 32 fb + (lane & 31)
+      bf16* dst = a.Wt[l] + b * per_layer + (int64_t)(16 * ks + 8 * (lane >> 5)) * F + 32 * fb + (lane & 31);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dst[(int64_t)j * F] = v[j];
+    }
   }
 }
 

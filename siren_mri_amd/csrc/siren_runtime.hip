@@ -13,6 +13,7 @@
 #include "siren_jvp.hip"
 #include "siren_fused.hip"
 #include "siren_adam.hip"
+#include "siren_loss.hip"
 
 using namespace siren;
 
@@ -302,6 +303,32 @@ int launch_reduce(const float* part, int64_t nsplit, int64_t sstride, int64_t nb
   return check_launch("reduce");
 }
 
+// Up to REDUCE_MAXSEG reductions (same arguments as launch_reduce) in one launch.
+struct ReduceList {
+  ReduceMultiArgs a;
+  int64_t blocks = 0;
+  ReduceList() { memset(&a, 0, sizeof(a)); }
+  void add(const float* part, int64_t nsplit, int64_t sstride, int64_t nb, int64_t slab, int64_t n_first, float* out0,
+           float* out1) {
+    ReduceSeg& g = a.seg[a.nseg++];
+    g.part = part;
+    g.nsplit = (int)nsplit;
+    g.split_stride = sstride;
+    g.total = (int)(nb * slab);
+    g.slab = (int)slab;
+    g.n_first = (int)n_first;
+    g.out0 = out0;
+    g.out1 = out1;
+    g.blocks = (int)cdiv(nb * slab, 128);
+    blocks += g.blocks;
+  }
+  int launch(hipStream_t st) {
+    if (a.nseg == 0) return SIREN_OK;
+    hipLaunchKernelGGL(reduce_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
+    return check_launch("reduce_multi");
+  }
+};
+
 // Convert every MFMA layer's weights (bf16 copy + transpose) into `dst` in one launch.
 template <int PREC>
 int prep_weights(const siren_mlp_desc* d, const Geo& g, const Layout& lo, char* dst, hipStream_t st) {
@@ -449,7 +476,11 @@ int fused_forward(const siren_mlp_desc* d, const Geo& g, const Layout& lo, const
   if (nh > 0) {
     FragPrepArgs fp;
     memset(&fp, 0, sizeof(fp));
-    for (int l = 1; l + 1 < g.L; ++l) fp.W[l - 1] = d->weight[l];
+    for (int l = 1; l + 1 < g.L; ++l) {
+      fp.W[l - 1] = d->weight[l];
+      // the backward's W^T copies, written by the same launch (prep_weights is skipped)
+      fp.Wt[l - 1] = saved ? (bf16*)(saved + lo.wt_op_off[l]) : nullptr;
+    }
     fp.out = (bf16*)(wbuf + lo.frag_off);
     fp.nb = g.nb;
     fp.F = F;
@@ -501,10 +532,9 @@ int forward_impl(const siren_mlp_desc* d, const float* x, float* y, char* saved,
   const Layout lo = layout_of(d);
   char* wbuf = saved ? saved : ws;  // prepared weights live in `saved` so backward reuses them
   const bool fused = PREC == kPrecBF16 && g_fused_forward && fused_shape(d);
-  if (fused && !saved) return fused_forward(d, g, lo, x, y, nullptr, wbuf, st);
+  if (fused) return fused_forward(d, g, lo, x, y, saved, wbuf, st);  // prepares its own weights
   int rc = prep_weights<PREC>(d, g, lo, wbuf, st);
   if (rc) return rc;
-  if (fused) return fused_forward(d, g, lo, x, y, saved, wbuf, st);
   auto phase_buf = [&](int l) -> char* {
     if (saved && lo.saved_off[l] >= 0) return saved + lo.saved_off[l];
     return ws + lo.pp_off[l & 1];  // (P_0 of a recompute stack: only layer 1 reads it)
@@ -658,16 +688,11 @@ int launch_pair(const siren_mlp_desc* d, const Geo& g, const Layout& lo, int kin
   tmark_end(kcls, st);
   int rc = check_launch("pair_ring");
   if (rc) return rc;
-  if ((rc = launch_reduce(part, npair, w.split_stride, g.nb, (int64_t)M * N + M, (int64_t)M * N, dW[l], db[l], st)))
-    return rc;
-  if (kind == 2 &&
-      (rc = launch_reduce(ta.partL, npair, ta.partL_stride, g.nb, (int64_t)O * M + O, (int64_t)O * M, dW[g.L - 1],
-                          db[g.L - 1], st)))
-    return rc;
-  if (kind == 3 && (rc = launch_reduce(a.bot.part, npair, bot_stride, g.nb, (int64_t)F0 * C + F0, (int64_t)F0 * C,
-                                       dW[0], db[0], st)))
-    return rc;
-  return SIREN_OK;
+  ReduceList red;
+  red.add(part, npair, w.split_stride, g.nb, (int64_t)M * N + M, (int64_t)M * N, dW[l], db[l]);
+  if (kind == 2) red.add(ta.partL, npair, ta.partL_stride, g.nb, (int64_t)O * M + O, (int64_t)O * M, dW[g.L - 1], db[g.L - 1]);
+  if (kind == 3) red.add(a.bot.part, npair, bot_stride, g.nb, (int64_t)F0 * C + F0, (int64_t)F0 * C, dW[0], db[0]);
+  return red.launch(st);
 }
 
 template <int PREC>
@@ -1419,6 +1444,49 @@ void siren_timing_disable(void) {
     delete[] g_timing.ev;
   }
   g_timing = Timing();
+}
+
+int64_t siren_sse_workspace_bytes(void) { return (int64_t)SSE_MAX_BLOCKS * 4 + 256; }
+
+int siren_sse_forward(const float* pred, const float* tgt, const float* mask, int64_t n, int64_t mask_n,
+                      float weight, float* d, float* loss, void* workspace, int64_t ws_bytes, void* stream) {
+  if (n < 0 || !loss || (n > 0 && (!pred || !tgt || !d)) || (mask && mask_n <= 0))
+    return fail(SIREN_EINVAL, "sse_forward: bad arguments (n=%lld, mask_n=%lld)", (long long)n, (long long)mask_n);
+  if (!workspace || ws_bytes < siren_sse_workspace_bytes())
+    return fail(SIREN_EINVAL, "sse_forward: workspace of %lld bytes, need %lld", (long long)ws_bytes,
+                (long long)siren_sse_workspace_bytes());
+  SseFwdArgs a;
+  a.pred = pred;
+  a.tgt = tgt;
+  a.mask = mask;
+  a.d = d;
+  a.loss = loss;
+  a.partial = (float*)workspace;
+  a.counter = (unsigned*)((char*)workspace + SSE_MAX_BLOCKS * 4);
+  a.n = n;
+  a.mask_n = mask ? mask_n : 1;
+  a.weight = weight;
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(SSE_MAX_BLOCKS, cdiv(n, 4 * SSE_THREADS)));
+  hipLaunchKernelGGL(sse_fwd_kernel, dim3(blocks), dim3(SSE_THREADS), 0, (hipStream_t)stream, a);
+  return check_launch("sse_forward");
+}
+
+int siren_sse_backward(const float* d, const float* mask, int64_t n, int64_t mask_n, const float* g, float scale,
+                       float* out, void* stream) {
+  if (n < 0 || (n > 0 && (!d || !g || !out)) || (mask && mask_n <= 0))
+    return fail(SIREN_EINVAL, "sse_backward: bad arguments (n=%lld, mask_n=%lld)", (long long)n, (long long)mask_n);
+  if (n == 0) return SIREN_OK;
+  SseBwdArgs a;
+  a.d = d;
+  a.mask = mask;
+  a.g = g;
+  a.out = out;
+  a.n = n;
+  a.mask_n = mask ? mask_n : 1;
+  a.scale = scale;
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(4096, cdiv(n, 4 * SSE_THREADS)));
+  hipLaunchKernelGGL(sse_bwd_kernel, dim3(blocks), dim3(SSE_THREADS), 0, (hipStream_t)stream, a);
+  return check_launch("sse_backward");
 }
 
 int siren_adam_step(const siren_adam_desc* d, void* stream) {

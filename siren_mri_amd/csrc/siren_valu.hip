@@ -519,6 +519,57 @@ __global__ __launch_bounds__(256) void reduce_kernel(const float* part, int nspl
   }
 }
 
+// Several reductions in one launch (the slabs of one backward kernel: a layer's dW/db and the
+// folded first or output layer's): block b belongs to the segment whose block range holds it.
+// Each segment's arithmetic is reduce_kernel's (same summation order).
+constexpr int REDUCE_MAXSEG = 3;
+struct ReduceSeg {
+  const float* part;
+  float* out0;
+  float* out1;
+  int64_t split_stride;
+  int nsplit, total, slab, n_first, blocks;
+};
+struct ReduceMultiArgs {
+  ReduceSeg seg[REDUCE_MAXSEG];
+  int nseg;
+};
+__global__ __launch_bounds__(256) void reduce_multi_kernel(ReduceMultiArgs a) {
+  __shared__ f32x4 red[8][32];
+  int blk = blockIdx.x, si = 0;
+  while (si + 1 < a.nseg && blk >= a.seg[si].blocks) blk -= a.seg[si++].blocks;
+  const ReduceSeg& g = a.seg[si];
+  const int c4 = threadIdx.x & 31, sl = threadIdx.x >> 5;
+  const int base = (blk * 32 + c4) * 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (base < g.total) {
+    int s = sl;
+    for (; s + 24 < g.nsplit; s += 32) {
+      const f32x4 v0 = *(const f32x4*)(g.part + (int64_t)s * g.split_stride + base);
+      const f32x4 v1 = *(const f32x4*)(g.part + (int64_t)(s + 8) * g.split_stride + base);
+      const f32x4 v2 = *(const f32x4*)(g.part + (int64_t)(s + 16) * g.split_stride + base);
+      const f32x4 v3 = *(const f32x4*)(g.part + (int64_t)(s + 24) * g.split_stride + base);
+      acc += (v0 + v1) + (v2 + v3);
+    }
+    for (; s < g.nsplit; s += 8) acc += *(const f32x4*)(g.part + (int64_t)s * g.split_stride + base);
+  }
+  red[sl][c4] = acc;
+  __syncthreads();
+  if (sl == 0 && base < g.total) {
+    f32x4 t = red[0][c4];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) t += red[k][c4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = base + e;
+      if (idx >= g.total) break;
+      const int b = idx / g.slab, r = idx - b * g.slab;
+      if (r < g.n_first) g.out0[(int64_t)b * g.n_first + r] = t[e];
+      else g.out1[(int64_t)b * (g.slab - g.n_first) + (r - g.n_first)] = t[e];
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Weight preparation for every MFMA layer in one launch (blockIdx.y = layer):
 // W [nb][O][I] fp32 -> Wop [nb][O][I] op_t (bf16 only) and WtOp [nb][I][O] op_t.

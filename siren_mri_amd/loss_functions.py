@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import torch
 
-from . import diff_operators
+from . import _native, diff_operators
 from .dataio import lin2img
 from .utils import create_circular_mask_torch
 
@@ -33,29 +33,52 @@ def _high_freq_mask(device):
     return m
 
 
+_SSE_WS: dict = {}
+
+
+def _sse_workspace(device):
+    ws = _SSE_WS.get(device)
+    if ws is None:
+        ws = torch.zeros(int(_native.lib().siren_sse_workspace_bytes()), dtype=torch.uint8, device=device)
+        _SSE_WS[device] = ws
+    return ws
+
+
 class _WeightedSSE(torch.autograd.Function):
-    """sum((m * (pred - tgt))^2) * w for real pred and a constant target: forward = one
-    subtraction (+ mask) and one dot product; backward = one scaled multiply, 2 w m^2 (pred - tgt) g
-    — the same values as the autograd chain of (diff.abs() ** 2).sum() * w, in 3-4 kernels
-    instead of ~12."""
+    """sum((m * (pred - tgt))^2) * w for real pred and a constant target on the native kernels
+    (siren_sse_forward / siren_sse_backward, siren_loss.hip): forward = one launch (d = m (pred -
+    tgt) and the deterministic weighted sum), backward = one launch, 2 w m^2 (pred - tgt) g — the
+    values of the autograd chain of (diff.abs() ** 2).sum() * w in 2 launches instead of ~6."""
 
     @staticmethod
     def forward(ctx, pred, tgt, mask, weight):
-        d = pred - tgt
-        if mask is not None:
-            d = mask * d
-        ctx.save_for_backward(d, mask)
+        predc, tgtc = pred.contiguous(), tgt.contiguous()
+        maskc = mask.contiguous() if mask is not None else None
+        n = predc.numel()
+        d = torch.empty_like(predc)
+        loss = torch.empty((), dtype=torch.float32, device=pred.device)
+        ws = _sse_workspace(pred.device)
+        rc = _native.lib().siren_sse_forward(
+            predc.data_ptr(), tgtc.data_ptr(), maskc.data_ptr() if maskc is not None else None, n,
+            maskc.numel() if maskc is not None else 0, float(weight), d.data_ptr(), loss.data_ptr(),
+            ws.data_ptr(), ws.numel(), _native.stream_handle(pred.device))
+        _native.check(rc, "siren_sse_forward")
+        ctx.save_for_backward(d, maskc)
         ctx.weight = weight
-        flat = d.reshape(-1)
-        return torch.dot(flat, flat) * weight
+        ctx.shape = pred.shape
+        return loss
 
     @staticmethod
     def backward(ctx, g):
         d, mask = ctx.saved_tensors
-        gd = d * (g * (2.0 * ctx.weight))
-        if mask is not None:
-            gd = mask * gd
-        return gd, None, None, None
+        gc = g.contiguous().to(torch.float32)
+        out = torch.empty_like(d)
+        rc = _native.lib().siren_sse_backward(
+            d.data_ptr(), mask.data_ptr() if mask is not None else None, d.numel(),
+            mask.numel() if mask is not None else 0, gc.data_ptr(), float(2.0 * ctx.weight), out.data_ptr(),
+            _native.stream_handle(d.device))
+        _native.check(rc, "siren_sse_backward")
+        return out.view(ctx.shape), None, None, None
 
 
 def image_mse(mask, model_output, gt, high_freq=True):
@@ -63,8 +86,9 @@ def image_mse(mask, model_output, gt, high_freq=True):
     pred = lin2img(model_output["model_out"])
     tgt = lin2img(gt["img"])
     hf = _high_freq_mask(pred.device) if (high_freq and pred.shape[-2:] == (128, 128)) else None
-    if (pred.dtype == torch.float32 and tgt.dtype == torch.float32 and not tgt.requires_grad
-            and pred.shape == tgt.shape and (hf is None or hf.dtype == torch.float32)):
+    if (pred.is_cuda and pred.dtype == torch.float32 and tgt.dtype == torch.float32 and not tgt.requires_grad
+            and pred.shape == tgt.shape and tgt.device == pred.device
+            and (hf is None or (hf.dtype == torch.float32 and pred.shape[-hf.dim():] == hf.shape))):
         return {"img_loss": _WeightedSSE.apply(pred, tgt, hf, _KSPACE_WEIGHT)}
     diff = pred - tgt
     if hf is not None:

@@ -247,8 +247,9 @@ class SingleBVPNet(MetaModule):
             print(self)
 
     def forward(self, model_input, params=None):
-        # grad leaf for derivatives w.r.t. coordinates (modules.py:151)
-        coords_org = model_input["coords"].clone().detach().requires_grad_(True)
+        # grad leaf for derivatives w.r.t. coordinates (modules.py:151). The reference clones first;
+        # a detached alias is the same leaf without a copy (nothing writes coordinates in place).
+        coords_org = model_input["coords"].detach().requires_grad_(True)
         coords = coords_org
         if self.image_downsampling.downsample:
             coords = self.image_downsampling(coords)
