@@ -1229,24 +1229,33 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
     const int64_t n = rows - t * BM;
     return n < BM ? n : BM;
   };
-  auto dma = [&](int64_t t, int st) {
+  // DMA of tile t into slot st, in parts (0: dZ / P_top pieces + dy, 1: P pieces) so the main
+  // loop can spread the issue of the next stage's pieces between its MFMAs
+  auto dma_part = [&](int64_t t, int st, int part) {
     char* base = smem + st * STAGE;
     const int64_t m0 = rowbase + t * BM, nv = nval(t);
-    const __amdgpu_buffer_rsrc_t rA = make_rsrc((const bf16*)(TOPO > 0 ? a.top.Ptop : a.A) + m0 * K, nv * K * 2);
-    const __amdgpu_buffer_rsrc_t rP = make_rsrc((const uint16_t*)a.Paux + m0 * N, nv * N * 2);
+    if (part == 0) {
+      const __amdgpu_buffer_rsrc_t rA = make_rsrc((const bf16*)(TOPO > 0 ? a.top.Ptop : a.A) + m0 * K, nv * K * 2);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(base + (wave + 8 * j) * 1024), 16, dvoff[j], 0, 0, 0);
-    if constexpr (TOPO > 0) {
-      const __amdgpu_buffer_rsrc_t rG = make_rsrc(a.top.dy + m0 * TOPO, nv * TOPO * 4);
-      if (lane < TOPO)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rG, (lds_void*)(base + A_BYTES + C_BYTES + 16 * TOPO * wave), 16,
-                                                 16 * (TOPO * wave + lane), 0, 0, 0);
+      for (int j = 0; j < 2; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(base + (wave + 8 * j) * 1024), 16, dvoff[j], 0, 0, 0);
+      if constexpr (TOPO > 0) {
+        const __amdgpu_buffer_rsrc_t rG = make_rsrc(a.top.dy + m0 * TOPO, nv * TOPO * 4);
+        if (lane < TOPO)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rG, (lds_void*)(base + A_BYTES + C_BYTES + 16 * TOPO * wave), 16,
+                                                   16 * (TOPO * wave + lane), 0, 0, 0);
+      }
+    } else {
+      const __amdgpu_buffer_rsrc_t rP = make_rsrc((const uint16_t*)a.Paux + m0 * N, nv * N * 2);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (lds_void*)(base + A_BYTES + (wave + 8 * j) * 1024), 16,
+                                                 dvoff[j], 0, 0, 0);
     }
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (lds_void*)(base + A_BYTES + (wave + 8 * j) * 1024), 16, dvoff[j],
-                                               0, 0, 0);
+  };
+  auto dma = [&](int64_t t, int st) {
+    dma_part(t, st, 0);
+    dma_part(t, st, 1);
   };
 
   // epilogue of tile t held in slot st with accumulator acc: dZ_{l-1} = acc cos(P) w0 (4 features
@@ -1286,6 +1295,7 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
     prof.tick(0);
     lds_barrier();
     prof.tick(1);
+    // (issuing these pieces between the MFMAs instead measured slower)
     if (i + S - 1 < niter) dma(t0 + (i + S - 1) * G, (int)((i + S - 1) % S));
     prof.tick(2);
     char* base = smem + st * STAGE;
