@@ -63,8 +63,13 @@ template <> struct Prec<kPrecBF16> {
     return enc_scaled(z, b * k, k);
   }
   // the same with the bias already multiplied by k = enck(w0)
+  // v_cvt_rpi_i32_f32 = floor(v + 0.5): one instruction for the round-and-convert (ties round up
+  // instead of to even; every encoder and every recompute of a phase uses this same form)
   static DEV phase_t enc_scaled(float z, float bk, float k) {
-    return (uint16_t)(int)__builtin_rintf(fmaf(z, k, bk));
+    const float v = fmaf(z, k, bk);
+    int r;
+    asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(v));
+    return (uint16_t)r;
   }
   static DEV float rev(phase_t v) { return (float)v * (1.0f / 65536.0f); }
   // v_sin_f32 / v_cos_f32 take revolutions and reduce them exactly: the float with bits

@@ -48,6 +48,7 @@ struct FusedFwdArgs {
   int C, F, O, nh;
   int sine_out;
   float w0;
+  int dbg;                        // debug timing only: bit 0 skips the K-loop fillers, bit 1 the VALU segment
 };
 
 constexpr int FUSED_NPROF = 4;    // layer-0 pass, MFMA K loop, epilogue, convert pass
@@ -410,6 +411,8 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
   if (tid < O) Swl[FUSED_MAXO * F + tid] = a.bL[wb * O + tid];
   for (int i = tid; i < 2 * NW * HB * FUSED_MAXO; i += NT) (&Yp[0][0][0])[i] = 0.f;
 
+  // (an XOR-swizzled 512-byte-row layout without the chunk-task bank conflicts measured slower:
+  // per-step address math and 19 spilled registers)
   auto h_off = [&](int r, int c) -> int { return r * RS + (c << 4); };
 
   // W fragments (fragment order, see prep_frag_kernel); wave w takes blocks FB w .. FB w + FB - 1.
@@ -432,10 +435,12 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
   auto x_issue = [&](int64_t t) {
 #pragma unroll
     for (int k = 0; k < NX; ++k) {
-      const int i = tid + NT * k;
+      // an in-range index for every lane (lanes past the tile's BM * C values are never parked):
+      // no select on the loaded value, so nothing waits for the load before x_park
+      const int i = (tid + NT * k) < BM * C ? tid + NT * k : 0;
       int64_t r = t * BM + i / C;
       r = r < rows ? r : rows - 1;
-      xr[k] = (i < BM * C) ? a.x[(batch * rows + r) * C + (i % C)] : 0.f;
+      xr[k] = a.x[(batch * rows + r) * C + (i % C)];
     }
   };
   auto x_park = [&](int xb) {
@@ -575,7 +580,7 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
 #pragma unroll
         for (int fb = 0; fb < FB; ++fb) wreg[fb][ks] = wfrag(lref, fb, ks);
       }
-      filler(ks);
+      if (!(a.dbg & 1)) filler(ks);
     }
   };
   auto EC = [&](int64_t t, int h, const f32x16 (&acc)[FB][2], int lh, auto last_tag) {
@@ -620,10 +625,12 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
     const bool more = t + G < ntiles;
     // seg 0: L0(A) + EC(nh, B) of the previous tile (+ its y rows of half A); x(t + G) issued first
     if (more) x_issue(t + G);
-    L0(t, 0, xb);
-    if (have_prev) {
-      EC(tp, 1, accB, nh - 1, T_{});
-      Ypass(tp, 0);
+    if (!(a.dbg & 2)) {
+      L0(t, 0, xb);
+      if (have_prev) {
+        EC(tp, 1, accB, nh - 1, T_{});
+        Ypass(tp, 0);
+      }
     }
     fused_barrier();
     // seg 1: K(1, A) + L0(B) (+ previous tile's y rows of half B); park x(t + G)

@@ -88,7 +88,8 @@ bool g_pair_ring = true;   // both gradients of a ring layer in one launch (pair
 int g_pair_roles = 3;      // debug timing: which pair_ring roles run (results are wrong unless 3)
 long long* g_ring_prof = nullptr;   // debug: pair_ring segment cycle counters, one block per launch
 int g_ring_prof_n = 0;
-long long* g_fused_prof = nullptr;  // debug: per-workgroup phase cycle counters of the fused forward
+long long* g_fused_prof = nullptr;
+int g_fwd_dbg = 0;  // debug timing: fused_fwd_pipe_kernel skip bits (results wrong unless 0)  // debug: per-workgroup phase cycle counters of the fused forward
 bool fused_shape(const siren_mlp_desc* d) {
   if (d->prec != SIREN_PREC_BF16) return false;
   if (d->dims[0] > FUSED_MAXC || d->dims[d->num_layers] > FUSED_MAXO) return false;
@@ -502,6 +503,7 @@ int fused_forward(const siren_mlp_desc* d, const Geo& g, const Layout& lo, const
   for (int l = 0; l + 1 < g.L; ++l) a.P[l] = (saved && lo.saved_off[l] >= 0) ? saved + lo.saved_off[l] : nullptr;
   a.y = y;
   a.prof = g_fused_prof;
+  a.dbg = g_fwd_dbg;
   a.rows_per_batch = g.rows;
   a.batched = d->weights_batched ? 1 : 0;
   a.C = d->dims[0];
@@ -1564,6 +1566,10 @@ int siren_config_set(const char* key, int64_t value) {
   if (key && strcmp(key, "debug_ring_profile") == 0) {  // device pointer or 0
     g_ring_prof = (long long*)(intptr_t)value;
     g_ring_prof_n = 0;
+    return SIREN_OK;
+  }
+  if (key && strcmp(key, "debug_fwd_skip") == 0 && value >= 0 && value <= 3) {
+    g_fwd_dbg = (int)value;
     return SIREN_OK;
   }
   if (key && strcmp(key, "debug_fused_profile") == 0) {  // device pointer or 0
