@@ -170,8 +170,14 @@ typedef struct siren_adam_desc {
   const float* grad[SIREN_ADAM_MAX_TENSORS];
   float* exp_avg[SIREN_ADAM_MAX_TENSORS];
   float* exp_avg_sq[SIREN_ADAM_MAX_TENSORS];
+  const float* dev_scalars;      /* NULL, or device {step_size, bias_correction2_sqrt} read by the
+                                    kernel (written by siren_adam_scalars: hipGraph replays) */
 } siren_adam_desc;
 int siren_adam_step(const siren_adam_desc* d, void* stream);
+/* Device-side bias corrections for graph-captured steps: *t += 1, then
+ * out[0] = -(lr / (1 - beta1^t)), out[1] = sqrt(1 - beta2^t), computed in double and rounded to
+ * float as the host path does (t, out: device pointers). One single-thread launch. */
+int siren_adam_scalars(double* t, double lr, double beta1, double beta2, float* out, void* stream);
 
 /*
  * Weighted sum of squared errors of image_mse (replaces loss_functions.py:66-101's

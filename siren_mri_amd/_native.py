@@ -39,6 +39,7 @@ EXPORTED_SYMBOLS = (
     "siren_config_set",
     "siren_config_get",
     "siren_adam_step",
+    "siren_adam_scalars",
     "siren_sse_workspace_bytes",
     "siren_sse_forward",
     "siren_sse_backward",
@@ -102,6 +103,7 @@ class SirenAdamDesc(ctypes.Structure):
         ("grad", ctypes.c_void_p * ADAM_MAX_TENSORS),
         ("exp_avg", ctypes.c_void_p * ADAM_MAX_TENSORS),
         ("exp_avg_sq", ctypes.c_void_p * ADAM_MAX_TENSORS),
+        ("dev_scalars", ctypes.c_void_p),
     ]
 
 
@@ -151,6 +153,9 @@ def _declare(lib):
     lib.siren_adam_step.argtypes = [ctypes.POINTER(SirenAdamDesc), vp]
     lib.siren_adam_step.restype = ctypes.c_int
     f32 = ctypes.c_float
+    f64 = ctypes.c_double
+    lib.siren_adam_scalars.argtypes = [vp, f64, f64, f64, vp, vp]
+    lib.siren_adam_scalars.restype = ctypes.c_int
     lib.siren_sse_workspace_bytes.argtypes = []
     lib.siren_sse_workspace_bytes.restype = i64
     lib.siren_sse_forward.argtypes = [vp, vp, vp, i64, i64, f32, vp, vp, vp, i64, vp]
@@ -285,6 +290,11 @@ class KernelTimer:
         self.total_ms = tot.value
         self.launches = n.value
         return False
+
+    def reset(self):
+        """Drop the launches recorded so far and start again (same class and capacity)."""
+        lib().siren_timing_disable()
+        check(lib().siren_timing_enable(self.kernel_class, self.max_launches), "siren_timing_enable")
 
     @property
     def avg_ms(self) -> float:

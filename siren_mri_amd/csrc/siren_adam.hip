@@ -16,8 +16,16 @@ struct AdamArgs {
   float* exp_avg_sq[SIREN_ADAM_MAX_TENSORS];
   int64_t numel[SIREN_ADAM_MAX_TENSORS];
   float one_minus_beta1, beta2, one_minus_beta2, eps, weight_decay, step, bc2_sqrt;
+  const float* dev;  // null, or device {step, bc2_sqrt} (graph-captured steps)
   int maximize;
 };
+
+__global__ void adam_scalars_kernel(double* t, double lr, double beta1, double beta2, float* out) {
+  const double tt = *t + 1.0;
+  *t = tt;
+  out[0] = (float)((lr / (1.0 - pow(beta1, tt))) * -1.0);
+  out[1] = (float)sqrt(1.0 - pow(beta2, tt));
+}
 
 DEV float torch_lerp(float self, float end, float w) {
   return fabsf(w) < 0.5f ? self + w * (end - self) : end - (end - self) * (1.f - w);
@@ -30,6 +38,8 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   const float* gr = a.grad[t];
   float* m = a.exp_avg[t];
   float* v = a.exp_avg_sq[t];
+  const float step = a.dev ? a.dev[0] : a.step;
+  const float bc2_sqrt = a.dev ? a.dev[1] : a.bc2_sqrt;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     float g = gr[i];
     if (a.maximize) g = -g;
@@ -38,11 +48,11 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
     const float mv = torch_lerp(m[i], g, a.one_minus_beta1);
     float vv = v[i] * a.beta2;
     vv = vv + a.one_minus_beta2 * (g * g);
-    float d = sqrtf(vv) / a.bc2_sqrt;
+    float d = sqrtf(vv) / bc2_sqrt;
     d = d + a.eps;
     m[i] = mv;
     v[i] = vv;
-    p[i] = pv + a.step * (mv / d);
+    p[i] = pv + step * (mv / d);
   }
 }
 

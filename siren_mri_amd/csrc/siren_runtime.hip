@@ -1448,6 +1448,12 @@ void siren_timing_disable(void) {
   g_timing = Timing();
 }
 
+int siren_adam_scalars(double* t, double lr, double beta1, double beta2, float* out, void* stream) {
+  if (!t || !out) return fail(SIREN_EINVAL, "adam_scalars: null pointer");
+  hipLaunchKernelGGL(adam_scalars_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, t, lr, beta1, beta2, out);
+  return check_launch("adam_scalars");
+}
+
 int64_t siren_sse_workspace_bytes(void) { return (int64_t)SSE_MAX_BLOCKS * 4 + 256; }
 
 int siren_sse_forward(const float* pred, const float* tgt, const float* mask, int64_t n, int64_t mask_n,
@@ -1515,6 +1521,7 @@ int siren_adam_step(const siren_adam_desc* d, void* stream) {
   a.weight_decay = d->weight_decay;
   a.step = d->step_size;
   a.bc2_sqrt = d->bias_correction2_sqrt;
+  a.dev = d->dev_scalars;
   a.maximize = d->maximize;
   if (maxn == 0) return SIREN_OK;
   hipLaunchKernelGGL(adam_kernel, dim3(grid1d(maxn, 1024), (unsigned)d->num_tensors), dim3(256), 0,

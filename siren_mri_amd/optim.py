@@ -18,6 +18,29 @@ from . import _native
 
 
 class Adam(torch.optim.Adam):
+    """torch.optim.Adam whose step is one native launch (see the module docstring).
+
+    ``enable_graph_mode()`` makes the step hipGraph-capturable: the bias corrections come from a
+    device-side step counter (siren_adam_scalars, one extra single-thread launch) instead of
+    host floats baked into the captured launch. The host-side ``state['step']`` keeps counting
+    eager calls only; ``sync_graph_steps()`` copies the device counters back into it."""
+
+    _graph_mode = False
+
+    def enable_graph_mode(self):
+        self._graph_mode = True
+        self._dev_step = {}
+
+    def sync_graph_steps(self):
+        for group in self.param_groups:
+            dev = getattr(self, "_dev_step", {}).get(id(group))
+            if dev is None:
+                continue
+            t = float(dev[0].item())
+            for p in group["params"]:
+                if p in self.state and "step" in self.state[p]:
+                    self.state[p]["step"].fill_(t)
+
     def _native_ok(self, group) -> bool:
         if group["amsgrad"] or group.get("capturable") or group.get("differentiable") or group.get("fused"):
             return False
@@ -70,6 +93,20 @@ class Adam(torch.optim.Adam):
                 st["step"] += 1
                 by_step.setdefault(float(st["step"].item()), []).append(p)
             stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+            dev_scalars = None
+            if self._graph_mode:
+                if len(by_step) != 1:
+                    raise RuntimeError("siren_mri_amd.optim.Adam: graph mode needs one step count per group")
+                dev = self._dev_step.get(id(group))
+                if dev is None:
+                    t0 = next(iter(by_step)) - 1
+                    dev = (torch.full((1,), t0, dtype=torch.float64, device=params[0].device),
+                           torch.zeros(2, dtype=torch.float32, device=params[0].device))
+                    self._dev_step[id(group)] = dev
+                if lib.siren_adam_scalars(dev[0].data_ptr(), float(group["lr"]), float(beta1), float(beta2),
+                                          dev[1].data_ptr(), stream) != 0:
+                    raise _native.NativeError(_native.last_error())
+                dev_scalars = dev[1].data_ptr()
             for t, plist in by_step.items():
                 bc1 = 1 - beta1 ** t
                 bc2 = 1 - beta2 ** t
@@ -83,6 +120,7 @@ class Adam(torch.optim.Adam):
                     d.one_minus_beta1, d.one_minus_beta2 = 1 - beta1, 1 - beta2
                     d.step_size = (group["lr"] / bc1) * -1
                     d.bias_correction2_sqrt = bc2 ** 0.5
+                    d.dev_scalars = dev_scalars
                     for k, p in enumerate(chunk):
                         st = self.state[p]
                         d.numel[k] = p.numel()

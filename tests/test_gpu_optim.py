@@ -42,3 +42,35 @@ def test_adam_state_dict_round_trip_with_torch():
     o2 = torch.optim.Adam([p], lr=1e-2)
     o2.load_state_dict(o1.state_dict())
     assert torch.equal(o2.state[p]["exp_avg"], o1.state[p]["exp_avg"])
+
+
+def test_adam_graph_mode_replay_matches_eager():
+    """enable_graph_mode(): bias corrections from a device step counter, so a hipGraph of the
+    step replays with the right t each time (same values as eager steps)."""
+    from siren_mri_amd.optim import Adam
+    g = torch.Generator().manual_seed(1)
+    init = torch.randn(300, generator=g)
+    grads = [torch.randn(300, generator=g).to(DEV) for _ in range(6)]
+    p_e = torch.nn.Parameter(init.clone().to(DEV))
+    o_e = Adam([p_e], lr=1e-2)
+    for gr in grads:
+        p_e.grad = gr.clone()
+        o_e.step()
+    p_g = torch.nn.Parameter(init.clone().to(DEV))
+    o_g = Adam([p_g], lr=1e-2)
+    o_g.enable_graph_mode()
+    gbuf = torch.empty(300, device=DEV)
+    p_g.grad = gbuf
+    gbuf.copy_(grads[0])
+    o_g.step()  # eager first step creates the device counter (t = 1)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        o_g.step()
+    for gr in grads[1:]:
+        gbuf.copy_(gr)
+        graph.replay()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(p_g.detach(), p_e.detach(), rtol=1e-6, atol=1e-7)
+    o_g.sync_graph_steps()
+    # the capture itself does not step: 1 eager + 5 replays = 6 steps, like the eager optimizer
+    assert float(o_g.state[p_g]["step"]) == 6.0
