@@ -320,6 +320,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.precision,
+        "precision_detail": ("forward hidden GEMMs fp16 x fp16 -> fp32, backward GEMMs bf16 x bf16 -> fp32, "
+                             "phases stored as 16-bit revolutions, weights / loss / Adam fp32"
+                             if args.precision == "bf16" else "fp32 throughout"),
         "data": "synthetic (smooth random 512^2 image per rank: 32 sinusoids; coords = get_mgrid(512))",
         "config": {"workload": f"train_img.py fit step: {args.side}x{args.side} coordinate grid per GPU, "
                                f"SingleBVPNet 2-{'-'.join([str(args.hidden)] * (args.num_hidden_layers + 1))}-1 "

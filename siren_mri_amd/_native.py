@@ -20,7 +20,8 @@ PRECISIONS = {"fp32": PREC_F32, "f32": PREC_F32, "float32": PREC_F32,
               "bf16": PREC_BF16, "bfloat16": PREC_BF16}
 
 LIB_NAME = "libsiren_mri_amd.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# SIREN_MRI_AMD_LIB: load another build of the same ABI (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("SIREN_MRI_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 # Every symbol include/siren_mri_amd.h declares (checked by tests/test_native_abi.py).
 EXPORTED_SYMBOLS = (

@@ -305,6 +305,7 @@ struct FragPrepArgs {
   bf16* Wt[FUSED_MAXH];        // optional: the backward's transposed bf16 copy [nb_w][F (in), F (out)]
   bf16* out;
   int64_t nb;
+  int f16;  // fragments in fp16 (the pipe kernel's operands) instead of bf16
   int F, nh;
 };
 
@@ -328,7 +329,14 @@ __global__ __launch_bounds__(256) void prep_frag_kernel(FragPrepArgs a) {
     bf16x8 v;
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = (bf16)src[j];
-    *(bf16x8*)(a.out + idx * 8) = v;
+    if (a.f16) {
+      h16x8 hv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) hv[j] = (_Float16)src[j];
+      *(h16x8*)(a.out + idx * 8) = hv;
+    } else {
+      *(bf16x8*)(a.out + idx * 8) = v;
+    }
     if (a.Wt[l]) {  // W^T[i][o] for the 8 inputs i of this slice, o = 32 fb + (lane & 31)
       bf16* dst = a.Wt[l] + b * per_layer + (int64_t)(16 * ks + 8 * (lane >> 5)) * F + 32 * fb + (lane & 31);
 #pragma unroll
@@ -419,11 +427,11 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
   // Buffer loads: the per-lane offset is one VGPR, the layer / block / K-step offset a scalar.
   const __amdgpu_buffer_rsrc_t wrs =
       fused_rsrc(a.Wfrag + wb * (int64_t)nh * F * F, (int64_t)nh * F * F * 2);
-  auto wfrag = [&](int l, int fb, int ks) -> bf16x8 {
+  auto wfrag = [&](int l, int fb, int ks) -> h16x8 {
     const int soff = __builtin_amdgcn_readfirstlane((((l * 8 + FB * wave + fb) * NKS + ks) * 64) * 16);
-    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, soff, 0));
+    return __builtin_bit_cast(h16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, soff, 0));
   };
-  bf16x8 wreg[FB][NKS];
+  h16x8 wreg[FB][NKS];
 #pragma unroll
   for (int fb = 0; fb < FB; ++fb)
 #pragma unroll
@@ -489,10 +497,10 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
       ph[e + 4] = PT::enc_scaled(z[e + 4], bb[e], kph);
     }
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, ph), rs, (r * F + 8 * cc) * 2, 0, 0);
-    bf16x8 hv;
+    h16x8 hv;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) hv[e] = (bf16)PT::sinp(ph[e]);
-    *(bf16x8*)(Hs[h] + h_off(r, cc)) = hv;
+    for (int e = 0; e < 8; ++e) hv[e] = (_Float16)PT::sinp(ph[e]);
+    *(h16x8*)(Hs[h] + h_off(r, cc)) = hv;
   };
 
   // EC of half h, hidden layer lh, in 16 slices: slices 0..7 write two accumulator groups each
@@ -529,10 +537,10 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
     const u16x8 ph = *(const u16x8*)hp;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, ph), rs, (r * F + 8 * cc) * 2, 0, 0);
     if constexpr (!last) {
-      bf16x8 hv;
+      h16x8 hv;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) hv[e] = (bf16)PT::sinp(ph[e]);
-      *(bf16x8*)hp = hv;
+      for (int e = 0; e < 8; ++e) hv[e] = (_Float16)PT::sinp(ph[e]);
+      *(h16x8*)hp = hv;
     } else {
       float hv[8];
 #pragma unroll
@@ -568,14 +576,14 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
         for (int e = 0; e < 16; ++e) acc[fb][bm][e] = 0.f;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
-      bf16x8 hf[2];
+      h16x8 hf[2];
 #pragma unroll
-      for (int bm = 0; bm < 2; ++bm) hf[bm] = *(const bf16x8*)(Hs[h] + h_off(32 * bm + j32, 2 * ks + hh));
+      for (int bm = 0; bm < 2; ++bm) hf[bm] = *(const h16x8*)(Hs[h] + h_off(32 * bm + j32, 2 * ks + hh));
 #pragma unroll
       for (int fb = 0; fb < FB; ++fb)
 #pragma unroll
         for (int bm = 0; bm < 2; ++bm)
-          acc[fb][bm] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wreg[fb][ks], hf[bm], acc[fb][bm], 0, 0, 0);
+          acc[fb][bm] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wreg[fb][ks], hf[bm], acc[fb][bm], 0, 0, 0);
       if constexpr (decltype(refill)::value) {
 #pragma unroll
         for (int fb = 0; fb < FB; ++fb) wreg[fb][ks] = wfrag(lref, fb, ks);

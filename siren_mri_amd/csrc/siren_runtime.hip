@@ -486,6 +486,7 @@ int fused_forward(const siren_mlp_desc* d, const Geo& g, const Layout& lo, const
     fp.nb = g.nb;
     fp.F = F;
     fp.nh = nh;
+    fp.f16 = g_fwd_pipe ? 1 : 0;  // the pipe kernel multiplies in fp16 (sin values need no bf16 range)
     hipLaunchKernelGGL(prep_frag_kernel, dim3(grid1d(g.nb * nh * (int64_t)F * F / 8, 1024)), dim3(256), 0,
                        st, fp);
     int rc = check_launch("prep_frag");

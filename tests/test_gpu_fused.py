@@ -1,8 +1,11 @@
-"""GPU: the single-kernel bf16 forward (siren_fused.hip) against the per-layer kernels and the
-fp64 oracle. The fused and per-layer paths share their arithmetic (same phase encoding, same
-bf16 operands, same output-layer reduction order); they may differ only through the MFMA's
-internal summation order, so y agrees to ~1e-3 norm-relative and parity vs the oracle keeps the
-bf16 tolerances of test_gpu_siren_stack.py (3e-2 forward, 5e-2 gradients)."""
+"""GPU: the single-kernel forward (siren_fused.hip) against the per-layer kernels and the fp64
+oracle. The fused and per-layer paths share the phase encoding and the output-layer reduction
+order; the width-256 pipe kernel multiplies hidden layers with fp16 operands (sin values in
+[-1, 1] and the weights need no bf16 range), so its y is ~8x closer to the oracle than the
+per-layer bf16 forward (measured 4.8e-4 vs 3.8e-3 norm-relative on the metric architecture,
+tools/fwd_acc_probe.py); the other fused shapes keep bf16 operands and match the per-layer path.
+Parity vs the oracle keeps the bf16 tolerances of test_gpu_siren_stack.py (3e-2 forward, 5e-2
+gradients)."""
 import pytest
 import torch
 
@@ -59,10 +62,14 @@ def test_fused_matches_per_layer_and_oracle(dims, B, n):
     x = torch.rand(B or 1, n, dims[0], generator=g) * 2 - 1
     y_f, g_f = _forward(x, params, fused=True, grad=True)
     y_u, g_u = _forward(x, params, fused=False, grad=True)
-    assert orc.norm_rel(y_f, y_u) < 2e-3
     with torch.no_grad():
         y_ref = orc.siren_forward(x.double(), [(W.double(), b.double()) for W, b in params])
-    assert orc.norm_rel(y_f, y_ref) < 3e-2
+    # the width-256 pipe kernel multiplies in fp16 (8x finer than the per-layer bf16 path), the
+    # other fused shapes in bf16: never further from the fp64 oracle than the per-layer forward
+    e_f, e_u = orc.norm_rel(y_f, y_ref), orc.norm_rel(y_u, y_ref)
+    assert e_f <= 1.01 * e_u + 1e-6, (e_f, e_u)
+    assert orc.norm_rel(y_f, y_u) < 5e-3
+    assert e_f < 3e-2
     for (dWf, dbf), (dWu, dbu) in zip(g_f, g_u):
         assert orc.norm_rel(dWf, dWu) < 2e-2
         assert orc.norm_rel(dbf, dbu) < 2e-2
