@@ -379,6 +379,11 @@ template <int C>
 __global__ __launch_bounds__(64 * SIREN_PIPE_NW)
 void fused_fwd_pipe_kernel(FusedFwdArgs a) {
   using PT = Prec<kPrecBF16>;
+#ifdef SIREN_FWD_DEBUG
+  const int dbg = a.dbg;  // timing experiments only: a runtime flag puts branches in the K loop
+#else
+  constexpr int dbg = 0;
+#endif
   constexpr int F = 256, BM = 128, HB = 64, NKS = F / 16, SMASK = 15;
   constexpr int NW = SIREN_PIPE_NW, NT = 64 * NW, FB = 8 / NW;  // waves, threads, 32-feature blocks per wave
   // H rows padded to 528 bytes (no swizzle): every LDS address below is one per-lane base plus a
@@ -472,8 +477,10 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
         fused_rsrc(a.P[0] ? (const uint16_t*)a.P[0] + (batch * rows + r0) * F : nullptr,
                    a.P[0] ? (int64_t)nval * F * 2 : 0);
     const float* xs = Xs[xb] + HB * h * C;
-    const int i = lane + 64 * k;
-    const int r = i / CPW, cc = CPW * wave + (i % CPW);
+    int tl = tid;
+    asm volatile("" : "+v"(tl));  // per-lane offsets recomputed per task, not held (VGPR pressure)
+    const int i = (tl & 63) + 64 * k;
+    const int r = i / CPW, cc = CPW * (tl >> 6) + (i % CPW);
     const f32x4 ba = *(const f32x4*)(Sw0 + C * F + 8 * cc);
     const f32x4 bb = *(const f32x4*)(Sw0 + C * F + 8 * cc + 4);
     float z[8];
@@ -514,7 +521,9 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
       for (int u = 0; u < 2; ++u) {
         const int gi = 2 * sl + u;
         const int fb = gi >> 3, g = (gi >> 1) & 3, bm = gi & 1;
-        const int f = 32 * FB * wave + 32 * fb + 8 * g + 4 * hh;
+        int tl = tid;
+        asm volatile("" : "+v"(tl));
+        const int f = 32 * FB * (tl >> 6) + 32 * fb + 8 * g + 4 * ((tl >> 5) & 1);
         const f32x4 bv = *(const f32x4*)(Sb + lh * F + f);
         u16x4 ph;
 #pragma unroll
@@ -531,8 +540,10 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
     void* Pl = a.P[lh + 1];
     const __amdgpu_buffer_rsrc_t rs =
         fused_rsrc(Pl ? (const uint16_t*)Pl + (batch * rows + r0) * F : nullptr, Pl ? (int64_t)nval * F * 2 : 0);
-    const int i = lane + 64 * k;
-    const int r = i / CPW, cc = CPW * wave + (i % CPW);
+    int tl = tid;
+    asm volatile("" : "+v"(tl));  // per-lane offsets recomputed per task, not held (VGPR pressure)
+    const int i = (tl & 63) + 64 * k;
+    const int r = i / CPW, cc = CPW * (tl >> 6) + (i % CPW);
     char* hp = Hs[h] + h_off(r, cc);
     const u16x8 ph = *(const u16x8*)hp;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, ph), rs, (r * F + 8 * cc) * 2, 0, 0);
@@ -578,17 +589,19 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
     for (int ks = 0; ks < NKS; ++ks) {
       h16x8 hf[2];
 #pragma unroll
-      for (int bm = 0; bm < 2; ++bm) hf[bm] = *(const h16x8*)(Hs[h] + h_off(32 * bm + j32, 2 * ks + hh));
+      for (int bm = 0; bm < 2; ++bm)
+        hf[bm] = *(const h16x8*)(Hs[h] + h_off(32 * bm + j32, 2 * ((dbg & 8) ? 0 : ks) + hh));
 #pragma unroll
       for (int fb = 0; fb < FB; ++fb)
 #pragma unroll
         for (int bm = 0; bm < 2; ++bm)
           acc[fb][bm] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wreg[fb][ks], hf[bm], acc[fb][bm], 0, 0, 0);
       if constexpr (decltype(refill)::value) {
+        if (!(dbg & 4))
 #pragma unroll
         for (int fb = 0; fb < FB; ++fb) wreg[fb][ks] = wfrag(lref, fb, ks);
       }
-      if (!(a.dbg & 1)) filler(ks);
+      if (!(dbg & 1)) filler(ks);
     }
   };
   auto EC = [&](int64_t t, int h, const f32x16 (&acc)[FB][2], int lh, auto last_tag) {
@@ -633,7 +646,7 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
     const bool more = t + G < ntiles;
     // seg 0: L0(A) + EC(nh, B) of the previous tile (+ its y rows of half A); x(t + G) issued first
     if (more) x_issue(t + G);
-    if (!(a.dbg & 2)) {
+    if (!(dbg & 2)) {
       L0(t, 0, xb);
       if (have_prev) {
         EC(tp, 1, accB, nh - 1, T_{});

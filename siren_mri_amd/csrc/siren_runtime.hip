@@ -1576,7 +1576,7 @@ int siren_config_set(const char* key, int64_t value) {
     g_ring_prof_n = 0;
     return SIREN_OK;
   }
-  if (key && strcmp(key, "debug_fwd_skip") == 0 && value >= 0 && value <= 3) {
+  if (key && strcmp(key, "debug_fwd_skip") == 0 && value >= 0 && value <= 15) {
     g_fwd_dbg = (int)value;
     return SIREN_OK;
   }

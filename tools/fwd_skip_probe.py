@@ -8,7 +8,7 @@ params = orc.siren_init(orc.siren_dims(2, 256, 3, 1), seed=0)
 ws = [W.to(dev).requires_grad_(True) for W, _ in params]
 bs = [b.to(dev).requires_grad_(True) for _, b in params]
 x = orc.get_mgrid(512).unsqueeze(0).to(dev)
-for dbg in (0, 1, 2, 3, 0):
+for dbg in [int(v) for v in (sys.argv[1:] or (0, 1, 2, 3, 0))]:
     _native.set_option("debug_fwd_skip", dbg)
     for _ in range(3): siren_mlp(x, ws, bs, precision="bf16")
     torch.cuda.synchronize()
