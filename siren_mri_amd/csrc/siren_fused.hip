@@ -585,12 +585,18 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
       for (int bm = 0; bm < 2; ++bm)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[fb][bm][e] = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      h16x8 hf[2];
+    // H fragments one K step ahead: the reads of step ks + 1 are in flight under step ks's MFMAs
+    auto hread = [&](h16x8 (&hf)[2], int ks) {
 #pragma unroll
       for (int bm = 0; bm < 2; ++bm)
         hf[bm] = *(const h16x8*)(Hs[h] + h_off(32 * bm + j32, 2 * ((dbg & 8) ? 0 : ks) + hh));
+    };
+    h16x8 hbuf[2][2];
+    hread(hbuf[0], 0);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      if (ks + 1 < NKS) hread(hbuf[(ks + 1) & 1], ks + 1);
+      h16x8 (&hf)[2] = hbuf[ks & 1];
 #pragma unroll
       for (int fb = 0; fb < FB; ++fb)
 #pragma unroll

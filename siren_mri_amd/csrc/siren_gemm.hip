@@ -844,6 +844,7 @@ constexpr int RING_BM = 32;
 constexpr int RING_NPROF = 6;
 
 // debug segment timer of the ring kernels (s_memtime; perturbs timing by ~10 %)
+#ifdef SIREN_RING_PROF
 struct RingProf {
   long long* out;
   long long acc[RING_NPROF];
@@ -864,6 +865,14 @@ struct RingProf {
       for (int i = 0; i < RING_NPROF; ++i) out[(slot * 8 + (threadIdx.x >> 6)) * RING_NPROF + i] = acc[i];
   }
 };
+#else
+// product builds: no counters (a runtime null check would split every tile's schedule at the ticks)
+struct RingProf {
+  DEV RingProf(long long*) {}
+  DEV void tick(int) {}
+  DEV void flush(int64_t) {}
+};
+#endif
 
 template <int VMCNT>
 DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMCNT) : "memory"); }
