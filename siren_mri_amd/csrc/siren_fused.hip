@@ -375,7 +375,8 @@ DEV __amdgpu_buffer_rsrc_t fused_rsrc(const void* base, int64_t bytes) { return 
 #ifndef SIREN_PIPE_NW
 #define SIREN_PIPE_NW 8
 #endif
-template <int C>
+// OC: the output width when known at compile time (1: the image-fitting nets; 0: a.O at run time)
+template <int C, int OC>
 __global__ __launch_bounds__(64 * SIREN_PIPE_NW)
 void fused_fwd_pipe_kernel(FusedFwdArgs a) {
   using PT = Prec<kPrecBF16>;
@@ -406,7 +407,7 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
   const int j32 = lane & 31, hh = lane >> 5;
   const int64_t batch = blockIdx.y;
   const int64_t wb = a.batched ? batch : 0;
-  const int O = a.O, nh = a.nh;
+  const int O = OC > 0 ? OC : a.O, nh = a.nh;
   const float w0 = a.w0;
   const float kph = PT::enck(w0);
   const int64_t rows = a.rows_per_batch;

@@ -520,10 +520,12 @@ int fused_forward(const siren_mlp_desc* d, const Geo& g, const Layout& lo, const
   using KernelFn = void (*)(FusedFwdArgs);
   static const KernelFn table[FUSED_MAXC] = {fused_fwd_bf16_kernel<256, 1>, fused_fwd_bf16_kernel<256, 2>,
                                              fused_fwd_bf16_kernel<256, 3>, fused_fwd_bf16_kernel<256, 4>};
-  static const KernelFn pipe[FUSED_MAXC] = {fused_fwd_pipe_kernel<1>, fused_fwd_pipe_kernel<2>,
-                                            fused_fwd_pipe_kernel<3>, fused_fwd_pipe_kernel<4>};
+  static const KernelFn pipe[2][FUSED_MAXC] = {
+      {fused_fwd_pipe_kernel<1, 0>, fused_fwd_pipe_kernel<2, 0>, fused_fwd_pipe_kernel<3, 0>, fused_fwd_pipe_kernel<4, 0>},
+      {fused_fwd_pipe_kernel<1, 1>, fused_fwd_pipe_kernel<2, 1>, fused_fwd_pipe_kernel<3, 1>, fused_fwd_pipe_kernel<4, 1>}};
   const bool use_pipe = g_fwd_pipe && nh > 0;
-  hipLaunchKernelGGL((use_pipe ? pipe : table)[a.C - 1], grid, dim3(use_pipe ? 64 * SIREN_PIPE_NW : 512), 0, st, a);
+  hipLaunchKernelGGL((use_pipe ? pipe[a.O == 1 ? 1 : 0] : table)[a.C - 1], grid,
+                     dim3(use_pipe ? 64 * SIREN_PIPE_NW : 512), 0, st, a);
   tmark_end(SIREN_KCLASS_FWD_FUSED, st);
   return check_launch("fused_fwd");
 }
