@@ -355,9 +355,10 @@ namespace siren {
 // A and B with their own LDS operand buffers; every segment pairs the K loop of one half with the
 // epilogue/convert (EC) of the other, and segments are separated by one barrier:
 //
-//   L0(A) + EC(nh,B of previous tile) | K(1,A) + L0(B) | K(1,B) + EC(1,A) | K(2,A) + EC(1,B) | ...
-//   ... | K(nh,B) + EC(nh,A) | (next tile) L0(A') + EC(nh,B) | ...
+//   K(1,A) + EC(nh,B of previous tile) + L0(B) | K(1,B) + EC(1,A) | K(2,A) + EC(1,B) | ...
+//   ... | K(nh,B) + EC(nh,A) + L0(A of next tile) | (next tile) K(1,A') + EC(nh,B) + L0(B') ...
 //
+// (only the first tile's L0(A) runs without MFMA work beside it).
 // EC is wave-local: a wave converts only the 32 features it computed (phases to LDS, read back as
 // 16-byte chunks, stored to P_l, turned into bf16 sin in place), so K and EC of different halves
 // need no barrier between them and the compiler can interleave MFMA and VALU issue. Stores go
@@ -645,29 +646,36 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
   x_issue(t);
   x_park(xb);
   fused_barrier();
+  L0(t, 0, xb);  // prologue: layer 0 of half A of the first tile (later tiles: in the last segment)
+  fused_barrier();
 
+  // Every segment pairs a K loop with VALU filler. The first one also takes the output EC of the
+  // previous tile's half B and the last one layer 0 of the next tile's half A (EC and L0 of one
+  // half are wave-local, in program order, so they share the half's LDS buffer in one segment).
+  // The first tile's "previous tile" is a dummy past the end: its stores and y rows drop out, so
+  // no run-time condition splits the K loop's schedule.
+  constexpr int ECS = FB * 4 + NTASK;  // EC slices
+  static_assert(ECS + NTASK <= NKS, "EC + L0 tasks must fit one K loop");
   f32x16 accA[FB][2], accB[FB][2];
-  bool have_prev = false;
-  int64_t tp = -1;
+#pragma unroll
+  for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) accB[fb][bm][e] = 0.f;
+  int64_t tp = ntiles;
   for (; t < ntiles; t += G) {
     const bool more = t + G < ntiles;
-    // seg 0: L0(A) + EC(nh, B) of the previous tile (+ its y rows of half A); x(t + G) issued first
     if (more) x_issue(t + G);
-    if (!(dbg & 2)) {
-      L0(t, 0, xb);
-      if (have_prev) {
-        EC(tp, 1, accB, nh - 1, T_{});
-        Ypass(tp, 0);
-      }
-    }
-    fused_barrier();
-    // seg 1: K(1, A) + L0(B) (+ previous tile's y rows of half B); park x(t + G)
+    Ypass(tp, 0);  // y rows of the previous tile's half A (its EC ended the previous iteration)
+    // seg 1: K(1, A) + EC(nh, B) of the previous tile + L0(B); park x(t + G)
     K(0, accA, F_{}, 0, [&](int ks) {
-      if ((ks & 1) == 0 && (ks >> 1) < NTASK) L0_task(t, 1, xb, ks >> 1);
+      if (ks < ECS) EC_slice(tp, 1, accB, nh - 1, T_{}, ks);
+      else if (ks - ECS < NTASK) L0_task(t, 1, xb, ks - ECS);
     });
-    if (have_prev) Ypass(tp, 1);
     if (more) x_park(xb ^ 1);
     fused_barrier();
+    Ypass(tp, 1);
     for (int l = 0; l < nh; ++l) {
       const int lnext = (l + 1 < nh) ? l + 1 : 0;
       if (l + 1 < nh) {
@@ -678,12 +686,15 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
         K(0, accA, F_{}, 0, [&](int ks) { EC_slice(t, 1, accB, l, F_{}, ks); });
         fused_barrier();
       } else {
-        // last layer: K(nh, B) + EC(nh, A) with the output layer; slots refilled for the next tile
-        K(1, accB, T_{}, lnext, [&](int ks) { EC_slice(t, 0, accA, l, T_{}, ks); });
+        // last layer: K(nh, B) + EC(nh, A) with the output layer + L0(A) of the next tile (past
+        // the end on the last iteration: its stores drop out); slots refilled for the next tile
+        K(1, accB, T_{}, lnext, [&](int ks) {
+          if (ks < ECS) EC_slice(t, 0, accA, l, T_{}, ks);
+          else if (ks - ECS < NTASK) L0_task(t + G, 0, xb ^ 1, ks - ECS);
+        });
         fused_barrier();
       }
     }
-    have_prev = true;
     tp = t;
     xb ^= 1;
   }
