@@ -191,8 +191,17 @@ def lib():
     return _lib if _lib is not None else load_library()
 
 
+_OPTIONS_EPOCH = [0]
+
+
+def options_epoch() -> int:
+    """Bumped by every set_option (buffer sizes may depend on the options)."""
+    return _OPTIONS_EPOCH[0]
+
+
 def set_option(key: str, value: int) -> None:
     """siren_config_set: process-wide execution options (e.g. "fused_forward")."""
+    _OPTIONS_EPOCH[0] += 1
     if lib().siren_config_set(key.encode(), int(value)) != 0:
         raise NativeError(last_error())
 
@@ -223,7 +232,9 @@ def precision_code(precision) -> int:
 
 
 def stream_handle(device: torch.device) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
+    """The current HIP stream of `device` as an integer (torch's raw getter: no Stream object)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    return torch._C._cuda_getCurrentRawStream(idx)
 
 
 def make_desc(dims, weights, biases, *, w0: float, prec: int, outermost_linear: bool,

@@ -90,6 +90,24 @@ def _flat_params(weights, biases, geo: _Geometry):
     return ws, bs
 
 
+_SIZES = {}
+
+
+def _sizes(L, desc, geo: _Geometry, prec: int, outermost_linear: bool, need_saved: bool):
+    """(saved, workspace) bytes of a geometry after siren_mlp_check. They depend only on the
+    geometry and options (not on the pointers), so they are asked once per geometry."""
+    key = (tuple(geo.dims), geo.batch, geo.rows, geo.batched, prec, outermost_linear,
+           _native.options_epoch())
+    hit = _SIZES.get(key)
+    if hit is None:
+        _native.check(L.siren_mlp_check(ctypes.byref(desc)), "siren_mlp_check")
+        hit = (L.siren_mlp_saved_bytes(ctypes.byref(desc)), L.siren_mlp_workspace_bytes(ctypes.byref(desc)))
+        if len(_SIZES) > 256:
+            _SIZES.clear()
+        _SIZES[key] = hit
+    return (hit[0] if need_saved else 0), hit[1]
+
+
 class _SirenMLPFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cfg, x, *params):
@@ -105,10 +123,8 @@ class _SirenMLPFunction(torch.autograd.Function):
                                  outermost_linear=outermost_linear, weights_batched=geo.batched,
                                  batch=geo.batch, rows_per_batch=geo.rows)
         L = _native.lib()
-        _native.check(L.siren_mlp_check(ctypes.byref(desc)), "siren_mlp_check")
         need_saved = grad_on and any(ctx.needs_input_grad)
-        saved_bytes = L.siren_mlp_saved_bytes(ctypes.byref(desc)) if need_saved else 0
-        ws_bytes = L.siren_mlp_workspace_bytes(ctypes.byref(desc))
+        saved_bytes, ws_bytes = _sizes(L, desc, geo, prec, outermost_linear, need_saved)
         saved = torch.empty(max(saved_bytes, 1), dtype=torch.uint8, device=dev) if need_saved else None
         work = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
         y = torch.empty(geo.lead_shape + (geo.dims[-1],), dtype=torch.float32, device=dev)
@@ -118,6 +134,7 @@ class _SirenMLPFunction(torch.autograd.Function):
         _native.check(rc, "siren_mlp_forward")
         ctx.cfg = cfg
         ctx.geo = geo
+        ctx.desc = desc  # its pointers are the tensors saved below
         ctx.saved_buf = saved
         ctx.saved_bytes = saved_bytes
         ctx.save_for_backward(xc, *ws, *bs)
@@ -134,11 +151,9 @@ class _SirenMLPFunction(torch.autograd.Function):
         bs = list(tensors[1 + n_layers:])
         dev = xc.device
         dyc = dy.contiguous().to(torch.float32)
-        desc = _native.make_desc(geo.dims, ws, bs, w0=w0, prec=prec,
-                                 outermost_linear=outermost_linear, weights_batched=geo.batched,
-                                 batch=geo.batch, rows_per_batch=geo.rows)
+        desc = ctx.desc
         L = _native.lib()
-        ws_bytes = L.siren_mlp_workspace_bytes(ctypes.byref(desc))
+        ws_bytes = _sizes(L, desc, geo, prec, outermost_linear, False)[1]
         work = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
         dW = [torch.empty_like(w) for w in ws]
         db = [torch.empty_like(b) for b in bs]
@@ -154,6 +169,7 @@ class _SirenMLPFunction(torch.autograd.Function):
                                   _native.stream_handle(dev))
         _native.check(rc, "siren_mlp_backward")
         ctx.saved_buf = None
+        ctx.desc = None
         if geo.squeeze_w:
             dW = [g.unsqueeze(0) for g in dW]
             db = [g.unsqueeze(0) for g in db]

@@ -87,12 +87,15 @@ class Adam(torch.optim.Adam):
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             # tensors sharing a step count go together (normally: all of them)
+            steps = [self.state[p]["step"] for p in params]
+            if steps:
+                torch._foreach_add_(steps, 1)  # one dispatch for all the CPU step counters
             by_step = {}
-            for p in params:
-                st = self.state[p]
-                st["step"] += 1
-                by_step.setdefault(float(st["step"].item()), []).append(p)
-            stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+            for p, st in zip(params, steps):
+                by_step.setdefault(float(st.item()), []).append(p)
+            if not params:
+                continue
+            stream = ctypes.c_void_p(_native.stream_handle(params[0].device))
             dev_scalars = None
             if self._graph_mode:
                 if len(by_step) != 1:
