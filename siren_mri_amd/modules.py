@@ -160,8 +160,13 @@ class FCBlock(MetaModule):
     def layer_params(self, params=None):
         """(weights, biases) lists of the linear layers, from `params` or the module's own."""
         if params is None:
-            ws = [self.net[i][0].weight for i in range(self.num_linear)]
-            bs = [self.net[i][0].bias for i in range(self.num_linear)]
+            lin = self.__dict__.get("_linears")
+            if lin is None or len(lin) != len(self.net) or any(
+                    self.net[i][0] is not m for i, m in ((0, lin[0]), (len(lin) - 1, lin[-1]))):
+                lin = [self.net[i][0] for i in range(self.num_linear)]  # (Sequential indexing is slow)
+                self.__dict__["_linears"] = lin
+            ws = [m.weight for m in lin]
+            bs = [m.bias for m in lin]
         else:
             ws = [params[f"{i}.0.weight"] for i in range(self.num_linear)]
             bs = [params[f"{i}.0.bias"] for i in range(self.num_linear)]
