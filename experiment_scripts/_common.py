@@ -20,6 +20,8 @@ def base_parser(batch_size=1, lr=1e-4, num_epochs=10000, epochs_til_ckpt=25, ste
     p.add_argument("--precision", type=str, default="fp32", choices=["fp32", "bf16"],
                    help="arithmetic of the native SIREN stack (fp32 = reference numerics)")
     p.add_argument("--checkpoint_path", default=None)
+    p.add_argument("--overwrite", action="store_true",
+                   help="replace an existing logging_root/experiment_name without asking")
     return p
 
 

@@ -25,4 +25,4 @@ model.cuda()
 root_path = f"{opt.logging_root}/{opt.experiment_name}"
 training.train(model=model, train_dataloader=dataloader, epochs=opt.num_epochs, lr=opt.lr,
                steps_til_summary=opt.steps_til_summary, epochs_til_checkpoint=opt.epochs_til_ckpt,
-               model_dir=root_path, loss_fn=partial(loss_functions.image_mse, None), summary_fn=psnr_summary())
+               model_dir=root_path, overwrite=opt.overwrite, loss_fn=partial(loss_functions.image_mse, None), summary_fn=psnr_summary())

@@ -50,7 +50,7 @@ fourier_transformer.save_B("current_B.pt")
 
 training.train(model=model, train_dataloader=dataloader, val_dataloader=dataloader_val, epochs=opt.num_epochs,
                lr=opt.lr, steps_til_summary=opt.steps_til_summary, epochs_til_checkpoint=opt.epochs_til_ckpt,
-               model_dir=f"{opt.logging_root}/{opt.experiment_name}",
+               model_dir=f"{opt.logging_root}/{opt.experiment_name}", overwrite=opt.overwrite,
                loss_fn=partial(loss_functions.image_hypernetwork_loss, None, kl_weight, fw_weight),
                summary_fn=psnr_summary(), clip_grad=True, fourier_feat_transformer=fourier_transformer,
                device=device, accumulation_steps=4)

@@ -24,5 +24,5 @@ def summary_fn(model, model_input, gt, model_output, writer, total_steps):
 
 training.train(model=model, train_dataloader=dataloader, epochs=opt.num_epochs, lr=opt.lr,
                steps_til_summary=opt.steps_til_summary, epochs_til_checkpoint=opt.epochs_til_ckpt,
-               model_dir=f"{opt.logging_root}/{opt.experiment_name}", loss_fn=loss_functions.gradients_mse,
+               model_dir=f"{opt.logging_root}/{opt.experiment_name}", overwrite=opt.overwrite, loss_fn=loss_functions.gradients_mse,
                summary_fn=summary_fn, double_precision=False)

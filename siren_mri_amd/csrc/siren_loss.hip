@@ -24,8 +24,19 @@ struct SseFwdArgs {
 };
 
 // Per-thread sums over a fixed grid-stride order, a fixed-order block tree, and the last block
-// to finish (told by its agent-scope acq_rel ticket) adds the block sums in index order: the
-// result does not depend on scheduling.
+// to finish adds the block sums in index order: the result does not depend on scheduling.
+//
+// Hand-off of the block sums (MI355X_MICROARCH.md, "Valid forms", the first row of the table of
+// hand-offs measured with sc1 loads in place of the acquire). Every atomic below is RELAXED at
+// agent scope; the ordering comes from the hardware path, not from the C++ memory model:
+//   producer: one lane per block stores its sum write-through (relaxed agent-scope store =
+//             global_store sc1), drains it with an explicit s_waitcnt vmcnt(0) (inline asm, so the
+//             compiler cannot drop it), then takes a ticket with one agent-scope atomic add;
+//   consumer: the block whose add returned gridDim.x - 1 reads every sum with sc1 loads (relaxed
+//             agent-scope loads = global_load sc1, served from L2, never from a stale L1).
+// This avoids the L2 write-back / invalidate of acq_rel fences (several us per launch). The
+// partial/counter workspace is per (device, stream) on the host side, so two launches never share
+// it concurrently.
 __global__ __launch_bounds__(SSE_THREADS) void sse_fwd_kernel(SseFwdArgs a) {
   __shared__ float red[SSE_THREADS / 64];
   __shared__ unsigned ticket;

@@ -58,6 +58,10 @@ class _SirenJVP(torch.autograd.Function):
     @once_differentiable
     def backward(ctx, dout):
         fcblock, prec, order, n_layers, _ = ctx.cfg
+        if ctx.saved_buf is None:
+            raise RuntimeError(
+                "siren_mri_amd: the native tangent-stream backward runs once per forward; backward "
+                "through the same graph a second time (retain_graph=True) is not supported")
         geo = ctx.geo
         t = ctx.saved_tensors
         xc, ws, bs = t[0], list(t[1:1 + n_layers]), list(t[1 + n_layers:])

@@ -27,7 +27,9 @@ _MASKS: dict = {}
 def _high_freq_mask(device):
     m = _MASKS.get(device)
     if m is None:
-        m = 1 - create_circular_mask_torch(129, 129, center=None, radius=20)
+        # float32 (the reference's mask is int64; 1 - mask promotes the product with pred to float
+        # either way), so the native weighted-SSE kernel takes it
+        m = (1 - create_circular_mask_torch(129, 129, center=None, radius=20)).to(torch.float32)
         m = m.to(device)
         _MASKS[device] = m
     return m
@@ -37,10 +39,13 @@ _SSE_WS: dict = {}
 
 
 def _sse_workspace(device):
-    ws = _SSE_WS.get(device)
+    # one workspace per (device, stream): its block sums and ticket must not be shared by two
+    # launches that may run concurrently
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    ws = _SSE_WS.get(key)
     if ws is None:
         ws = torch.zeros(int(_native.lib().siren_sse_workspace_bytes()), dtype=torch.uint8, device=device)
-        _SSE_WS[device] = ws
+        _SSE_WS[key] = ws
     return ws
 
 

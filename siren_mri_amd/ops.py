@@ -144,6 +144,12 @@ class _SirenMLPFunction(torch.autograd.Function):
     @once_differentiable
     def backward(ctx, dy):
         w0, prec, outermost_linear, n_layers, _ = ctx.cfg
+        if ctx.saved_buf is None and ctx.saved_bytes:
+            # the saved activations are released at the end of the first backward (they are the
+            # largest allocation of a step); the reference's autograd graph could be re-entered
+            raise RuntimeError(
+                "siren_mri_amd: the native SIREN backward runs once per forward; backward through "
+                "the same graph a second time (retain_graph=True) is not supported")
         geo = ctx.geo
         tensors = ctx.saved_tensors
         xc = tensors[0]

@@ -13,7 +13,12 @@ Deliberate deviations:
     validation loader (bug 0.3, training.py:145);
   * the per-step loss is kept on the device and read back only at summary steps and at the end
     (the reference calls .item() every step, a host sync per step);
-  * an existing model_dir is overwritten without an interactive prompt when stdin is not a TTY.
+  * an existing model_dir is never deleted without consent: interactively the reference's prompt
+    asks (training.py:25-33); in a non-interactive run (nohup, a batch scheduler, a pipe) the
+    reference's input() raises EOFError and nothing is lost — here a FileExistsError says so,
+    unless overwrite=True (or hyperopt_run=True, as in the reference) was passed;
+  * with accumulation_steps > 1 and a data-parallel grad_reducer, each micro-step's exchange
+    carries only the gradient added since the previous exchange (see _reduce_micro_step).
 """
 from __future__ import annotations
 
@@ -51,12 +56,18 @@ def model_device(model):
     return torch.device("cpu")
 
 
-def prepare_model_dir(model_dir, hyperopt_run=False):
+def prepare_model_dir(model_dir, hyperopt_run=False, overwrite=False):
+    """training.py:25-37. Deletes an existing model_dir only on consent: hyperopt_run or overwrite,
+    or a 'y' at the interactive prompt. A non-interactive run raises instead of deleting."""
     if os.path.exists(model_dir):
-        if hyperopt_run or not sys.stdin.isatty():
+        if hyperopt_run or overwrite:
             val = "y"
-        else:
+        elif sys.stdin is not None and sys.stdin.isatty():
             val = input("The model directory %s exists. Overwrite? (y/n)" % model_dir)
+        else:
+            raise FileExistsError(
+                f"model directory {model_dir} exists and stdin is not interactive; pass "
+                "overwrite=True (scripts: --overwrite) to replace it, or choose another experiment name")
         if val == "y":
             shutil.rmtree(model_dir)
     os.makedirs(model_dir, exist_ok=True)
@@ -89,14 +100,14 @@ def make_adam(params, lr):
 def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_checkpoint, model_dir, loss_fn,
           summary_fn, val_dataloader=None, double_precision=False, clip_grad=False, use_lbfgs=False,
           loss_schedules=None, fourier_feat_transformer=None, device=None, hyperopt_run=False,
-          accumulation_steps=1, grad_reducer=None, write_outputs=True):
-    """Fit `model` (training.py:19-146). `grad_reducer`, if given, is called after each backward
-    (before clipping) — the data-parallel gradient exchange of training_ddp. With
-    write_outputs=False (non-zero data-parallel ranks) nothing is written to disk."""
+          accumulation_steps=1, grad_reducer=None, write_outputs=True, overwrite=False):
+    """Fit `model` (training.py:19-146). `grad_reducer`, if given, is the data-parallel gradient
+    exchange of training_ddp (see _reduce_micro_step for when it runs). With write_outputs=False
+    (non-zero data-parallel ranks) nothing is written to disk."""
     optim = make_adam(model.parameters(), lr)
     dev = model_device(model) if device is None else torch.device(device)
     if write_outputs:
-        summaries_dir, checkpoints_dir = prepare_model_dir(model_dir, hyperopt_run)
+        summaries_dir, checkpoints_dir = prepare_model_dir(model_dir, hyperopt_run, overwrite)
         writer = make_writer(summaries_dir)
     else:
         checkpoints_dir, writer = None, _NullWriter()
@@ -137,13 +148,17 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
             del model_output, losses
 
             train_loss = train_loss / accumulation_steps
+            last_micro = (step + 1) % accumulation_steps == 0 or (step + 1 == n_batches)
+            window_start = step % accumulation_steps == 0
+            if grad_reducer is not None and clip_grad and not window_start:
+                grad_reducer.snapshot()
             train_loss.backward()
             if grad_reducer is not None:
-                grad_reducer()
+                _reduce_micro_step(grad_reducer, clip_grad, last_micro, window_start)
             if clip_grad:
                 max_norm = 1.0 if isinstance(clip_grad, bool) else clip_grad
                 torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
-            if (step + 1) % accumulation_steps == 0 or (step + 1 == n_batches):
+            if last_micro:
                 optim.step()
                 optim.zero_grad()
 
@@ -163,6 +178,25 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
     if mean_val_loss is not None:
         return mean_val_loss
     return None if last_loss is None else float(last_loss.detach()) * accumulation_steps
+
+
+def _reduce_micro_step(grad_reducer, clip_grad, last_micro, window_start):
+    """When the data-parallel exchange runs inside an accumulation window (training.py:90-103).
+
+    The reference's DDP all-reduces (averages) the accumulated .grad after every backward
+    (training_ddp.py:96-109, no no_sync), and clips every micro-step. Exchanging the whole
+    accumulated gradient each micro-step is right only for an average and only because the earlier
+    part is already identical on every rank; with a sum it would add the earlier micro-steps W times
+    over. So:
+      * without clipping, only the micro-step followed by optim.step() exchanges (DDP no_sync
+        semantics: one collective per optimizer step, identical result for 'mean' and 'sum');
+      * with clipping (which needs the exchanged gradient every micro-step, as in the reference),
+        each exchange carries only what this backward added (the .grad minus the snapshot taken
+        before it), so 'sum' and 'mean' both give sum/average over ranks of every micro-step."""
+    if clip_grad:
+        grad_reducer(delta=not window_start)
+    elif last_micro:
+        grad_reducer()
 
 
 @torch.no_grad()

@@ -68,16 +68,30 @@ class GradAllReducer:
         if cur:
             self.buckets.append(cur)
         self._flat = [None] * len(self.buckets)
+        self._base = None  # snapshot of the accumulated gradient (micro-step deltas)
         if broadcast and self.world > 1:
             with torch.no_grad():
                 for p in self.params:
                     dist.broadcast(p.data, src=0, group=group)
 
-    def __call__(self):
+    @torch.no_grad()
+    def snapshot(self):
+        """Remember the current (already exchanged) gradient; the next call with delta=True
+        exchanges only what was added since."""
         if self.world == 1:
             return
+        self._base = [[None if p.grad is None else p.grad.detach().clone() for p in b] for b in self.buckets]
+
+    @torch.no_grad()
+    def __call__(self, delta: bool = False):
+        if self.world == 1:
+            return
+        base = self._base if delta else None
+        self._base = None
         for i, bucket in enumerate(self.buckets):
             grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in bucket]
+            if base is not None:
+                grads = [g if b is None else g - b for g, b in zip(grads, base[i])]
             numel = sum(g.numel() for g in grads)
             flat = self._flat[i]
             if flat is None or flat.numel() != numel or flat.device != grads[0].device:
@@ -93,11 +107,14 @@ class GradAllReducer:
             dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
             if self.op == "mean":
                 flat.mul_(1.0 / self.world)
-            for p, (o, n) in zip(bucket, views):
+            for j, (p, (o, n)) in enumerate(zip(bucket, views)):
+                red = flat[o:o + n].view_as(p)
+                if base is not None and base[i][j] is not None:
+                    red = red + base[i][j]
                 if p.grad is None:
-                    p.grad = flat[o:o + n].view_as(p).clone()
+                    p.grad = red.clone()
                 else:
-                    p.grad.copy_(flat[o:o + n].view_as(p))
+                    p.grad.copy_(red)
 
 
 def train_ddp(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_checkpoint, model_dir, loss_fn,
@@ -133,7 +150,9 @@ def train_ddp(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til
                          summary_fn if rank == 0 else (lambda *a, **k: None),
                          val_dataloader=val_dataloader if rank == 0 else None,
                          double_precision=double_precision, clip_grad=clip_grad, loss_schedules=loss_schedules,
-                         fourier_feat_transformer=fourier_feat_transformer, hyperopt_run=True,
+                         fourier_feat_transformer=fourier_feat_transformer,
+                         # rank 0 replaces model_dir unconditionally, as training_ddp.py:29-33 does
+                         hyperopt_run=True,
                          accumulation_steps=accumulation_steps, grad_reducer=reducer,
                          write_outputs=(rank == 0))
     return out

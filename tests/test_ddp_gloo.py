@@ -145,3 +145,90 @@ def test_shard_rows_partition():
     assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
     sizes = [b - a for a, b in spans]
     assert max(sizes) - min(sizes) <= 1
+
+
+def _rank_batches(rank, n=4, side=8):
+    coords = orc.get_mgrid(side)
+    g = torch.Generator().manual_seed(1000 + rank)
+    return [({"coords": coords[None]}, {"img": torch.randn(1, side * side, 1, generator=g)}) for _ in range(n)]
+
+
+def _accum_worker(rank, world, port, op, clip, root, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    from siren_mri_amd import training_ddp
+    training_ddp.ddp_setup(rank, world, backend="gloo")
+    model = orc.OracleSiren(hidden_features=16, num_hidden_layers=1, seed=3)
+    training_ddp.train_ddp(model, _rank_batches(rank), epochs=1, lr=1e-3, steps_til_summary=1000,
+                           epochs_til_checkpoint=1000, model_dir=root, loss_fn=sse,
+                           summary_fn=lambda *a, **k: None, device=rank, clip_grad=clip,
+                           accumulation_steps=2, grad_op=op)
+    out_q.put((rank, [p.detach().numpy().copy() for p in model.parameters()]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _accum_reference(world, op, clip, acc=2):
+    """Single-process statement of the intended semantics (training_ddp.py:96-109 with DDP
+    averaging, or a sum for coordinate-sharded fits): every micro-step's gradient is reduced over
+    ranks exactly once, added to the window's gradient, and clipped every micro-step."""
+    from siren_mri_amd.training import make_adam
+    model = orc.OracleSiren(hidden_features=16, num_hidden_layers=1, seed=3)
+    params = list(model.parameters())
+    optim = make_adam(params, 1e-3)
+    batches = [_rank_batches(r) for r in range(world)]
+    for step in range(len(batches[0])):
+        per_rank = []
+        for r in range(world):
+            inp, gt = batches[r][step]
+            loss = sse(model(inp), gt)["img_loss"].mean() / acc
+            per_rank.append(torch.autograd.grad(loss, params))
+        with torch.no_grad():
+            for i, p in enumerate(params):
+                red = sum(g[i] for g in per_rank)
+                if op == "mean":
+                    red = red / world
+                p.grad = red.clone() if p.grad is None else p.grad + red
+        if clip:
+            torch.nn.utils.clip_grad_norm_(params, max_norm=1.0)
+        if (step + 1) % acc == 0:
+            optim.step()
+            optim.zero_grad()
+    return [p.detach().numpy() for p in params]
+
+
+@pytest.mark.parametrize("op", ["sum", "mean"])
+@pytest.mark.parametrize("clip", [False, True])
+def test_grad_accumulation_reduces_each_micro_step_once(tmp_path, op, clip):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    root = str(tmp_path / "acc_run")
+    procs = [ctx.Process(target=_accum_worker, args=(r, world, port, op, clip, root, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _accum_reference(world, op, clip)
+    for a, b in zip(results[0], results[1]):
+        assert np.array_equal(a, b), "ranks diverged"
+    for a, r in zip(results[0], ref):
+        assert orc.norm_rel(torch.from_numpy(a), torch.from_numpy(r)) < 1e-5
+
+
+def test_model_dir_not_deleted_without_consent(tmp_path, monkeypatch):
+    import io
+    from siren_mri_amd.training import prepare_model_dir
+    d = tmp_path / "exp"
+    (d / "checkpoints").mkdir(parents=True)
+    (d / "checkpoints" / "model_final.pth").write_bytes(b"keep")
+    monkeypatch.setattr("sys.stdin", io.StringIO(""))  # not a TTY (nohup / batch / pipe)
+    with pytest.raises(FileExistsError):
+        prepare_model_dir(str(d))
+    assert (d / "checkpoints" / "model_final.pth").read_bytes() == b"keep"
+    prepare_model_dir(str(d), overwrite=True)
+    assert not (d / "checkpoints" / "model_final.pth").exists()
