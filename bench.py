@@ -279,6 +279,10 @@ def main():
             totals[kc] = t.total_ms
     dom = max(totals, key=totals.get)
     p0_recompute = args.precision == "bf16" and bool(_native.get_option("fused_forward"))
+    if bool(_native.get_option("fused_forward_reg")):  # class 4 is the register-resident forward
+        KCLASS_NAMES[4] = ("fused_fwd_reg_kernel (whole forward, activations in registers: layer 0 on the "
+                           "f32 MFMA, hidden and output layers on the f16 MFMA)")
+        KCLASS_SYMBOL["bf16"][4] = "siren::fused_fwd_reg_kernel<2, 1>"
 
     with _native.KernelTimer(dom, max_launches=max(64, 8 * args.steps)) as kt:
         elapsed = timed_region(step, args.steps, world)

@@ -209,8 +209,11 @@ int siren_sse_backward(const float* d, const float* mask, int64_t n, int64_t mas
  *                    layer's ring kernels (bf16, outermost_linear, O <= 2); 0: last_bwd kernel.
  *   "dx_ring"        1 (default): 256x256 bf16 input-gradient layers use the 4-stage
  *                    load pipeline kernel; 0: the double-buffered one.
- *   "fused_forward_pipe"  1 (default): the fused forward overlaps one half-tile's MFMA work with
- *                    the other's epilogue; 0: the sequential single-kernel forward.
+ *   "fused_forward_reg"  1 (default): the fused forward keeps every layer's activations in the
+ *                    registers of the wave that owns the rows (weights streamed through an LDS
+ *                    ring); 0: the LDS-staged fused forward below.
+ *   "fused_forward_pipe"  1 (default): the LDS-staged fused forward overlaps one half-tile's MFMA
+ *                    work with the other's epilogue; 0: the sequential single-kernel forward.
  *   "bwd_ring"       0 (default), 1: middle 256x256 bf16 layers compute both gradients in one
  *                    kernel (dZ and P read once); 0: separate input/weight-gradient kernels.
  *   "dw_ring"        1 (default): 256x256 bf16 weight-gradient layers use the ring kernel

@@ -1,0 +1,547 @@
+// siren_fwdreg.hip — the whole SIREN forward with the activations kept in registers
+// (bf16 mode, hidden width 256, gfx950).
+//
+//   layer 0   P_0 = w0 (x W_0^T + b_0)                    modules.py:25-26,38 (f32 MFMA, exact fp32)
+//   hidden l  P_l = w0 (sin(P_{l-1}) W_l^T + b_l)           modules.py:25-26,38 (f16 MFMA, fp32 acc)
+//   output    y   = sin(P_{L-2}) W_L^T + b_L  (sin(w0 .))   modules.py:78      (f16 MFMA, fp32 acc)
+//
+// Design: every wave owns 32 coordinate rows and computes ALL 256 features of every layer for
+// them, so a layer's output never leaves the wave. The MFMA runs transposed, P^T = W . H^T
+// (A = weight fragment, B = activation fragment), and the weights are prepared so that the
+// accumulator a lane holds IS the next layer's B fragment:
+//   * output-feature order (freg_phi): lane (j, h) of a 32x32 accumulator holds features
+//     32 fb + 8 h + 0..7 and 32 fb + 16 + 8 h + 0..7 of row j;
+//   * input-feature order (freg_in0): K step s, lane half h supplies features
+//     32 (s >> 1) + 16 (s & 1) + 8 h + 0..7 — exactly one converted half of one accumulator.
+// So the epilogue is register-to-register: no LDS exchange, no barrier between layers. The
+// weights (pre-multiplied by w0 / 2 pi, so an accumulator is a phase in revolutions; the bias is
+// the accumulator's initial value) are streamed block by block (32 output features x 256 inputs =
+// 16 KB of f16 fragments) through an 8-slot LDS ring that every wave of the workgroup reads; one
+// barrier per block keeps the ring in step, and each slot is refilled by LDS-DMA seven blocks
+// before it is read again.
+//
+// Epilogue per element: fr = fract(acc) (v_fract_f32), h = sin(fr) (v_sin_f32 takes revolutions),
+// f16 pack (v_cvt_pk_f16_f32), phase code for the backward = unorm16(fr) (v_cvt_pknorm_u16_f32,
+// two per instruction). The code is round(fr * 65535); the backward decodes it as code / 65536
+// revolutions (siren_common.h Prec<kPrecBF16>::rev128), a difference of at most one code step
+// (9.6e-5 rad), well inside the bf16 backward's own rounding.
+//
+// The epilogue of block fb runs beside the MFMAs of block fb + 1 (the last block's beside the
+// next layer's first: its two fragments are the last two K steps there), so VALU and MFMA issue
+// overlap inside every wave, and two waves per SIMD fill each other's gaps.
+#include <type_traits>
+
+#include "siren_common.h"
+
+namespace siren {
+
+constexpr int FREG_WROWS = 32;      // rows per wave tile
+constexpr int FREG_WG_ROWS = 256;   // rows per workgroup round (8 waves)
+constexpr int FREG_SLOT = 16384;    // bytes of one block: 16 K steps x 64 lanes x 16 B
+constexpr int FREG_WL_BYTES = 4096; // output-layer fragments, rows 0..7 only: [16 ks][2 h][8 rows][16 B]
+// Blocks per ring synchronisation (one barrier every FREG_SYNC blocks, 1 or 2).
+#ifndef SIREN_FREG_SYNC
+#define SIREN_FREG_SYNC 2
+#endif
+constexpr int FREG_SYNC = SIREN_FREG_SYNC;
+static_assert(FREG_SYNC == 1 || FREG_SYNC == 2, "ring sync interval");
+// Vector-memory operations a wave has issued after the ring refill it must see land (every block
+// issues two phase stores — a null tensor's are still issued and dropped by their resource — and
+// every refill of a slot two DMAs):
+//   FREG_SYNC 1: the slot read by block k + 1 was refilled at the barrier of block k - 6: at least
+//                1 + 2 x 5 (refills) + 2 x 6 (stores) = 23 are younger;
+//   FREG_SYNC 2: the slot read by block k + 2 was refilled (first of two slots) at the barrier of
+//                block k - 4: at least 1 + 2 + 4 (refills) + 2 x 4 (stores) = 15 are younger.
+#if SIREN_FREG_SYNC == 1
+#define SIREN_FREG_VMWAIT "s_waitcnt vmcnt(22)"
+#else
+#define SIREN_FREG_VMWAIT "s_waitcnt vmcnt(15)"
+#endif
+
+struct FwdRegArgs {
+  const float* x;             // [rows, C] per weight set
+  const float* W0;            // [nb_w][F, C]
+  const float* b0;            // [nb_w][F]
+  const _Float16* Wreg;       // [nb_w][nh][8 fb][16 ks][64 lanes][8] prepared hidden fragments
+  const _Float16* WLreg;      // [nb_w][16 ks][2 h][8 rows][8] prepared output fragments
+  const float* bias[FUSED_MAXH];
+  const float* bL;            // [nb_w][O]
+  void* P0;                   // phase codes of sine layer 0 (null: not kept)
+  char* Pb;                   // phase codes of sine layer 1 (null: none kept); layer l at Pb + (l - 1) pstride
+  int64_t pstride;
+  float* y;                   // [rows, O]
+  int64_t rows_per_batch;
+  int batched;
+  int O, nh, sine_out;
+  float w0;
+};
+
+DEV void freg_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Feature offset (within a 32-feature block) of MFMA output row i = 8 g + 4 h + e, which lane half
+// h holds as accumulator element v = 4 g + e: features 8 h + v for v < 8 and 16 + 8 h + (v - 8)
+// for v >= 8, so the two lane halves of a row hold adjacent 16-byte phase chunks (one 32-byte
+// piece of the row per store instruction) and K step 2 fb + q of the next layer takes features
+// 32 fb + 16 q + 0..15 (lane half h: 32 fb + 16 q + 8 h + 0..7).
+DEV constexpr int freg_phi(int i) {
+  const int h = (i >> 2) & 1, v = 4 * (i >> 3) + (i & 3);
+  return v + 8 * h + (v >= 8 ? 8 : 0);
+}
+DEV constexpr int freg_in0(int ks, int h) { return 32 * (ks >> 1) + 16 * (ks & 1) + 8 * h; }
+
+// The 8 two-element parts of a pending epilogue are spread over K steps 0..13 (part p at step
+// 13 p / 7): one part per one or two MFMAs, and both converted halves are ready before K steps
+// 14 and 15, which read them when the pending block is the previous layer's last.
+DEV constexpr int freg_part_at(int ks) {
+  for (int p = 0; p < 8; ++p)
+    if (13 * p / 7 == ks) return p;
+  return -1;
+}
+
+template <int B, int E, typename Fn>
+DEV void freg_for(Fn&& fn) {
+  if constexpr (B < E) {
+    fn(std::integral_constant<int, B>{});
+    freg_for<B + 1, E>(fn);
+  }
+}
+
+// Fragment reads from the ring as inline asm: the compiler's wait-count pass cannot tell them
+// apart from the LDS-DMA refills in flight and would drain the DMA (vmcnt(0)) before them. The
+// caller owns the wait: freg_lgkm<N>(v) (N = fragment reads issued after v's) ties v to it.
+template <int OFF>
+DEV void freg_read(h16x8& d, uint32_t va) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(va), "n"(OFF));
+}
+template <int N>
+DEV void freg_lgkm(h16x8& v) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "n"(N));
+}
+
+template <int C, int OC>
+__global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
+  constexpr int F = 256, NKS = 16, NB = 8;
+  constexpr int NKK = (C + 1) / 2;  // K pairs of the f32 layer-0 MFMA
+  static_assert(C >= 1 && C <= 4, "1..4 inputs");
+  // the ring's 8 slots as separate objects: the compiler's wait-count pass then knows that a read
+  // of slot fb cannot alias the LDS-DMA just issued into slot fb - 1 (one array would put an
+  // s_waitcnt vmcnt(0) in front of every fragment read after a refill)
+  __shared__ __attribute__((aligned(16))) char ring0[FREG_SLOT], ring1[FREG_SLOT], ring2[FREG_SLOT], ring3[FREG_SLOT],
+      ring4[FREG_SLOT], ring5[FREG_SLOT], ring6[FREG_SLOT], ring7[FREG_SLOT];
+  auto slot = [&](int fb) -> char* {
+    switch (fb) {
+      case 0: return ring0;
+      case 1: return ring1;
+      case 2: return ring2;
+      case 3: return ring3;
+      case 4: return ring4;
+      case 5: return ring5;
+      case 6: return ring6;
+      default: return ring7;
+    }
+  };
+  __shared__ __attribute__((aligned(16))) char wlf[FREG_WL_BYTES + 16];   // + a zero fragment
+  __shared__ __attribute__((aligned(16))) float sbias[(FUSED_MAXH + 1) * F];  // layer 0, hidden 0..nh-1
+  __shared__ __attribute__((aligned(16))) float xs[2][FREG_WG_ROWS * 4];
+  __shared__ __attribute__((aligned(16))) float sbl[8];
+
+#ifdef SIREN_FREG_DBG
+  // timing builds only (compile-time, so the schedule of the rest is unchanged): 1: no hidden-
+  // layer epilogue, 2: no barriers / ring refills, 4: no phase stores, 8: no layer-0 epilogue,
+  // 16: no hidden-layer MFMAs
+  constexpr int dbg = SIREN_FREG_DBG;
+#else
+  constexpr int dbg = 0;
+#endif
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar) index
+  const int j = lane & 31, hh = lane >> 5;
+  const int64_t batch = blockIdx.y;
+  const int64_t wb = a.batched ? batch : 0;
+  const int nh = a.nh;
+  const int O = OC > 0 ? OC : a.O;
+  const float w0 = a.w0;
+  const float k1 = w0 * kInv2Pi;
+  const int64_t rows = a.rows_per_batch;
+  const int64_t ntiles = (rows + FREG_WG_ROWS - 1) / FREG_WG_ROWS;
+  const int64_t G = gridDim.x;
+  const int64_t t0 = blockIdx.x;
+  if (t0 >= ntiles) return;
+
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  const _Float16* wsrc = a.Wreg + wb * (int64_t)nh * F * F;
+
+  // ---- stage the small per-weight-set operands ----
+  for (int i = tid; i < F; i += 512) sbias[i] = a.b0[wb * F + i] * k1;
+  for (int l = 0; l < nh; ++l)
+    for (int i = tid; i < F; i += 512) sbias[(l + 1) * F + i] = a.bias[l][wb * F + i] * k1;
+  if (tid < 8) sbl[tid] = tid < O ? a.bL[wb * O + tid] : 0.f;
+  if (tid < FREG_WL_BYTES / 16)
+    *(u32x4_t*)(wlf + 16 * tid) = *(const u32x4_t*)((const char*)(a.WLreg + wb * (FREG_WL_BYTES / 2)) + 16 * tid);
+  if (tid == FREG_WL_BYTES / 16) *(u32x4_t*)(wlf + FREG_WL_BYTES) = u32x4_t{0u, 0u, 0u, 0u};
+
+  // layer-0 weights as f32 MFMA A operands (lane (i, k): W_0[32 fb + phi(i)][2 kk + k] w0/2pi)
+  const int phij = freg_phi(j);
+  float w0r[NB][NKK];
+#pragma unroll
+  for (int fb = 0; fb < NB; ++fb)
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      const int col = 2 * kk + hh;
+      w0r[fb][kk] = col < C ? a.W0[(wb * F + 32 * fb + phij) * C + col] * k1 : 0.f;
+    }
+
+  // ---- LDS-DMA: ring blocks and x tiles ----
+  // block (layer, fb) of hidden layer `layer` into ring slot fb (the slot of every layer's block fb)
+  auto dma_block = [&](int layer, int fb) {
+    const char* src = (const char*)(wsrc + ((int64_t)layer * NB + fb) * (FREG_SLOT / 2)) + wave * 2048 + lane * 16;
+    char* dst = slot(fb) + wave * 2048;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(src + 1024), (lds_void*)(dst + 1024), 16, 0, 0);
+  };
+  // x rows of workgroup tile t (C KB; rows past the end arrive as zeros): waves 0..C-1, 1 KB each
+  auto dma_x = [&](int64_t t, int xb) {
+    if (wave < C) {
+      const int64_t r0 = t * FREG_WG_ROWS;
+      const int64_t nv = rows - r0 < 0 ? 0 : (rows - r0 < FREG_WG_ROWS ? rows - r0 : FREG_WG_ROWS);
+      const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x + (batch * rows + r0) * C, nv * C * 4);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_void*)((char*)xs[xb] + wave * 1024), 16,
+                                               wave * 1024 + lane * 16, 0, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int fb = 0; fb < NB; ++fb) dma_block(0, fb);
+  dma_x(t0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  freg_barrier();
+
+  // ---- helpers ----
+  auto bias_acc = [&](int layer, int fb) -> f32x16 {  // layer 0 = first layer, 1 + l = hidden l
+    const float* bp = sbias + layer * F + 32 * fb + 8 * hh;
+    f32x16 r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 v = *(const f32x4*)(bp + 4 * (q & 1) + 16 * (q >> 1));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[4 * q + e] = v[e];
+    }
+    return r;
+  };
+  const int frag_lane = lane * 16;
+  auto slot_va = [&](int fb) -> uint32_t { return lds_addr(slot(fb)) + frag_lane; };
+  // output fragments: rows >= 8 read the zero fragment (offset by -ks * 256 so every K step's
+  // immediate offset lands on it)
+  const uint32_t wl_va = lds_addr(wlf) + (j < 8 ? hh * 128 + j * 16 : FREG_WL_BYTES);
+#ifndef SIREN_FREG_PFD
+#define SIREN_FREG_PFD 3
+#endif
+  constexpr int PFD = SIREN_FREG_PFD;  // fragment prefetch distance (K steps, <= 3: four buffers)
+
+  // phase-code stores: sine layer pl, block pfb, of the wave's 32 rows of tile t (buffer resource
+  // sized to the valid rows: stores past the end are dropped; null layer: everything dropped)
+  int64_t tcur = t0;
+  int64_t p_rowoff = 0;  // byte offset of the current tile's first row in a phase tensor
+  int p_bytes = 0;       // valid bytes of the current tile in a phase tensor
+  auto p_rsrc = [&](int pl) -> __amdgpu_buffer_rsrc_t {
+    const char* base = pl == 0 ? (const char*)a.P0 : (a.Pb ? a.Pb + (int64_t)(pl - 1) * a.pstride : nullptr);
+    const uint64_t addr = base ? (uint64_t)(base + p_rowoff) : 0;
+    // every operand is wave-uniform; say so, or the compiler wraps each store in a waterfall loop
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)addr);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane(base ? p_bytes : 0);
+    return make_rsrc((const void*)(((uint64_t)hi << 32) | lo), nb);
+  };
+  const int p_voff = (wave * FREG_WROWS + j) * (F * 2) + hh * 16;
+  auto p_store = [&](int pl, int pfb, int half, const u32x4_t& c) {
+    if constexpr ((dbg & 4) != 0) return;
+    if constexpr ((dbg & 32) != 0) {  // timing only: the same bytes as one contiguous 1 KB per store
+      __builtin_amdgcn_raw_buffer_store_b128(c, p_rsrc(pl), wave * 16384 + lane * 16, (pfb * 2 + half) * 1024, 0);
+      return;
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(c, p_rsrc(pl), p_voff, pfb * 64 + half * 32, 0);
+  };
+
+  // Epilogue of one accumulator, in 8 parts of 2 elements (part p: elements 2p, 2p + 1, packed
+  // at once into one f16 pair and one phase-code pair); after part 3 the first K fragment (and
+  // 16-byte phase chunk) is complete, after part 7 the second.
+  struct Epi {
+    uint32_t hp[4];
+    uint32_t cp[4];
+  };
+  auto epi_part = [&](Epi& ep, const f32x16& acc, int p, h16x8& t0h, h16x8& t1h, int pl, int pfb,
+                      auto codes_tag) {
+    constexpr bool codes = decltype(codes_tag)::value;  // false: the phases are not kept
+    typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+    h16x2 hv;
+    float f0, f1;
+    if constexpr ((dbg & 64) != 0) {  // timing only: convert without fract / sin
+      f0 = acc[2 * p];
+      f1 = acc[2 * p + 1];
+      hv[0] = (_Float16)f0;
+      hv[1] = (_Float16)f1;
+    } else {
+      f0 = __builtin_amdgcn_fractf(acc[2 * p]);
+      f1 = __builtin_amdgcn_fractf(acc[2 * p + 1]);
+      hv[0] = (_Float16)__builtin_amdgcn_sinf(f0);
+      hv[1] = (_Float16)__builtin_amdgcn_sinf(f1);
+    }
+    uint32_t hpk = __builtin_bit_cast(uint32_t, hv);
+    // computed here, not sunk to the next layer's MFMA that reads it: the unpacked fp32 values
+    // would otherwise stay live across the layer (twice the registers of the packed pair)
+    asm volatile("" : "+v"(hpk));
+    ep.hp[p & 3] = hpk;
+    if constexpr (codes) ep.cp[p & 3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pknorm_u16(f0, f1));
+    if ((p & 3) == 3) {
+      const u32x4_t hq = {ep.hp[0], ep.hp[1], ep.hp[2], ep.hp[3]};
+      const u32x4_t c = codes ? u32x4_t{ep.cp[0], ep.cp[1], ep.cp[2], ep.cp[3]} : u32x4_t{0u, 0u, 0u, 0u};
+      if (p == 3) t0h = __builtin_bit_cast(h16x8, hq);
+      else t1h = __builtin_bit_cast(h16x8, hq);
+      if constexpr (codes) p_store(pl, pfb, p == 3 ? 0 : 1, c);
+    }
+  };
+
+  auto out_init = [&]() -> f32x16 {  // output accumulator rows 0..7 = b_L (lanes' elements 0..3)
+    f32x16 r;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) r[e] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[e] = sbl[4 * hh + e];
+    return r;
+  };
+
+  h16x8 Ha[NKS], Hb[NKS];
+  h16x8 wq[4];    // rolling fragment prefetch (two steps ahead)
+  f32x16 accP;    // the block whose epilogue is pending
+  f32x16 accNx;   // the next block's initial accumulator (its bias), loaded into accP's registers
+                  // once that block's epilogue is done
+  int pend_pl = 0;
+  int64_t kblk = 0;  // blocks consumed so far (ring position)
+  const bool refill = nh > 1;
+
+  // Ring synchronisation before block (l, fb), every FREG_SYNC blocks. FREG_SYNC 1: the slot of
+  // the block after it has landed (this wave's part: vmcnt; every wave's: the barrier) and the
+  // slot of the block before it is free: refill it with (l + 1 mod nh, fb - 1), or (l, 7) at
+  // fb = 0. FREG_SYNC 2 (even fb): slots fb + 1 and fb + 2 have landed; slots fb - 2 and fb - 1
+  // are free: refill them with layer l + 1 mod nh (at fb = 0: slots 6 and 7 with layer l).
+  auto block_sync = [&](int l, int fb) {
+    if constexpr ((dbg & 2) != 0) return;
+    if (FREG_SYNC == 2 && (fb & 1)) {
+      ++kblk;
+      return;
+    }
+    asm volatile(SIREN_FREG_VMWAIT ::: "memory");
+    freg_barrier();
+    if (refill && kblk >= FREG_SYNC) {
+      const int ln = l + 1 == nh ? 0 : l + 1;
+      if (FREG_SYNC == 1) {
+        if (fb > 0) dma_block(ln, fb - 1);
+        else dma_block(l, NB - 1);
+      } else {
+        if (fb > 0) {
+          dma_block(ln, fb - 2);
+          dma_block(ln, fb - 1);
+        } else {
+          dma_block(l, NB - 2);
+          dma_block(l, NB - 1);
+        }
+      }
+    }
+    ++kblk;
+  };
+
+  // one hidden layer l: Hin -> Hout (runtime l; register arrays bound at the call site;
+  // last_tag: whether the output layer follows — its fragments are prefetched at the end)
+  auto hidden_layer = [&](int l, h16x8 (&Hin)[NKS], h16x8 (&Hout)[NKS], auto last_tag) {
+    constexpr bool last = decltype(last_tag)::value;
+    freg_for<0, NB>([&](auto fb_c) {
+      constexpr int fb = decltype(fb_c)::value;
+      block_sync(l, fb);
+      if (fb == 0 && l == 0) dma_x(tcur + G, (int)(((tcur - t0) / G + 1) & 1));  // next round's x
+      f32x16 accN = accNx;
+      const uint32_t va_cur = slot_va(fb);
+      const uint32_t va_nxt = (fb + 1 < NB) ? slot_va(fb + 1) : (last ? wl_va : slot_va(0));
+      Epi ep;
+      freg_for<0, NKS>([&](auto ks_c) {
+        constexpr int ks = decltype(ks_c)::value;
+        constexpr int k3 = ks + PFD;
+        if constexpr (k3 < NKS) freg_read<k3 * 1024>(wq[k3 & 3], va_cur);
+        else if constexpr (fb + 1 < NB || !last) freg_read<(k3 - NKS) * 1024>(wq[k3 & 3], va_nxt);
+        else freg_read<(k3 - NKS) * 256>(wq[k3 & 3], va_nxt);
+        freg_lgkm<PFD>(wq[ks & 3]);
+        if constexpr (!(dbg & 16)) accN = __builtin_amdgcn_mfma_f32_32x32x16_f16(wq[ks & 3], Hin[ks], accN, 0, 0, 0);
+        constexpr int part = freg_part_at(ks);
+        if constexpr (part >= 0 && !(dbg & 1)) {
+          if constexpr (fb == 0) epi_part(ep, accP, part, Hin[14], Hin[15], pend_pl, 7, T_{});
+          else epi_part(ep, accP, part, Hout[2 * fb - 2], Hout[2 * fb - 1], l + 1, fb - 1, T_{});
+        }
+        if constexpr (ks == NKS - 2) {  // the pending epilogue is done: the next block's bias
+          if constexpr (fb + 1 < NB) accNx = bias_acc(l + 1, fb + 1);
+          else if constexpr (!last) accNx = bias_acc(l + 2, 0);
+          else accNx = out_init();
+        }
+      });
+      accP = accN;
+      pend_pl = l + 1;
+    });
+  };
+
+  // output layer: y = H W_L^T + b_L (MFMA rows = outputs), beside the last hidden block's epilogue
+  auto output_layer = [&](h16x8 (&Hin)[NKS]) {
+    f32x16 accO = accNx;
+    Epi ep;
+    const uint32_t va_nxt = slot_va(0);  // the next round's first block
+    freg_for<0, NKS>([&](auto ks_c) {
+      constexpr int ks = decltype(ks_c)::value;
+      constexpr int k3 = ks + PFD;
+      if constexpr (k3 < NKS) freg_read<k3 * 256>(wq[k3 & 3], wl_va);
+      else freg_read<(k3 - NKS) * 1024>(wq[k3 & 3], va_nxt);
+      freg_lgkm<PFD>(wq[ks & 3]);
+      accO = __builtin_amdgcn_mfma_f32_32x32x16_f16(wq[ks & 3], Hin[ks], accO, 0, 0, 0);
+      constexpr int part = freg_part_at(ks);
+      if constexpr (part >= 0) epi_part(ep, accP, part, Hin[14], Hin[15], pend_pl, 7, T_{});
+    });
+    // y[row][o], o = 4 h + e (rows 0..7 of the output accumulator are lanes' elements 0..3)
+    const int64_t r0 = tcur * FREG_WG_ROWS;
+    const int64_t nv = rows - r0 < FREG_WG_ROWS ? rows - r0 : FREG_WG_ROWS;
+    const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.y + (batch * rows + r0) * O, nv * O * 4);
+    const int yrow = wave * FREG_WROWS + j;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int o = 4 * hh + e;
+      if (o < O) {
+        float z = accO[e];
+        if (a.sine_out) z = Prec<kPrecBF16>::sinr(w0 * z);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, z), ry, (yrow * O + o) * 4, 0, 0);
+      }
+    }
+  };
+
+  // first fragments of the stream (later rounds: prefetched by the output layer)
+  {
+    const uint32_t va0 = slot_va(0);
+    freg_read<0>(wq[0], va0);
+    freg_read<1024>(wq[1], va0);
+    freg_read<2048>(wq[2], va0);
+  }
+
+  for (int64_t t = t0; t < ntiles; t += G) {
+    tcur = t;
+    {
+      const int64_t r0 = t * FREG_WG_ROWS;
+      p_rowoff = (batch * rows + r0) * (F * 2);
+      p_bytes = (int)((rows - r0 < FREG_WG_ROWS ? rows - r0 : FREG_WG_ROWS) * F * 2);
+    }
+    const int xb = (int)(((t - t0) / G) & 1);
+    // ---- layer 0 (f32 MFMA, K = C): blocks 0..6 converted here, block 7 beside hidden block 0 ----
+    auto layer0 = [&](auto codes_tag) {
+      const float* xt = xs[xb] + (wave * FREG_WROWS + j) * C;
+      float xr[NKK];
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) xr[kk] = (2 * kk + hh) < C ? xt[2 * kk + hh] : 0.f;
+      // block fb + 1's MFMAs are issued before block fb's epilogue (its result latency and the
+      // bias reads overlap the conversion)
+      auto l0_mfma = [&](int fb) {
+        f32x16 acc = bias_acc(0, fb);
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w0r[fb][kk], xr[kk], acc, 0, 0, 0);
+        return acc;
+      };
+      f32x16 acc = l0_mfma(0);
+#pragma unroll
+      for (int fb = 0; fb < NB; ++fb) {
+        if (fb + 1 < NB) {
+          const f32x16 accn = l0_mfma(fb + 1);
+          Epi ep;
+          if constexpr (!(dbg & 8))
+#pragma unroll
+            for (int p = 0; p < 8; ++p) epi_part(ep, acc, p, Ha[2 * fb], Ha[2 * fb + 1], 0, fb, codes_tag);
+          acc = accn;
+        } else {
+          accP = acc;
+          pend_pl = 0;
+        }
+      }
+      accNx = bias_acc(1, 0);  // hidden layer 0, block 0
+    };
+    if constexpr ((dbg & 128) != 0) {  // timing only: no layer 0
+      accNx = bias_acc(1, 0);
+    } else if (a.P0) {
+      layer0(T_{});
+    } else {
+      layer0(F_{});
+    }
+    int l = 0;
+    for (; l + 2 < nh; l += 2) {
+      hidden_layer(l, Ha, Hb, F_{});
+      hidden_layer(l + 1, Hb, Ha, F_{});
+    }
+    if (nh - l == 2) {
+      hidden_layer(l, Ha, Hb, F_{});
+      hidden_layer(l + 1, Hb, Ha, T_{});
+      output_layer(Ha);
+    } else {
+      hidden_layer(l, Ha, Hb, T_{});
+      output_layer(Hb);
+    }
+  }
+  // no LDS-DMA may land after the workgroup has released its LDS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Prepared weights of the register-resident forward (see the header comment):
+//   hidden: Wreg[b][l][fb][ks][lane][m] = f16(W_l[b][32 fb + phi(lane & 31)][in0(ks, lane >> 5) + m] w0/2pi)
+//   output: WLreg[b][ks][h][i][m] = f16(W_L[b][i][in0(ks, h) + m]) (0 for i >= O)
+// and, optionally, the backward's bf16 W_l^T copies.
+struct RegPrepArgs {
+  const float* W[FUSED_MAXH];
+  bf16* Wt[FUSED_MAXH];
+  const float* WL;
+  _Float16* out;
+  _Float16* outL;
+  int64_t nb;
+  int nh, O;
+  float k1;
+};
+
+__global__ __launch_bounds__(256) void prep_reg_kernel(RegPrepArgs a) {
+  constexpr int F = 256;
+  const int64_t nhid = a.nb * a.nh * (F * F / 8);
+  const int64_t nout = a.nb * (FREG_WL_BYTES / 16);
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < nhid + nout; idx += (int64_t)gridDim.x * 256) {
+    if (idx < nhid) {
+      const int lane = (int)(idx & 63), ks = (int)((idx >> 6) & 15), fb = (int)((idx >> 10) & 7);
+      const int64_t lb = idx >> 13;
+      const int l = (int)(lb % a.nh);
+      const int64_t b = lb / a.nh;
+      const int orow = 32 * fb + freg_phi(lane & 31);
+      const int in0 = freg_in0(ks, lane >> 5);
+      const float* src = a.W[l] + b * F * F + (int64_t)orow * F + in0;
+      h16x8 v;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) v[m] = (_Float16)(src[m] * a.k1);
+      *(h16x8*)(a.out + idx * 8) = v;
+      if (a.Wt[l]) {
+        bf16* dst = a.Wt[l] + b * F * F + (int64_t)in0 * F + orow;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) dst[(int64_t)m * F] = (bf16)src[m];
+      }
+    } else {
+      const int64_t o = idx - nhid;
+      const int i = (int)(o & 7), h = (int)((o >> 3) & 1), ks = (int)((o >> 4) & 15);
+      const int64_t b = o >> 8;
+      const int in0 = freg_in0(ks, h);
+      h16x8 v;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) v[m] = i < a.O ? (_Float16)a.WL[(b * a.O + i) * F + in0 + m] : (_Float16)0.f;
+      *(h16x8*)(a.outL + o * 8) = v;
+    }
+  }
+}
+
+}  // namespace siren

@@ -12,6 +12,7 @@
 #include "siren_gemm.hip"
 #include "siren_jvp.hip"
 #include "siren_fused.hip"
+#include "siren_fwdreg.hip"
 #include "siren_adam.hip"
 #include "siren_loss.hip"
 
@@ -82,6 +83,7 @@ bool g_fuse_top = false;   // output-layer fusion into the tiled kernels: slower
 bool g_ring_top = true;    // output layer folded into the top 256x256 layer's ring kernels
 bool g_bwd_ring = false;   // middle 256x256 layers in one ring kernel: measured slower (179 vs 145 us)
 bool g_fwd_pipe = true;    // fused forward: half-tile MFMA/VALU pipelined kernel
+bool g_fwd_reg = true;     // fused forward: activations resident in registers (siren_fwdreg.hip)
 bool g_dx_ring = true;     // 256x256 input-gradient layers on the 4-stage ring kernel
 bool g_dw_ring = true;     // 256x256 weight-gradient layers on the 4-stage ring kernel
 bool g_pair_ring = true;   // both gradients of a ring layer in one launch (pair_ring_bf16_kernel)
@@ -204,8 +206,9 @@ Layout layout_of(const siren_mlp_desc* d) {
   }
   lo.frag_off = -1;
   if (fused_shape(d) && g.L > 2) {
+    // hidden-layer fragments, then (register-resident forward) the output-layer fragments
     lo.frag_off = off;
-    off = align_up(off + g.nb * (int64_t)(g.L - 2) * d->dims[1] * d->dims[1] * 2, 256);
+    off = align_up(off + g.nb * ((int64_t)(g.L - 2) * d->dims[1] * d->dims[1] + FREG_WL_BYTES / 2) * 2, 256);
   }
   lo.weights_bytes = off;
   lo.p0_rec = p0_recompute(d);
@@ -471,9 +474,67 @@ int launch_nt(const NTArgs& a, int64_t nb, int kclass, hipStream_t st) {
   return check_launch(names[MODE]);
 }
 
+// Register-resident forward (siren_fwdreg.hip): one weight-prep launch, one forward launch.
+int fused_forward_reg(const siren_mlp_desc* d, const Geo& g, const Layout& lo, const float* x, float* y,
+                      char* saved, char* wbuf, hipStream_t st) {
+  const int F = d->dims[1], nh = g.L - 2;
+  _Float16* wreg = (_Float16*)(wbuf + lo.frag_off);
+  _Float16* wlreg = wreg + g.nb * (int64_t)nh * F * F;
+  {
+    RegPrepArgs p;
+    memset(&p, 0, sizeof(p));
+    for (int l = 1; l + 1 < g.L; ++l) {
+      p.W[l - 1] = d->weight[l];
+      p.Wt[l - 1] = saved ? (bf16*)(saved + lo.wt_op_off[l]) : nullptr;  // the backward's W^T
+    }
+    p.WL = d->weight[g.L - 1];
+    p.out = wreg;
+    p.outL = wlreg;
+    p.nb = g.nb;
+    p.nh = nh;
+    p.O = d->dims[g.L];
+    p.k1 = d->w0 * kInv2Pi;
+    const int64_t work = g.nb * ((int64_t)nh * F * F / 8 + FREG_WL_BYTES / 16);
+    hipLaunchKernelGGL(prep_reg_kernel, dim3(grid1d(work, 1024)), dim3(256), 0, st, p);
+    int rc = check_launch("prep_reg");
+    if (rc) return rc;
+  }
+  FwdRegArgs a;
+  memset(&a, 0, sizeof(a));
+  a.x = x;
+  a.W0 = d->weight[0];
+  a.b0 = d->bias[0];
+  a.Wreg = wreg;
+  a.WLreg = wlreg;
+  for (int l = 1; l + 1 < g.L; ++l) a.bias[l - 1] = d->bias[l];
+  a.bL = d->bias[g.L - 1];
+  a.P0 = (saved && lo.saved_off[0] >= 0) ? saved + lo.saved_off[0] : nullptr;
+  a.Pb = saved ? saved + lo.saved_off[1] : nullptr;
+  a.pstride = (saved && nh >= 2) ? lo.saved_off[2] - lo.saved_off[1] : 0;
+  a.y = y;
+  a.rows_per_batch = g.rows;
+  a.batched = d->weights_batched ? 1 : 0;
+  a.O = d->dims[g.L];
+  a.nh = nh;
+  a.sine_out = d->outermost_linear ? 0 : 1;
+  a.w0 = d->w0;
+  const int64_t tiles = cdiv(g.rows, FREG_WG_ROWS);
+  const int64_t per = std::max<int64_t>(1, 256 / g.nb);
+  dim3 grid((unsigned)std::min<int64_t>(tiles, per), (unsigned)g.nb);
+  using KernelFn = void (*)(FwdRegArgs);
+  static const KernelFn table[2][FUSED_MAXC] = {
+      {fused_fwd_reg_kernel<1, 0>, fused_fwd_reg_kernel<2, 0>, fused_fwd_reg_kernel<3, 0>, fused_fwd_reg_kernel<4, 0>},
+      {fused_fwd_reg_kernel<1, 1>, fused_fwd_reg_kernel<2, 1>, fused_fwd_reg_kernel<3, 1>, fused_fwd_reg_kernel<4, 1>}};
+  tmark_begin(SIREN_KCLASS_FWD_FUSED, st);
+  hipLaunchKernelGGL(table[a.O == 1 ? 1 : 0][d->dims[0] - 1], grid, dim3(512), 0, st, a);
+  tmark_end(SIREN_KCLASS_FWD_FUSED, st);
+  return check_launch("fused_fwd_reg");
+}
+
 int fused_forward(const siren_mlp_desc* d, const Geo& g, const Layout& lo, const float* x, float* y,
                   char* saved, char* wbuf, hipStream_t st) {
   const int F = d->dims[1], nh = g.L - 2;
+  if (g_fwd_reg && nh > 0) return fused_forward_reg(d, g, lo, x, y, saved, wbuf, st);
   if (nh > 0) {
     FragPrepArgs fp;
     memset(&fp, 0, sizeof(fp));
@@ -1553,6 +1614,10 @@ int siren_config_set(const char* key, int64_t value) {
     g_fwd_pipe = value != 0;
     return SIREN_OK;
   }
+  if (key && strcmp(key, "fused_forward_reg") == 0 && (value == 0 || value == 1)) {
+    g_fwd_reg = value != 0;
+    return SIREN_OK;
+  }
   if (key && strcmp(key, "bwd_ring") == 0 && (value == 0 || value == 1)) {
     g_bwd_ring = value != 0;
     return SIREN_OK;
@@ -1578,7 +1643,7 @@ int siren_config_set(const char* key, int64_t value) {
     g_ring_prof_n = 0;
     return SIREN_OK;
   }
-  if (key && strcmp(key, "debug_fwd_skip") == 0 && value >= 0 && value <= 15) {
+  if (key && strcmp(key, "debug_fwd_skip") == 0 && value >= 0 && value <= 31) {
     g_fwd_dbg = (int)value;
     return SIREN_OK;
   }
@@ -1599,6 +1664,7 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "bwd_ring") == 0) return g_bwd_ring ? 1 : 0;
   if (key && strcmp(key, "pair_ring") == 0) return g_pair_ring ? 1 : 0;
   if (key && strcmp(key, "fused_forward_pipe") == 0) return g_fwd_pipe ? 1 : 0;
+  if (key && strcmp(key, "fused_forward_reg") == 0) return g_fwd_reg ? 1 : 0;
   return -1;
 }
 

@@ -1,0 +1,8 @@
+#!/bin/bash
+# Forward-kernel time of each library variant: tools/freg_variants.sh name1 name2 ...
+# (name "base" = siren_mri_amd/libsiren_mri_amd.so, else libsiren_mri_amd_<name>.so)
+for n in "$@"; do
+  if [ "$n" = base ]; then lib=$PWD/siren_mri_amd/libsiren_mri_amd.so; else lib=$PWD/siren_mri_amd/libsiren_mri_amd_$n.so; fi
+  printf "%s: " "$n"
+  SIREN_MRI_AMD_LIB=$lib timeout -k 10 100 python -u tools/freg_probe.py 0 2>/dev/null | tail -1 || exit 1
+done
