@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #define DEV __device__ __forceinline__
 
 namespace siren {
@@ -89,6 +91,16 @@ template <> struct Prec<kPrecBF16> {
     return __builtin_amdgcn_cosf(r - floorf(r));
   }
 };
+
+// Compile-time loop: fn(std::integral_constant<int, i>) for i in [B, E) (indices usable as
+// template arguments, e.g. inline-asm immediate offsets).
+template <int B, int E, typename Fn>
+DEV void static_for(Fn&& fn) {
+  if constexpr (B < E) {
+    fn(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(fn);
+  }
+}
 
 DEV float to_f32(float v) { return v; }
 DEV float to_f32(bf16 v) { return (float)v; }

@@ -102,13 +102,6 @@ DEV constexpr int freg_part_at(int ks) {
   return -1;
 }
 
-template <int B, int E, typename Fn>
-DEV void freg_for(Fn&& fn) {
-  if constexpr (B < E) {
-    fn(std::integral_constant<int, B>{});
-    freg_for<B + 1, E>(fn);
-  }
-}
 
 // Fragment reads from the ring as inline asm: the compiler's wait-count pass cannot tell them
 // apart from the LDS-DMA refills in flight and would drain the DMA (vmcnt(0)) before them. The
@@ -359,7 +352,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   // last_tag: whether the output layer follows — its fragments are prefetched at the end)
   auto hidden_layer = [&](int l, h16x8 (&Hin)[NKS], h16x8 (&Hout)[NKS], auto last_tag) {
     constexpr bool last = decltype(last_tag)::value;
-    freg_for<0, NB>([&](auto fb_c) {
+    static_for<0, NB>([&](auto fb_c) {
       constexpr int fb = decltype(fb_c)::value;
       block_sync(l, fb);
       if (fb == 0 && l == 0) dma_x(tcur + G, (int)(((tcur - t0) / G + 1) & 1));  // next round's x
@@ -367,7 +360,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
       const uint32_t va_cur = slot_va(fb);
       const uint32_t va_nxt = (fb + 1 < NB) ? slot_va(fb + 1) : (last ? wl_va : slot_va(0));
       Epi ep;
-      freg_for<0, NKS>([&](auto ks_c) {
+      static_for<0, NKS>([&](auto ks_c) {
         constexpr int ks = decltype(ks_c)::value;
         constexpr int k3 = ks + PFD;
         if constexpr (k3 < NKS) freg_read<k3 * 1024>(wq[k3 & 3], va_cur);
@@ -396,7 +389,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     f32x16 accO = accNx;
     Epi ep;
     const uint32_t va_nxt = slot_va(0);  // the next round's first block
-    freg_for<0, NKS>([&](auto ks_c) {
+    static_for<0, NKS>([&](auto ks_c) {
       constexpr int ks = decltype(ks_c)::value;
       constexpr int k3 = ks + PFD;
       if constexpr (k3 < NKS) freg_read<k3 * 256>(wq[k3 & 3], wl_va);

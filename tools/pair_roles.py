@@ -20,8 +20,10 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--side", type=int, default=512)
     p.add_argument("--reps", type=int, default=10)
+    p.add_argument("--roles", type=int, nargs="*", default=[3, 1, 2, 3])
+    p.add_argument("--option", default=None, help="NAME=V1,V2: repeat every role set per option value")
     cli = p.parse_args()
-    sys.argv = [sys.argv[0], "--side", str(cli.side)]
+    sys.argv = [sys.argv[0], "--side", str(cli.side), "--no-psnr", "--no-cpu-baseline"]
     args = bench.parse()
     _native.load_library()
     dev = torch.device("cuda", 0)
@@ -29,7 +31,13 @@ def main():
     for _ in range(5):
         step()
     torch.cuda.synchronize()
-    for roles in (3, 1, 2, 3):
+    opts = [(None, None)]
+    if cli.option:
+        name, vals = cli.option.split("=")
+        opts = [(name, int(v)) for v in vals.split(",")]
+    for (oname, oval), roles in [(o, r) for o in opts for r in cli.roles]:
+        if oname:
+            _native.set_option(oname, oval)
         _native.set_option("debug_pair_roles", roles)
         row = []
         for kc in (_native.KCLASS_PAIR_RING, _native.KCLASS_PAIR_RING_TOP, _native.KCLASS_PAIR_RING_BOT):
@@ -37,7 +45,7 @@ def main():
                 for _ in range(cli.reps):
                     step()
             row.append(f"{kc}: {t.total_ms / max(1, t.launches) * 1e3:7.1f} us")
-        print(f"roles={roles}  " + "  ".join(row), flush=True)
+        print((f"{oname}={oval} " if oname else "") + f"roles={roles}  " + "  ".join(row), flush=True)
     _native.set_option("debug_pair_roles", 3)
 
 
