@@ -69,13 +69,13 @@ def test_check_rejects_unsupported(dims, msg):
 
 def test_saved_bytes_formula_bf16():
     """saved = prepared bf16 weights (W, W^T and the fused forward's fragment-order copy of each
-    MFMA layer) + one 16-bit phase tensor per sine layer except the first (recomputed from x by
+    MFMA layer, plus the register-resident forward's 4 KiB output-layer fragments) + one 16-bit phase tensor per sine layer except the first (recomputed from x by
     the backward) — 2 bytes per activation element."""
     lib = _native.load_library()
     rows = 512 * 512
     d = _desc([2, 256, 256, 256, 256, 1], rows_per_batch=rows)
     got = lib.siren_mlp_saved_bytes(ctypes.byref(d))
-    weights = 3 * 3 * 256 * 256 * 2
+    weights = 3 * 3 * 256 * 256 * 2 + 4096
     phases = 3 * rows * 256 * 2
     assert got == weights + phases
 
