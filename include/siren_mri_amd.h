@@ -212,10 +212,6 @@ int siren_sse_backward(const float* d, const float* mask, int64_t n, int64_t mas
  *   "fused_forward_reg"  1 (default): the fused forward keeps every layer's activations in the
  *                    registers of the wave that owns the rows (weights streamed through an LDS
  *                    ring); 0: the LDS-staged fused forward below.
- *   "split_pair"     0 (default): middle 256x256 bf16 layers on the pair_ring kernel (one
- *                    workgroup per gradient); 1: workgroup pairs that each take both gradients for
- *                    half of the input-feature columns (siren_spair.hip; bit-identical results,
- *                    measured slower: the tile stream through LDS-DMA bounds both forms).
  *   "fused_forward_pipe"  1 (default): the LDS-staged fused forward overlaps one half-tile's MFMA
  *                    work with the other's epilogue; 0: the sequential single-kernel forward.
  *   "bwd_ring"       0 (default), 1: middle 256x256 bf16 layers compute both gradients in one

@@ -877,6 +877,35 @@ struct RingProf {
 template <int VMCNT>
 DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMCNT) : "memory"); }
 
+// The dx_ring MFMA chain over K = 256: acc = sum_ks W^T[ks] . B(ks), the B fragments read from
+// the staged 32-row tile (row r, 16-byte chunk c at chunk c ^ (r & 15)). The lane's fragment of
+// K step ks sits at byte off0 ^ (32 ks) of the image (off0 = r * 512 + 16 (h ^ (r & 15))), so
+// each read is one XOR and one add. The reads are inline asm, PF in flight, each MFMA tied to
+// its own read by a counted wait: the compiler neither serialises them (one read, wait, MFMA)
+// under register pressure nor drains the ring's LDS-DMA in front of them (vmcnt(0)).
+DEV void ring_read_b128(bf16x8& d, uint32_t va) { asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"(va)); }
+template <int N>
+DEV void ring_lgkm(bf16x8& v) { asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "n"(N)); }
+template <int PF = 4>
+DEV f32x16 ring_chain(const bf16x8 (&wf)[16], uint32_t sbase, uint32_t off0) {
+  bf16x8 b[PF];
+  static_for<0, PF>([&](auto k_c) {
+    constexpr int k = decltype(k_c)::value;
+    ring_read_b128(b[k], sbase + (off0 ^ (32 * k)));
+  });
+  f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  static_for<0, 16>([&](auto ks_c) {
+    constexpr int ks = decltype(ks_c)::value;
+    constexpr int after = (15 - ks) < (PF - 1) ? (15 - ks) : (PF - 1);  // reads issued after ks's
+    ring_lgkm<after>(b[ks % PF]);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], b[ks % PF], acc, 0, 0, 0);
+    if constexpr (ks + PF < 16) ring_read_b128(b[ks % PF], sbase + (off0 ^ (32 * (ks + PF))));
+  });
+  return acc;
+}
+
 // BOTC > 0: the bottom hidden layer with the first layer folded in (C = BOTC inputs): dZ_0 stays
 // in LDS; a VALU pass over it accumulates dW_0 / db_0 (first_bwd_kernel's sums, per-workgroup
 // partial slabs in a.bot.part) and, with DXOUT, writes dx = dZ_0 W_0 (a.C, [rows, C] f32).
@@ -1183,8 +1212,13 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
   constexpr int A_BYTES = BM * K * 2, C_BYTES = BM * N * 2, STAGE = A_BYTES + C_BYTES + G_BYTES;
   static_assert(S * STAGE == dx_ring_lds_bytes<0, TOPO>(), "dx_ring LDS size");
   constexpr int NKS = K / 16;
-  constexpr int NDMA = 4 + (TOPO > 0 ? 1 : 0);  // VMEM instructions per wave per stage (loads)
-  constexpr int NST = 2;                        // buffer stores per wave per tile
+  // the ring's DMA is issued by waves 0..NIO-1 only (4 dZ + 4 P pieces each): waves 4-7 lose the
+  // VALU/MFMA arbitration to their SIMD partners, and the issue cost lands where the barrier
+  // wait is (measured: the partners wait for them at every barrier)
+  constexpr int NIO = 4;
+  constexpr int NPC = 16 / NIO;                        // 1 KB pieces per image per I/O wave
+  constexpr int NDMA = 2 * NPC + (TOPO > 0 ? 1 : 0);  // VMEM loads per I/O wave per stage
+  constexpr int NST = 2;                               // buffer stores per wave per tile
   // VMEM ops issued after DMA(i) when iteration i waits for it: stores of tiles i-3..i-1 and the
   // DMAs of tiles i+1, i+2
   constexpr int STEADY = 3 * NST + 2 * NDMA;
@@ -1213,11 +1247,12 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
   }
 
   // both images: row r (512 B), 16-byte chunk c stored at chunk c ^ (r & 15)
+  const uint32_t boff0 = r32 * 512 + 16 * (h ^ (r32 & 15));  // B fragment of K step 0 (ring_chain)
   auto img_off = [](int r, int c) -> int { return r * 512 + ((c ^ (r & 15)) << 4); };
-  uint32_t dvoff[2];  // DMA piece j: rows 2 i, 2 i + 1 (i = wave + 8 j)
+  uint32_t dvoff[NPC];  // DMA piece j: rows 2 i, 2 i + 1 (i = wave + NIO j)
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int i = wave + 8 * j;
+  for (int j = 0; j < NPC; ++j) {
+    const int i = wave + NIO * j;
     const int r = 2 * i + (lane >> 5), p = lane & 31;
     dvoff[j] = r * 512 + 16 * (p ^ (r & 15));
   }
@@ -1246,19 +1281,22 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
     if (part == 0) {
       const __amdgpu_buffer_rsrc_t rA = make_rsrc((const bf16*)(TOPO > 0 ? a.top.Ptop : a.A) + m0 * K, nv * K * 2);
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(base + (wave + 8 * j) * 1024), 16, dvoff[j], 0, 0, 0);
+      for (int j = 0; j < NPC; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(base + (wave + NIO * j) * 1024), 16, dvoff[j], 0, 0,
+                                                 0);
       if constexpr (TOPO > 0) {
+        // dy rows of the tile: BM * O floats; I/O wave w moves bytes [16 GL w, 16 GL (w + 1))
+        constexpr int GL = 8 * TOPO / NIO;
         const __amdgpu_buffer_rsrc_t rG = make_rsrc(a.top.dy + m0 * TOPO, nv * TOPO * 4);
-        if (lane < TOPO)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rG, (lds_void*)(base + A_BYTES + C_BYTES + 16 * TOPO * wave), 16,
-                                                   16 * (TOPO * wave + lane), 0, 0, 0);
+        if (lane < GL)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rG, (lds_void*)(base + A_BYTES + C_BYTES + 16 * GL * wave), 16,
+                                                   16 * (GL * wave + lane), 0, 0, 0);
       }
     } else {
       const __amdgpu_buffer_rsrc_t rP = make_rsrc((const uint16_t*)a.Paux + m0 * N, nv * N * 2);
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (lds_void*)(base + A_BYTES + (wave + 8 * j) * 1024), 16,
+      for (int j = 0; j < NPC; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (lds_void*)(base + A_BYTES + (wave + NIO * j) * 1024), 16,
                                                  dvoff[j], 0, 0, 0);
     }
   };
@@ -1290,8 +1328,10 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
 
   // (An in-wave software pipeline — tile i's MFMAs beside tile i - 1's epilogue — measured
   // slower: the two waves of a SIMD already overlap one's MFMAs with the other's epilogue.)
-  for (int s = 0; s < S - 1; ++s)
-    if (s < niter) dma(t0 + s * G, s);
+  const bool io = wave < NIO;
+  if (io)
+    for (int s = 0; s < S - 1; ++s)
+      if (s < niter) dma(t0 + s * G, s);
 
   RingProf prof(a.prof);
   for (int64_t i = 0; i < niter; ++i) {
@@ -1299,13 +1339,15 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
     const int64_t t = t0 + i * G;
     // this stage's DMA (this wave's part) landed; then every wave's part, and every wave is done
     // with the stage the next DMA overwrites (tile i - 1: MFMA reads and its store pass)
-    if (i >= S - 1 && i + S - 2 < niter) vm_wait<STEADY>();
-    else vm_drain();
+    if (io) {
+      if (i >= S - 1 && i + S - 2 < niter) vm_wait<STEADY>();
+      else vm_drain();
+    }
     prof.tick(0);
     lds_barrier();
     prof.tick(1);
     // (issuing these pieces between the MFMAs instead measured slower)
-    if (i + S - 1 < niter) dma(t0 + (i + S - 1) * G, (int)((i + S - 1) % S));
+    if (io && i + S - 1 < niter) dma(t0 + (i + S - 1) * G, (int)((i + S - 1) % S));
     prof.tick(2);
     char* base = smem + st * STAGE;
     if constexpr (TOPO > 0) {
@@ -1333,14 +1375,7 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
       lds_barrier();
     }
     // dZ_{l-1}^T (32 features x 32 rows) = W^T slice . dZ_l^T: B fragments = dZ rows from LDS
-    f32x16 acc;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      const bf16x8 bfr = *(const bf16x8*)(base + img_off(r32, 2 * ks + h));
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], bfr, acc, 0, 0, 0);
-    }
+    const f32x16 acc = ring_chain(wf, lds_addr(base), boff0);
     prof.tick(3);
     epilogue(t, st, acc);
     prof.tick(5);
@@ -1349,27 +1384,47 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
 }
 
 // dx_ring body of the bottom hidden layer with the first layer folded in and P_0 rebuilt from x
-// (C = BOTC <= 4 inputs). Transposed MFMA as dx_ring_body_v2; the epilogue keeps dZ_0 in
-// registers (rounded to bf16 exactly like the stored-and-reloaded value of the v1 kernel) and
-// accumulates per lane: db_0 and dW_0 = dZ_0^T x for its 16 features (reduced over the lanes once,
-// at the end), and dx = dZ_0 W_0 partials over its features, summed over the 8 waves in wave
-// order through LDS after the next barrier. The ring carries dZ_1 and x only (no P image).
+// (C = BOTC <= 4 inputs). Transposed MFMA as dx_ring_body_v2 (lane (row r32, half h) holds the
+// wave's features 32 w + 8 g + 4 h + e in accumulator element 4 g + e). Per tile the epilogue
+//   z_0 (revolutions) = one or two f32 MFMAs (32x32x2) with operands W_0 w0/2pi, x and b_0 w0/2pi:
+//                       the register-resident forward's layer-0 instructions on the same values,
+//                       so the phase is bit-identical to the one its sin() used
+//   dZ_0 = bf16((acc cos(fract(z_0))) w0)                       (modules.py:38 chain rule)
+//   dx partial = W_0^T dZ_0^T over the wave's 32 features: two bf16 MFMAs whose A operand holds
+//                W_0 split into bf16 hi + lo rows (hi rows 0..C-1, lo rows 4..4+C-1), so the
+//                product is exact to ~2^-16 of W_0; the dZ_0 fragments are the accumulator
+//                elements in order (K step s = elements 8 s .. 8 s + 7)
+//   db_0, dW_0 = dZ_0^T x: per-lane VALU sums (reduced over the lanes once, at the end).
+// The ring carries dZ_1 and x only (no P image).
+// Stagger (MI355X_MICROARCH.md, two waves per SIMD, item 9): waves 4-7 run each tile's epilogue
+// one tile late, at the head of the next iteration, keeping the accumulator and the x values in
+// registers across the barrier; so on every SIMD one wave's MFMA chain runs beside its partner's
+// VALU epilogue instead of both waves contending for the matrix pipe and then for VALU issue.
+// Per-lane sums keep their tile order (bit-identical to the unstaggered order). The dx partials
+// of tile j (waves 0-3 in iteration j, waves 4-7 in j + 1) sit in Yp[j % 3] and are summed over
+// the 8 waves x 2 halves by the dx store pass of iteration j + 2.
 template <int BOTC, bool DXOUT>
 DEV void dx_ring_body_v2bot(const NTArgs& a, char* smem, const int64_t t0, const int64_t G, const int64_t niter,
                             const int64_t slab) {
-  using PT = Prec<kPrecBF16>;
   constexpr int K = 256, F0 = 256, BM = RING_BM, S = RING_S, C = BOTC;
+  constexpr int NKK = (C + 1) / 2;                // K = 2 steps of the z_0 MFMA
   constexpr int A_BYTES = BM * K * 2, X_BYTES = BM * C * 4, STAGE = A_BYTES + X_BYTES;
-  constexpr int YP_BYTES = 2 * 8 * BM * C * 4;  // dx partials [2][wave][row][C]
-  constexpr int W0_BYTES = F0 * C * 4 + F0 * 4;  // W_0 [F0][C] and k * b_0 [F0], staged once
-  static_assert(S * STAGE + YP_BYTES + W0_BYTES <= dx_ring_lds_bytes<BOTC, 0>(), "dx_ring LDS size");
+  constexpr int YP_BYTES = 3 * 16 * BM * C * 4;  // dx partials [3][wave][half][row][C]
+  static_assert(C <= 4, "dx MFMA rows: hi 0..3, lo 4..7");
+  static_assert(S * STAGE + YP_BYTES <= dx_ring_lds_bytes<BOTC, 0>(), "dx_ring LDS size");
   constexpr int NKS = K / 16;
-  constexpr int NDMA = 2 + 1;              // dZ_1 pieces + the x piece
-  constexpr int NST = DXOUT ? 1 : 0;       // dx stores per wave per tile
+  // C <= 2: staggered halves (waves 4-7 run each epilogue one tile late; C = 3, 4: the late
+  // copies of acc and x would spill). With the stagger the ring's I/O (DMA issue, vm waits and
+  // dx stores) is all done by waves 0-3, which otherwise wait at the barrier for the late half.
+  constexpr bool STAG = C <= 2;
+  constexpr int NIO = STAG ? 4 : 8;        // waves that issue the DMA and the dx stores
+  constexpr int NPC = 16 / NIO;            // dZ_1 pieces (1 KB) per I/O wave per tile
+  constexpr int XL = 8 * C / NIO;          // lanes (16 B) of the x piece per I/O wave
+  constexpr int SR = BM / NIO;             // dx rows stored per I/O wave
+  constexpr int NDMA = NPC + 1;            // dZ_1 pieces + the x piece
+  constexpr int NST = DXOUT ? 1 : 0;       // dx stores per I/O wave per tile
   constexpr int STEADY = (S - 1) * NST + (S - 2) * NDMA;
   float* Yp = (float*)(smem + S * STAGE);
-  float* W0s = (float*)(smem + S * STAGE + YP_BYTES);
-  float* b0ks = W0s + F0 * C;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -1377,20 +1432,39 @@ DEV void dx_ring_body_v2bot(const NTArgs& a, char* smem, const int64_t t0, const
   const int64_t batch = blockIdx.y;
   const int64_t rows = a.rows_per_batch;
   const int64_t rowbase = batch * rows;
-  const float kph = PT::enck(a.w0);
+  const float k1 = a.w0 * kInv2Pi;
+  const int fw = 32 * wave;
 
-  const bf16* Wb = (const bf16*)a.W + batch * a.w_bstride + (int64_t)(32 * wave + r32) * K;
+  const bf16* Wb = (const bf16*)a.W + batch * a.w_bstride + (int64_t)(fw + r32) * K;
   bf16x8 wf[NKS];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) wf[ks] = *(const bf16x8*)(Wb + 16 * ks + 8 * h);
-  // W_0 and k * b_0 staged in LDS (visible after the first barrier); the lane's 16 first-layer
-  // features are f = 32 w + 8 g + 4 h + e, u = 4 g + e
-  {
-    const float* W0 = a.bot.W0 + batch * a.bot.w0_bstride;
-    const float* b0 = a.bot.b0 + batch * a.bot.b0_bstride;
-    for (int idx = tid; idx < F0 * C; idx += 512) W0s[idx] = W0[idx];
-    for (int f = tid; f < F0; f += 512) b0ks[f] = b0[f] * kph;
-  }
+  const float* W0 = a.bot.W0 + batch * a.bot.w0_bstride;
+  const float* b0 = a.bot.b0 + batch * a.bot.b0_bstride;
+  // z_0 MFMA: A lane (i, k) = W_0[fw + i][2 kk + k] w0/2pi, C = b_0 w0/2pi of the lane's features
+  float w0a[NKK];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) w0a[kk] = 2 * kk + h < C ? W0[(fw + r32) * C + 2 * kk + h] * k1 : 0.f;
+  f32x16 zb;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) zb[v] = b0[fw + 8 * (v >> 2) + 4 * h + (v & 3)] * k1;
+  // dx MFMA: A lane (i, kh) for K step s holds W_0 (hi for i < C, lo for 4 <= i < 4 + C) at the
+  // features f(s, 8 kh + m) = fw + 8 (2 s + m / 4) + 4 kh + m % 4 of the B fragment's K order
+  bf16x8 dxa[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int f = fw + 8 * (2 * s + (m >> 2)) + 4 * h + (m & 3);
+      const int c = r32 & 3;
+      bf16 v = (bf16)0.f;
+      if (r32 < 8 && c < C) {
+        const float w = W0[f * C + c];
+        const bf16 hi = (bf16)w;
+        v = r32 < 4 ? hi : (bf16)(w - (float)hi);
+      }
+      dxa[s][m] = v;
+    }
   float dwacc[16][C], dbacc[16];
 #pragma unroll
   for (int u = 0; u < 16; ++u) {
@@ -1399,12 +1473,13 @@ DEV void dx_ring_body_v2bot(const NTArgs& a, char* smem, const int64_t t0, const
     for (int c = 0; c < C; ++c) dwacc[u][c] = 0.f;
   }
 
+  const uint32_t boff0 = r32 * 512 + 16 * (h ^ (r32 & 15));  // B fragment of K step 0 (ring_chain)
   auto img_off = [](int r, int c) -> int { return r * 512 + ((c ^ (r & 15)) << 4); };
-  uint32_t dvoff[2];
+  uint32_t dvoff[NPC];  // DMA piece q = wave + NIO j: rows 2 q, 2 q + 1
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int i = wave + 8 * j;
-    const int r = 2 * i + (lane >> 5), p = lane & 31;
+  for (int j = 0; j < NPC; ++j) {
+    const int q = wave + NIO * j;
+    const int r = 2 * q + (lane >> 5), p = lane & 31;
     dvoff[j] = r * 512 + 16 * (p ^ (r & 15));
   }
   auto nval = [&](int64_t t) -> int64_t {
@@ -1417,95 +1492,122 @@ DEV void dx_ring_body_v2bot(const NTArgs& a, char* smem, const int64_t t0, const
     const __amdgpu_buffer_rsrc_t rA = make_rsrc((const bf16*)a.A + m0 * K, nv * K * 2);
     const __amdgpu_buffer_rsrc_t rX = make_rsrc(a.bot.x + m0 * C, nv * C * 4);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(base + (wave + 8 * j) * 1024), 16, dvoff[j], 0, 0, 0);
-    // x rows of the tile: BM * C floats; wave w moves bytes [16 C w, 16 C (w + 1)) (C lanes)
-    if (lane < C)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)(base + A_BYTES + 16 * C * wave), 16,
-                                               16 * (C * wave + lane), 0, 0, 0);
+    for (int j = 0; j < NPC; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(base + (wave + NIO * j) * 1024), 16, dvoff[j], 0, 0,
+                                               0);
+    // x rows of the tile: BM * C floats; I/O wave w moves bytes [16 XL w, 16 XL (w + 1)) (XL lanes)
+    if (lane < XL)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)(base + A_BYTES + 16 * XL * wave), 16,
+                                               16 * (XL * wave + lane), 0, 0, 0);
   };
-  // dx of tile t from the wave partials in Yp[buf]: wave w stores rows 4 w .. 4 w + 3 (lanes < 4 C)
+  // dx of tile t from the partials in Yp[buf]: I/O wave w stores rows SR w .. SR (w + 1) - 1
   auto dx_store = [&](int64_t t, int buf) {
     if constexpr (DXOUT) {
-      const int idx = 4 * C * wave + lane;  // (row, c) element of the tile, row-major
+      const int idx = SR * C * wave + lane;  // (row, c) element of the tile, row-major
       float v = 0.f;
-      if (lane < 4 * C) {
+      if (lane < SR * C) {
 #pragma unroll
-        for (int w = 0; w < 8; ++w) v += Yp[(buf * 8 + w) * BM * C + idx];
+        for (int w = 0; w < 16; ++w) v += Yp[(buf * 16 + w) * BM * C + idx];
       }
       const __amdgpu_buffer_rsrc_t rD = make_rsrc(a.C ? (float*)a.C + (rowbase + t * BM) * C : nullptr,
                                                   a.C ? nval(t) * C * 4 : 0);
-      if (lane < 4 * C) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rD, idx * 4, 0, 0);
+      if (lane < SR * C) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rD, idx * 4, 0, 0);
     }
   };
 
-  for (int s = 0; s < S - 1; ++s)
-    if (s < niter) dma(t0 + s * G, s);
-
-  for (int64_t i = 0; i < niter; ++i) {
-    const int st = (int)(i % S);
-    const int64_t t = t0 + i * G;
-    if (i >= S - 1 && i + S - 2 < niter) vm_wait<STEADY>();
-    else vm_drain();
-    lds_barrier();  // also publishes tile i - 1's dx partials
-    if (i + S - 1 < niter) dma(t0 + (i + S - 1) * G, (int)((i + S - 1) % S));
-    if (i > 0) dx_store(t - G, (int)((i - 1) & 1));
-    char* base = smem + st * STAGE;
-    f32x16 acc;
+  // epilogue of tile j from its accumulator and x values (see the header)
+  auto epilogue = [&](const f32x16& acc, const float (&xb)[NKK], const float (&xv)[C], int64_t j) {
+    f32x16 z = zb;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    for (int kk = 0; kk < NKK; ++kk) z = __builtin_amdgcn_mfma_f32_32x32x2f32(w0a[kk], xb[kk], z, 0, 0, 0);
+    bf16x8 dzb[2];
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      const bf16x8 bfr = *(const bf16x8*)(base + img_off(r32, 2 * ks + h));
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], bfr, acc, 0, 0, 0);
-    }
-    // epilogue: P_0 rebuilt from x (the forward's arithmetic), dZ_0 = bf16(acc cos(P_0) w0)
-    const float* xr = (const float*)(base + A_BYTES) + r32 * C;
-    float xv[C];
-#pragma unroll
-    for (int c = 0; c < C; ++c) xv[c] = xr[c];
-    float dxp[C];
-#pragma unroll
-    for (int c = 0; c < C; ++c) dxp[c] = 0.f;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int f0 = 32 * wave + 8 * g + 4 * h;
-      float wv[4 * C];
-#pragma unroll
-      for (int k4 = 0; k4 < C; ++k4) {
-        const f32x4 v = *(const f32x4*)(W0s + f0 * C + 4 * k4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) wv[4 * k4 + e] = v[e];
-      }
-      const f32x4 bk = *(const f32x4*)(b0ks + f0);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int u = 4 * g + e;
-        float z = 0.f;
-#pragma unroll
-        for (int c = 0; c < C; ++c) z = fmaf(xv[c], wv[e * C + c], z);
-        const uint16_t ph = PT::enc_scaled(z, bk[e], kph);
-        const float dz = (float)(bf16)((acc[u] * PT::cosp(ph)) * a.w0);
-        dbacc[u] += dz;
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-          dwacc[u][c] = fmaf(dz, xv[c], dwacc[u][c]);
-          dxp[c] = fmaf(dz, wv[e * C + c], dxp[c]);
-        }
-      }
-    }
+    for (int v = 0; v < 16; ++v)
+      dzb[v >> 3][v & 7] = (bf16)((acc[v] * __builtin_amdgcn_cosf(__builtin_amdgcn_fractf(z[v]))) * a.w0);
     if constexpr (DXOUT) {
+      f32x16 dd;
 #pragma unroll
-      for (int c = 0; c < C; ++c) dxp[c] += __shfl_xor(dxp[c], 32, 64);
-      if (h == 0) {
+      for (int e = 0; e < 16; ++e) dd[e] = 0.f;
+      dd = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dxa[0], dzb[0], dd, 0, 0, 0);
+      dd = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dxa[1], dzb[1], dd, 0, 0, 0);
+      float* yp = Yp + (((int)(j % 3) * 8 + wave) * 2 + h) * BM * C + r32 * C;
 #pragma unroll
-        for (int c = 0; c < C; ++c) Yp[((i & 1) * 8 + wave) * BM * C + r32 * C + c] = dxp[c];
-      }
+      for (int c = 0; c < C; ++c) yp[c] = dd[c];
     }
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const float dz = (float)dzb[v >> 3][v & 7];
+      dbacc[v] += dz;
+#pragma unroll
+      for (int c = 0; c < C; ++c) dwacc[v][c] = fmaf(dz, xv[c], dwacc[v][c]);
+    }
+  };
+
+  if (wave < NIO)
+    for (int s = 0; s < S - 1; ++s)
+      if (s < niter) dma(t0 + s * G, s);
+
+  auto loop = [&](auto late_tag) {
+    constexpr bool LATE = decltype(late_tag)::value;
+    f32x16 accp;
+    float xbp[NKK], xvp[C];
+    RingProf prof(a.prof);
+    for (int64_t i = 0; i < niter; ++i) {
+      const int st = (int)(i % S);
+      // counted wait: from iteration S + 1 on, S - 1 dx stores and S - 2 DMAs follow DMA(i)
+      if constexpr (!LATE) {
+        if (i >= S + 1 && i + S - 2 < niter) vm_wait<STEADY>();
+        else vm_drain();
+      }
+      prof.tick(0);
+      lds_barrier();  // DMA(i) of every I/O wave landed; also publishes tile i - 2's dx partials
+      prof.tick(1);
+      if constexpr (!LATE) {
+        if (i + S - 1 < niter) dma(t0 + (i + S - 1) * G, (int)((i + S - 1) % S));
+        if (i > 1) dx_store(t0 + (i - 2) * G, (int)((i - 2) % 3));
+      }
+      prof.tick(2);
+      if constexpr (LATE) {
+        if (i > 0) epilogue(accp, xbp, xvp, i - 1);
+      }
+      prof.tick(3);
+      char* base = smem + st * STAGE;
+      const float* xr = (const float*)(base + A_BYTES) + r32 * C;
+      float xb[NKK], xv[C];
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) xb[kk] = 2 * kk + h < C ? xr[2 * kk + h] : 0.f;
+#pragma unroll
+      for (int c = 0; c < C; ++c) xv[c] = xr[c];
+      const f32x16 acc = ring_chain(wf, lds_addr(base), boff0);
+      prof.tick(4);
+      if constexpr (LATE) {
+        accp = acc;
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) xbp[kk] = xb[kk];
+#pragma unroll
+        for (int c = 0; c < C; ++c) xvp[c] = xv[c];
+      } else {
+        epilogue(acc, xb, xv, i);
+      }
+      prof.tick(5);
+    }
+    prof.flush(blockIdx.x);
+    if constexpr (LATE) {
+      if (niter > 0) epilogue(accp, xbp, xvp, niter - 1);
+    }
+  };
+  if constexpr (STAG) {
+    if (wave >= 4) loop(std::true_type{});
+    else loop(std::false_type{});
+  } else {
+    loop(std::false_type{});
   }
   if (niter > 0) {
     lds_barrier();
-    dx_store(t0 + (niter - 1) * G, (int)((niter - 1) & 1));
+    if (wave < NIO) {
+      if (niter > 1) dx_store(t0 + (niter - 2) * G, (int)((niter - 2) % 3));
+      dx_store(t0 + (niter - 1) * G, (int)((niter - 1) % 3));
+    }
   }
   // per-workgroup slab: dW_0 [F0][C] then db_0 [F0]: sums over the 32 lanes of each half-wave
 #pragma unroll
@@ -1523,7 +1625,7 @@ DEV void dx_ring_body_v2bot(const NTArgs& a, char* smem, const int64_t t0, const
     for (int g = 0; g < 4; ++g)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int f = 32 * wave + 8 * g + 4 * h + e, u = 4 * g + e;
+        const int f = fw + 8 * g + 4 * h + e, u = 4 * g + e;
 #pragma unroll
         for (int c = 0; c < C; ++c) part[f * C + c] = dwacc[u][c];
         part[F0 * C + f] = dbacc[u];
@@ -1562,7 +1664,8 @@ namespace siren {
 // wave per stage. Counted waits keep three stages (96 KB per CU) in flight.
 // ------------------------------------------------------------------------------------------
 // RECC > 0: layer 1 with P_0 not kept by the forward: the x tile (RECC inputs) rides in the ring
-// instead of P_0, and the convert pass recomputes the phases exactly as the forward did.
+// instead of P_0, and the convert pass rebuilds H_0 = sin(fract(z_0)) from x and the prescaled
+// W_0 w0/2pi, b_0 w0/2pi (the register-resident forward's layer-0 arithmetic, exact fp32 phase).
 // TOPO > 0: the top hidden layer with the output layer folded in (outermost_linear, O = TOPO): the
 // ring carries P_top (in the dZ image) and the dy tile; the convert pass forms dZ_top in place
 // (last_bwd_kernel's arithmetic) and sums the output layer's dW_L = dy^T sin(P_top), db_L = sum dy
@@ -1586,8 +1689,11 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
   constexpr int G_BYTES = TOPO > 0 ? KC * TOPO * 4 : 0;
   constexpr int D_BYTES = KC * M * 2, P_BYTES = KC * N * 2, STAGE = D_BYTES + P_BYTES + X_BYTES + G_BYTES;
   static_assert(S * STAGE == dw_ring_lds_bytes<RECC, TOPO>(), "dw_ring LDS size");
-  constexpr int ND = 2 + (TOPO > 0 ? 1 : 0);   // DMA instructions per wave per stage: dZ (or P_top) (+ dy)
-  constexpr int NP = RECC > 0 ? 1 : 2;         // P_{l-1} (or x)
+  // the ring's DMA is issued by waves 0..NIO-1 only (see dx_ring_body_v2)
+  constexpr int NIO = 4;
+  constexpr int NPC = 16 / NIO;                      // 1 KB pieces per image per I/O wave
+  constexpr int ND = NPC + (TOPO > 0 ? 1 : 0);       // DMA per I/O wave per stage: dZ (or P_top) (+ dy)
+  constexpr int NP = RECC > 0 ? 1 : NPC;             // P_{l-1} (or x)
   constexpr int NDMA = ND + NP;
   static_assert(!(RECC > 0 && TOPO > 0), "one hidden layer: the plain output-layer path");
 
@@ -1611,10 +1717,10 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
   // (4 consecutive chunks each) then fall on four disjoint bank groups
   auto swz = [](int r, int c) -> int { return c ^ (4 * (r & 3)); };
   // DMA piece j of a 32-row image: rows 2 i, 2 i + 1 (i = wave + 8 j), lane -> (row, chunk)
-  uint32_t dvoff[2];
+  uint32_t dvoff[NPC];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int i = wave + 8 * j;
+  for (int j = 0; j < NPC; ++j) {
+    const int i = wave + NIO * j;
     const int r = 2 * i + (lane >> 5), p = lane & 31;
     dvoff[j] = r * 512 + 16 * swz(r, p);
   }
@@ -1622,23 +1728,25 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
     char* base = smem + st * STAGE;
     const uint32_t cb = (uint32_t)(k * KC * 512);  // the chunk's first byte in a 512-byte-row tensor
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rD, (lds_void*)(base + (wave + 8 * j) * 1024), 16, dvoff[j] + cb, 0,
+    for (int j = 0; j < NPC; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rD, (lds_void*)(base + (wave + NIO * j) * 1024), 16, dvoff[j] + cb, 0,
                                                0, 0);
     if constexpr (TOPO > 0) {
-      // dy rows of the chunk: KC * O floats; wave w moves bytes [16 O w, 16 O (w + 1)) (O lanes)
-      if (lane < TOPO)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rG, (lds_void*)(base + D_BYTES + P_BYTES + X_BYTES + 16 * TOPO * wave),
-                                                 16, (uint32_t)(k * KC * TOPO * 4) + 16 * (TOPO * wave + lane), 0, 0, 0);
+      // dy rows of the chunk: KC * O floats; I/O wave w moves bytes [16 GL w, 16 GL (w + 1))
+      constexpr int GL = 8 * TOPO / NIO;
+      if (lane < GL)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rG, (lds_void*)(base + D_BYTES + P_BYTES + X_BYTES + 16 * GL * wave),
+                                                 16, (uint32_t)(k * KC * TOPO * 4) + 16 * (GL * wave + lane), 0, 0, 0);
     }
     if constexpr (RECC > 0) {
-      if (lane < RECC)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (lds_void*)(base + D_BYTES + P_BYTES + 16 * RECC * wave), 16,
-                                                 (uint32_t)(k * KC * RECC * 4) + 16 * (RECC * wave + lane), 0, 0, 0);
+      constexpr int XL = 8 * RECC / NIO;
+      if (lane < XL)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (lds_void*)(base + D_BYTES + P_BYTES + 16 * XL * wave), 16,
+                                                 (uint32_t)(k * KC * RECC * 4) + 16 * (XL * wave + lane), 0, 0, 0);
     } else {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (lds_void*)(base + D_BYTES + (wave + 8 * j) * 1024), 16,
+      for (int j = 0; j < NPC; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (lds_void*)(base + D_BYTES + (wave + NIO * j) * 1024), 16,
                                                  dvoff[j] + cb, 0, 0, 0);
     }
   };
@@ -1679,11 +1787,12 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
   if constexpr (RECC > 0) {
     const float* W0 = a.rec_W0 + batch * a.rec_w0_bstride;
     const float* b0 = a.rec_b0 + batch * a.rec_b0_bstride;
+    const float k1 = a.w0 * kInv2Pi;  // operands in revolutions, as the forward's layer 0
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      b0r[e] = b0[8 * cth + e];
+      b0r[e] = b0[8 * cth + e] * k1;
 #pragma unroll
-      for (int c = 0; c < CR; ++c) w0r[e][c] = W0[(8 * cth + e) * RECC + c];
+      for (int c = 0; c < CR; ++c) w0r[e][c] = W0[(8 * cth + e) * RECC + c] * k1;
     }
   }
 
@@ -1695,22 +1804,23 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
     char* Pb = Db + D_BYTES;
     const int r = rth + 16 * qq;
     const int off = coff + 8192 * qq;
-    u16x8 ph;
+    bf16x8 hv;
     if constexpr (RECC > 0) {
+      // H_0 = sin(fract(z_0)), z_0 in revolutions from the prescaled operands (fma chain over the
+      // inputs from the bias, the order of the forward's f32 MFMA)
       const float* xr = (const float*)(Pb + P_BYTES) + r * RECC;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float z = 0.f;
+        float z = b0r[e];
 #pragma unroll
         for (int c = 0; c < CR; ++c) z = fmaf(xr[c], w0r[e][c], z);
-        ph[e] = PT::encz(z, b0r[e], a.w0);
+        hv[e] = (bf16)__builtin_amdgcn_sinf(__builtin_amdgcn_fractf(z));
       }
     } else {
-      ph = *(const u16x8*)(Pb + off);
-    }
-    bf16x8 hv;
+      const u16x8 ph = *(const u16x8*)(Pb + off);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) hv[e] = (bf16)PT::sinp(ph[e]);
+      for (int e = 0; e < 8; ++e) hv[e] = (bf16)PT::sinp(ph[e]);
+    }
     *(bf16x8*)(Pb + off) = hv;
     if constexpr (TOPO > 0) {
       const float* gt = (const float*)(Pb + P_BYTES + X_BYTES) + r * TOPO;
@@ -1762,14 +1872,17 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
   }
   const uint32_t smem_lds = lds_addr(smem);
 
-  for (int s = 0; s < S - 1; ++s)
-    if (s < nchunk) dma(s, s);
+  const bool io = wave < NIO;
+  if (io)
+    for (int s = 0; s < S - 1; ++s)
+      if (s < nchunk) dma(s, s);
 
   // The convert pass of chunk k + 1 runs beside the MFMAs of chunk k (different slots); one
   // barrier per chunk. Slots in use at iteration k: k (MFMA), k + 1 (convert); DMAs k + 2, k + 3
   // in flight (issued two iterations ahead).
   if (nchunk > 0) {
-    if (nchunk >= 3) vm_wait<2 * NDMA>();
+    if (!io) {
+    } else if (nchunk >= 3) vm_wait<2 * NDMA>();
     else if (nchunk == 2) vm_wait<NDMA>();
     else vm_drain();
     lds_barrier();
@@ -1781,14 +1894,14 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
     const int st = (int)(k % S);
     const bool next = k + 1 < nchunk;
     // DMA(k + 1) landed (issued after it: DMA(k + 2), if any)
-    if (next) {
+    if (next && io) {
       if (k + 2 < nchunk) vm_wait<NDMA>();
       else vm_drain();
     }
     prof.tick(0);
     lds_barrier();  // convert(k) visible, DMA(k + 1) visible, MFMA(k - 1) done with slot k - 1
     prof.tick(1);
-    if (k + S - 1 < nchunk) dma(k + S - 1, (int)((k + S - 1) % S));
+    if (io && k + S - 1 < nchunk) dma(k + S - 1, (int)((k + S - 1) % S));
     prof.tick(2);
     const int stn = (int)((k + 1) % S);
     const uint32_t sb = smem_lds + st * STAGE;

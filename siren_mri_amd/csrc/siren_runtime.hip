@@ -13,7 +13,6 @@
 #include "siren_jvp.hip"
 #include "siren_fused.hip"
 #include "siren_fwdreg.hip"
-#include "siren_spair.hip"
 #include "siren_adam.hip"
 #include "siren_loss.hip"
 
@@ -85,7 +84,6 @@ bool g_ring_top = true;    // output layer folded into the top 256x256 layer's r
 bool g_bwd_ring = false;   // middle 256x256 layers in one ring kernel: measured slower (179 vs 145 us)
 bool g_fwd_pipe = true;    // fused forward: half-tile MFMA/VALU pipelined kernel
 bool g_fwd_reg = true;     // fused forward: activations resident in registers (siren_fwdreg.hip)
-bool g_spair = false;      // middle 256x256 layers: feature-split pair backward (siren_spair.hip; measured slower: 109-115 vs 102-104 us)
 bool g_dx_ring = true;     // 256x256 input-gradient layers on the 4-stage ring kernel
 bool g_dw_ring = true;     // 256x256 weight-gradient layers on the 4-stage ring kernel
 bool g_pair_ring = true;   // both gradients of a ring layer in one launch (pair_ring_bf16_kernel)
@@ -736,19 +734,7 @@ int launch_pair(const siren_mlp_desc* d, const Geo& g, const Layout& lo, int kin
   const dim3 grid((unsigned)(2 * npair), (unsigned)g.nb);
   const int kcls = kind == 1 ? SIREN_KCLASS_PAIR_RING : kind == 2 ? SIREN_KCLASS_PAIR_RING_TOP : SIREN_KCLASS_PAIR_RING_BOT;
   tmark_begin(kcls, st);
-  if (kind == 1 && g_spair && g_pair_roles == 3) {
-    SpairArgs sp;
-    sp.dZ = (const bf16*)(ws + lo.dz_off[cur]);
-    sp.P = (const uint16_t*)(saved + lo.saved_off[l - 1]);
-    sp.Wt = (const bf16*)(saved + lo.wt_op_off[l]);
-    sp.dZo = (bf16*)(ws + lo.dz_off[cur ^ 1]);
-    sp.part = part;
-    sp.split_stride = w.split_stride;
-    sp.rows_per_batch = g.rows;
-    sp.w_bstride = d->weights_batched ? (int64_t)M * N : 0;
-    sp.w0 = d->w0;
-    hipLaunchKernelGGL(spair_mid_kernel, grid, dim3(512), 0, st, sp);
-  } else if (kind == 1) {
+  if (kind == 1) {
     hipLaunchKernelGGL((pair_ring_bf16_kernel<0, false, false, 0, 0>), grid, dim3(512), 0, st, a, w);
   } else if (kind == 2) {
     if (O == 1) hipLaunchKernelGGL((pair_ring_bf16_kernel<0, false, false, 1, 0>), grid, dim3(512), 0, st, a, w);
@@ -1632,10 +1618,6 @@ int siren_config_set(const char* key, int64_t value) {
     g_fwd_reg = value != 0;
     return SIREN_OK;
   }
-  if (key && strcmp(key, "split_pair") == 0 && (value == 0 || value == 1)) {
-    g_spair = value != 0;
-    return SIREN_OK;
-  }
   if (key && strcmp(key, "bwd_ring") == 0 && (value == 0 || value == 1)) {
     g_bwd_ring = value != 0;
     return SIREN_OK;
@@ -1683,7 +1665,6 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "pair_ring") == 0) return g_pair_ring ? 1 : 0;
   if (key && strcmp(key, "fused_forward_pipe") == 0) return g_fwd_pipe ? 1 : 0;
   if (key && strcmp(key, "fused_forward_reg") == 0) return g_fwd_reg ? 1 : 0;
-  if (key && strcmp(key, "split_pair") == 0) return g_spair ? 1 : 0;
   return -1;
 }
 

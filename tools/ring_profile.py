@@ -17,6 +17,7 @@ from siren_mri_amd import _native  # noqa: E402
 NPROF = 6
 DX_SEG = ["vm_wait", "barrier", "dma issue", "mfma+epi1", "barrier2", "epi2 stores"]
 DW_SEG = ["vm_wait", "barrier", "dma issue", "mfma+convert", "-", "-"]
+BOT_SEG = ["vm_wait", "barrier", "dma+dx store", "late epi", "mfma", "epi"]
 
 
 def main():
@@ -41,13 +42,14 @@ def main():
         if blk.abs().sum() == 0:
             continue
         role = torch.tensor([(b >> 3) & 1 for b in range(256)])
-        for r, segs in ((0, DX_SEG), (1, DW_SEG)):
+        for r, segs in ((0, DX_SEG if li < 2 else BOT_SEG), (1, DW_SEG)):
             sel = blk[role == r]  # [128, 8, NPROF]
-            m = sel.mean(dim=(0, 1))
-            tot = m.sum().item()
-            parts = "  ".join(f"{segs[k]} {m[k].item():8.0f} ({100 * m[k].item() / max(tot, 1):4.1f}%)"
-                              for k in range(NPROF) if segs[k] != "-")
-            print(f"{names[li]:12s} {'dx' if r == 0 else 'dw'}: total {tot:9.0f} cyc | {parts}", flush=True)
+            for wl, ws in (("w0-7", slice(0, 8)), ("w0-3", slice(0, 4)), ("w4-7", slice(4, 8))):
+                m = sel[:, ws].mean(dim=(0, 1))
+                tot = m.sum().item()
+                parts = "  ".join(f"{segs[k]} {m[k].item():7.0f} ({100 * m[k].item() / max(tot, 1):4.1f}%)"
+                                  for k in range(NPROF) if segs[k] != "-")
+                print(f"{names[li]:12s} {'dx' if r == 0 else 'dw'} {wl}: total {tot:9.0f} | {parts}", flush=True)
 
 
 if __name__ == "__main__":
