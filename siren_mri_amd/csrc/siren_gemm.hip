@@ -2014,7 +2014,7 @@ __global__ __launch_bounds__(512) void dw_ring_bf16_kernel(TNArgs a) {
 // gridDim.x = 2 * npair, a multiple of 16.
 // ------------------------------------------------------------------------------------------
 template <int BOTC, bool DXOUT, bool REC, int TOPO, int RECC>
-__global__ __launch_bounds__(512) void pair_ring_bf16_kernel(NTArgs ax, TNArgs aw) {
+__global__ __launch_bounds__(512) void pair_ring_bf16_kernel(NTArgs ax, TNArgs aw, ReduceMultiArgs prev) {
   constexpr int LX = dx_ring_lds_bytes<BOTC, TOPO>(), LW = dw_ring_lds_bytes<RECC, TOPO>();
   __shared__ __attribute__((aligned(16))) char smem[LX > LW ? LX : LW];
   const int b = blockIdx.x;
@@ -2027,9 +2027,18 @@ __global__ __launch_bounds__(512) void pair_ring_bf16_kernel(NTArgs ax, TNArgs a
     if (!(aw.pair_roles & 1)) return;
     dx_ring_body<BOTC, DXOUT, REC, TOPO>(ax, smem, tb, 1, te - tb, pair);
   } else {
-    if (!(aw.pair_roles & 2)) return;
     const int64_t r_end = te * RING_BM < rows ? te * RING_BM : rows;
-    dw_ring_body<RECC, TOPO>(aw, smem, tb * RING_BM, r_end, pair);
+    if (aw.pair_roles & 2) dw_ring_body<RECC, TOPO>(aw, smem, tb * RING_BM, r_end, pair);
+    // tail: the previous pair launch's slab reduction (this role finishes ahead of the
+    // input-gradient role), 128-float blocks dealt over the weight-gradient workgroups, two
+    // 256-thread groups each; reduce_multi_kernel's block body and summation order
+    if (prev.nseg > 0) {
+      __syncthreads();
+      f32x4(*red)[32] = (f32x4(*)[32])(smem + (threadIdx.x >> 8) * (8 * 32 * 16));
+      const int nblk = reduce_total_blocks(prev);
+      const int wg = (int)(pair + npair * blockIdx.y), per = (int)(2 * npair * gridDim.y);
+      for (int k = 0; k * per < nblk; ++k) reduce_block(prev, k * per + 2 * wg + (threadIdx.x >> 8), threadIdx.x & 255, red);
+    }
   }
 }
 

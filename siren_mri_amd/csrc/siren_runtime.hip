@@ -88,6 +88,7 @@ bool g_dx_ring = true;     // 256x256 input-gradient layers on the 4-stage ring 
 bool g_dw_ring = true;     // 256x256 weight-gradient layers on the 4-stage ring kernel
 bool g_pair_ring = true;   // both gradients of a ring layer in one launch (pair_ring_bf16_kernel)
 int g_pair_roles = 3;      // debug timing: which pair_ring roles run (results are wrong unless 3)
+bool g_tail_reduce = true;  // a pair launch reduces the previous pair launch's slabs (no reduce launch)
 long long* g_ring_prof = nullptr;   // debug: pair_ring segment cycle counters, one block per launch
 int g_ring_prof_n = 0;
 long long* g_fused_prof = nullptr;
@@ -173,6 +174,7 @@ struct Layout {
   int64_t part_off;
   int64_t partL_off;      // output-layer partial slabs of the fused top backward layer
   int64_t partB_off;      // first-layer partial slabs of the paired bottom layer (P_0 recompute)
+  int64_t part2_off;      // second slab buffer of consecutive pair launches (-1: none)
   int64_t xcopy_off;      // 16-byte aligned copy of x (P_0 recompute with a misaligned x)
   bool p0_rec;
   int64_t ws_bytes;
@@ -264,6 +266,13 @@ Layout layout_of(const siren_mlp_desc* d) {
   if (lo.p0_rec) off = align_up(off + kMaxPairs * split_stride(g, (int64_t)d->dims[1] * d->dims[0] + d->dims[1]) * 4, 256);
   lo.xcopy_off = off;
   if (lo.p0_rec) off = align_up(off + g.total * d->dims[0] * 4, 256);
+  // paired 256x256 layers alternate between part and part2: a pair launch reduces the previous
+  // one's slabs in its weight-gradient role's tail (pair_ring_bf16_kernel)
+  lo.part2_off = -1;
+  if (fused_shape(d) && g.L >= 4) {
+    lo.part2_off = off;
+    off = align_up(off + pair_count(g) * split_stride(g, (int64_t)256 * 256 + 256) * 4, 256);
+  }
   lo.ws_bytes = off;
   return lo;
 }
@@ -684,7 +693,7 @@ int forward_impl(const siren_mlp_desc* d, const float* x, float* y, char* saved,
 template <int PREC>
 int launch_pair(const siren_mlp_desc* d, const Geo& g, const Layout& lo, int kind, int l, const float* x,
                 const TopArgs& ta, char* ws, const char* saved, float* part, float* const* dW, float* const* db,
-                float* dx, int cur, hipStream_t st) {
+                float* dx, int cur, ReduceList& pend, hipStream_t st) {
   const int M = d->dims[l + 1], N = d->dims[l], C = d->dims[0], F0 = d->dims[1], O = d->dims[g.L];
   const int64_t npair = pair_count(g);
   TNArgs w;
@@ -734,15 +743,16 @@ int launch_pair(const siren_mlp_desc* d, const Geo& g, const Layout& lo, int kin
   const dim3 grid((unsigned)(2 * npair), (unsigned)g.nb);
   const int kcls = kind == 1 ? SIREN_KCLASS_PAIR_RING : kind == 2 ? SIREN_KCLASS_PAIR_RING_TOP : SIREN_KCLASS_PAIR_RING_BOT;
   tmark_begin(kcls, st);
+  const ReduceMultiArgs prev = pend.a;  // the previous pair launch's slabs, reduced in this one's tail
   if (kind == 1) {
-    hipLaunchKernelGGL((pair_ring_bf16_kernel<0, false, false, 0, 0>), grid, dim3(512), 0, st, a, w);
+    hipLaunchKernelGGL((pair_ring_bf16_kernel<0, false, false, 0, 0>), grid, dim3(512), 0, st, a, w, prev);
   } else if (kind == 2) {
-    if (O == 1) hipLaunchKernelGGL((pair_ring_bf16_kernel<0, false, false, 1, 0>), grid, dim3(512), 0, st, a, w);
-    else hipLaunchKernelGGL((pair_ring_bf16_kernel<0, false, false, 2, 0>), grid, dim3(512), 0, st, a, w);
+    if (O == 1) hipLaunchKernelGGL((pair_ring_bf16_kernel<0, false, false, 1, 0>), grid, dim3(512), 0, st, a, w, prev);
+    else hipLaunchKernelGGL((pair_ring_bf16_kernel<0, false, false, 2, 0>), grid, dim3(512), 0, st, a, w, prev);
   } else {
-#define SIREN_PAIR_BOT(CC)                                                                                   \
-  if (dx) hipLaunchKernelGGL((pair_ring_bf16_kernel<CC, true, true, 0, CC>), grid, dim3(512), 0, st, a, w);   \
-  else hipLaunchKernelGGL((pair_ring_bf16_kernel<CC, false, true, 0, CC>), grid, dim3(512), 0, st, a, w);
+#define SIREN_PAIR_BOT(CC)                                                                                         \
+  if (dx) hipLaunchKernelGGL((pair_ring_bf16_kernel<CC, true, true, 0, CC>), grid, dim3(512), 0, st, a, w, prev);   \
+  else hipLaunchKernelGGL((pair_ring_bf16_kernel<CC, false, true, 0, CC>), grid, dim3(512), 0, st, a, w, prev);
     switch (C) {
       case 1: SIREN_PAIR_BOT(1) break;
       case 2: SIREN_PAIR_BOT(2) break;
@@ -754,11 +764,13 @@ int launch_pair(const siren_mlp_desc* d, const Geo& g, const Layout& lo, int kin
   tmark_end(kcls, st);
   int rc = check_launch("pair_ring");
   if (rc) return rc;
+  // this launch's slabs: reduced by the next pair launch, or by a reduce_multi launch (flush)
   ReduceList red;
   red.add(part, npair, w.split_stride, g.nb, (int64_t)M * N + M, (int64_t)M * N, dW[l], db[l]);
   if (kind == 2) red.add(ta.partL, npair, ta.partL_stride, g.nb, (int64_t)O * M + O, (int64_t)O * M, dW[g.L - 1], db[g.L - 1]);
   if (kind == 3) red.add(a.bot.part, npair, bot_stride, g.nb, (int64_t)F0 * C + F0, (int64_t)F0 * C, dW[0], db[0]);
-  return red.launch(st);
+  pend = red;
+  return SIREN_OK;
 }
 
 template <int PREC>
@@ -770,6 +782,14 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
   float* part = (float*)(ws + lo.part_off);
   auto P = [&](int l) -> const void* { return saved + lo.saved_off[l]; };
   const int O = d->dims[g.L], C = d->dims[0], F0 = d->dims[1];
+  // slab reduction of the last pair launch, not yet issued (see launch_pair)
+  ReduceList pend;
+  int npair_launches = 0;
+  auto flush = [&]() -> int {
+    const int r = pend.launch(st);
+    pend = ReduceList();
+    return r;
+  };
   // bf16-mode fusions (siren_gemm.hip TopArgs / BotArgs): the output layer's backward folds into
   // the top hidden layer's kernels, the first layer's weight gradient into the bottom one's.
   const bool fuse = PREC == kPrecBF16 && g_fused_backward && g.L >= 3;
@@ -854,6 +874,7 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
       b.split_stride = split_stride(g, (int64_t)M * N + M);
       b.w_bstride = d->weights_batched ? (int64_t)M * N : 0;
       b.w0 = d->w0;
+      if ((rc = flush())) return rc;
       tmark_begin(SIREN_KCLASS_BWD_FUSED, st);
       hipLaunchKernelGGL(bwd_ring_bf16_kernel, dim3((unsigned)s.nsplit, (unsigned)g.nb), dim3(256), 0, st, b);
       tmark_end(SIREN_KCLASS_BWD_FUSED, st);
@@ -873,12 +894,22 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
                        : (!is_top && !is_bot && !rec1 && g_dw_ring && g_dx_ring) ? 1
                                                                            : 0;
       if (kind) {
-        if ((rc = launch_pair<PREC>(d, g, lo, kind, l, x, ta, ws, saved, part, dW, db, dx, cur, st))) return rc;
-        if (kind == 3) return SIREN_OK;  // first layer done
+        // consecutive pair launches alternate slab buffers (the pending reduction reads the other
+        // one); without a second buffer the pending reduction goes first
+        float* pp = part;
+        if (!g_tail_reduce && (rc = flush())) return rc;
+        if (lo.part2_off >= 0) {
+          if (npair_launches++ & 1) pp = (float*)(ws + lo.part2_off);
+        } else if ((rc = flush())) {
+          return rc;
+        }
+        if ((rc = launch_pair<PREC>(d, g, lo, kind, l, x, ta, ws, saved, pp, dW, db, dx, cur, pend, st))) return rc;
+        if (kind == 3) return flush();  // first layer done
         cur ^= 1;
         continue;
       }
     }
+    if ((rc = flush())) return rc;  // the per-layer kernels below reuse `part`
     const bool ring = rec1 || ring_t || (PREC == kPrecBF16 && g_dw_ring && !is_top && M == 256 && N == 256);
     {
       const Split s = ring ? dw_ring_split(g) : tn_split(g, M, N);
@@ -992,6 +1023,7 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
       cur ^= 1;
     }
   }
+  if ((rc = flush())) return rc;
   // First layer.
   if (wide_input(d)) {
     const int F0 = d->dims[1], C = d->dims[0];
@@ -1634,6 +1666,10 @@ int siren_config_set(const char* key, int64_t value) {
     g_pair_roles = (int)value;
     return SIREN_OK;
   }
+  if (key && strcmp(key, "pair_tail_reduce") == 0 && (value == 0 || value == 1)) {
+    g_tail_reduce = value != 0;
+    return SIREN_OK;
+  }
   if (key && strcmp(key, "pair_ring") == 0 && (value == 0 || value == 1)) {
     g_pair_ring = value != 0;
     return SIREN_OK;
@@ -1662,6 +1698,7 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "dx_ring") == 0) return g_dx_ring ? 1 : 0;
   if (key && strcmp(key, "dw_ring") == 0) return g_dw_ring ? 1 : 0;
   if (key && strcmp(key, "bwd_ring") == 0) return g_bwd_ring ? 1 : 0;
+  if (key && strcmp(key, "pair_tail_reduce") == 0) return g_tail_reduce ? 1 : 0;
   if (key && strcmp(key, "pair_ring") == 0) return g_pair_ring ? 1 : 0;
   if (key && strcmp(key, "fused_forward_pipe") == 0) return g_fwd_pipe ? 1 : 0;
   if (key && strcmp(key, "fused_forward_reg") == 0) return g_fwd_reg ? 1 : 0;

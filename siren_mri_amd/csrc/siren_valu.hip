@@ -534,12 +534,19 @@ struct ReduceMultiArgs {
   ReduceSeg seg[REDUCE_MAXSEG];
   int nseg;
 };
-__global__ __launch_bounds__(256) void reduce_multi_kernel(ReduceMultiArgs a) {
-  __shared__ f32x4 red[8][32];
-  int blk = blockIdx.x, si = 0;
+// One 128-float block of a segmented slab reduction (256 threads t = threadIdx.x - t0; red: this
+// group's 8 x 32 f32x4 of LDS). Shared by reduce_multi_kernel and the tail of the next paired
+// backward launch (pair_ring_bf16_kernel), so both sum in the same order.
+DEV int reduce_total_blocks(const ReduceMultiArgs& a) {
+  int n = 0;
+  for (int i = 0; i < a.nseg; ++i) n += a.seg[i].blocks;
+  return n;
+}
+DEV void reduce_block(const ReduceMultiArgs& a, int blk, int t, f32x4 (*red)[32]) {
+  int si = 0;
   while (si + 1 < a.nseg && blk >= a.seg[si].blocks) blk -= a.seg[si++].blocks;
   const ReduceSeg& g = a.seg[si];
-  const int c4 = threadIdx.x & 31, sl = threadIdx.x >> 5;
+  const int c4 = t & 31, sl = t >> 5;
   const int base = (blk * 32 + c4) * 4;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (base < g.total) {
@@ -556,18 +563,24 @@ __global__ __launch_bounds__(256) void reduce_multi_kernel(ReduceMultiArgs a) {
   red[sl][c4] = acc;
   __syncthreads();
   if (sl == 0 && base < g.total) {
-    f32x4 t = red[0][c4];
+    f32x4 v = red[0][c4];
 #pragma unroll
-    for (int k = 1; k < 8; ++k) t += red[k][c4];
+    for (int k = 1; k < 8; ++k) v += red[k][c4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int idx = base + e;
       if (idx >= g.total) break;
       const int b = idx / g.slab, r = idx - b * g.slab;
-      if (r < g.n_first) g.out0[(int64_t)b * g.n_first + r] = t[e];
-      else g.out1[(int64_t)b * (g.slab - g.n_first) + (r - g.n_first)] = t[e];
+      if (r < g.n_first) g.out0[(int64_t)b * g.n_first + r] = v[e];
+      else g.out1[(int64_t)b * (g.slab - g.n_first) + (r - g.n_first)] = v[e];
     }
   }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void reduce_multi_kernel(ReduceMultiArgs a) {
+  __shared__ f32x4 red[8][32];
+  reduce_block(a, blockIdx.x, threadIdx.x, red);
 }
 
 // ------------------------------------------------------------------------------------------
