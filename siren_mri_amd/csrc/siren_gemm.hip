@@ -1326,32 +1326,12 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
     }
   };
 
-  // (An in-wave software pipeline — tile i's MFMAs beside tile i - 1's epilogue — measured
-  // slower: the two waves of a SIMD already overlap one's MFMAs with the other's epilogue.)
-  const bool io = wave < NIO;
-  if (io)
-    for (int s = 0; s < S - 1; ++s)
-      if (s < niter) dma(t0 + s * G, s);
-
-  RingProf prof(a.prof);
-  for (int64_t i = 0; i < niter; ++i) {
-    const int st = (int)(i % S);
-    const int64_t t = t0 + i * G;
-    // this stage's DMA (this wave's part) landed; then every wave's part, and every wave is done
-    // with the stage the next DMA overwrites (tile i - 1: MFMA reads and its store pass)
-    if (io) {
-      if (i >= S - 1 && i + S - 2 < niter) vm_wait<STEADY>();
-      else vm_drain();
-    }
-    prof.tick(0);
-    lds_barrier();
-    prof.tick(1);
-    // (issuing these pieces between the MFMAs instead measured slower)
-    if (io && i + S - 1 < niter) dma(t0 + (i + S - 1) * G, (int)((i + S - 1) % S));
-    prof.tick(2);
-    char* base = smem + st * STAGE;
+  // TOPO: dZ_top = (dy W_L) cos(P_top) w0 over the staged phases of slot st, in place
+  // (last_bwd's arithmetic); run for tile i + 1 right after tile i's MFMAs, so no barrier
+  // separates it from the MFMAs that read it (the next iteration's barrier publishes it)
+  auto top_pass = [&](int st) {
     if constexpr (TOPO > 0) {
-      // dZ_top = (dy W_L) cos(P_top) w0 over the staged phases, in place (last_bwd's arithmetic)
+      char* base = smem + st * STAGE;
       const float* gt = (const float*)(base + A_BYTES + C_BYTES);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -1372,11 +1352,54 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
         }
         *(bf16x8*)pp = v;
       }
-      lds_barrier();
     }
+  };
+  // TOPO: iteration i waits for DMA(i + 1) (its pass runs in iteration i); issued in iteration
+  // i + 2 - S, then followed by the stores of S - 2 iterations and S - 3 DMAs
+  constexpr int STEADY_T = (S - 2) * NST + (S - 3) * NDMA;
+
+  // (An in-wave software pipeline — tile i's MFMAs beside tile i - 1's epilogue — measured
+  // slower: the two waves of a SIMD already overlap one's MFMAs with the other's epilogue.)
+  const bool io = wave < NIO;
+  if (io)
+    for (int s = 0; s < S - 1; ++s)
+      if (s < niter) dma(t0 + s * G, s);
+  if constexpr (TOPO > 0) {
+    if (io) vm_drain();
+    lds_barrier();
+    if (niter > 0) top_pass(0);
+  }
+
+  RingProf prof(a.prof);
+  for (int64_t i = 0; i < niter; ++i) {
+    const int st = (int)(i % S);
+    const int64_t t = t0 + i * G;
+    // this stage's DMA (this wave's part) landed; then every wave's part, and every wave is done
+    // with the stage the next DMA overwrites (tile i - 1: MFMA reads and its store pass)
+    if (io) {
+      if constexpr (TOPO > 0) {
+        if (i + 1 < niter) {
+          if (i >= S - 2 && i + S - 2 < niter) vm_wait<STEADY_T>();
+          else vm_drain();
+        }
+      } else {
+        if (i >= S - 1 && i + S - 2 < niter) vm_wait<STEADY>();
+        else vm_drain();
+      }
+    }
+    prof.tick(0);
+    lds_barrier();
+    prof.tick(1);
+    // (issuing these pieces between the MFMAs instead measured slower)
+    if (io && i + S - 1 < niter) dma(t0 + (i + S - 1) * G, (int)((i + S - 1) % S));
+    prof.tick(2);
+    char* base = smem + st * STAGE;
     // dZ_{l-1}^T (32 features x 32 rows) = W^T slice . dZ_l^T: B fragments = dZ rows from LDS
     const f32x16 acc = ring_chain(wf, lds_addr(base), boff0);
     prof.tick(3);
+    if constexpr (TOPO > 0) {
+      if (i + 1 < niter) top_pass((int)((i + 1) % S));
+    }
     epilogue(t, st, acc);
     prof.tick(5);
   }
