@@ -221,6 +221,9 @@ int siren_sse_backward(const float* d, const float* mask, int64_t n, int64_t mas
  *   "pair_ring"      1 (default): a 256x256 bf16 layer whose two gradients both run on the ring
  *                    kernels computes them in ONE launch, on co-scheduled workgroup pairs that
  *                    stream the same tiles (one HBM read of dZ and P per pair); 0: two launches.
+ *   "pair_tail_reduce"  1 (default): a pair launch's weight-gradient workgroups also reduce the
+ *                    previous pair launch's split-K slabs after their own rows (two slab buffers
+ *                    alternate); 0: every pair launch is followed by a reduce_multi launch.
  *   "debug_pair_roles"  3 (default); 1 / 2 run only the input- / weight-gradient role of
  *                    pair_ring_bf16_kernel (timing experiments only: the gradients are then wrong).
  *   "debug_fused_profile"  device address of an int64 buffer [grid][4] that receives per-
