@@ -221,6 +221,9 @@ int siren_sse_backward(const float* d, const float* mask, int64_t n, int64_t mas
  *   "pair_ring"      1 (default): a 256x256 bf16 layer whose two gradients both run on the ring
  *                    kernels computes them in ONE launch, on co-scheduled workgroup pairs that
  *                    stream the same tiles (one HBM read of dZ and P per pair); 0: two launches.
+ *   "dx_stagger"     0 (default); 1: the middle/top input-gradient ring runs waves 4-7 one tile
+ *                    late (epilogue from registers through a private staging tile; bit-identical,
+ *                    measured 5-9 us/step slower).
  *   "pair_tail_reduce"  1 (default): a pair launch's weight-gradient workgroups also reduce the
  *                    previous pair launch's split-K slabs after their own rows (two slab buffers
  *                    alternate); 0: every pair launch is followed by a reduce_multi launch.

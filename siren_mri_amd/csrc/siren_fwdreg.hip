@@ -44,6 +44,10 @@ constexpr int FREG_WL_BYTES = 4096; // output-layer fragments, rows 0..7 only: [
 #define SIREN_FREG_SYNC 2
 #endif
 constexpr int FREG_SYNC = SIREN_FREG_SYNC;
+// cache-policy bits of the phase-code stores (timing experiments: 2 = nt)
+#ifndef SIREN_FREG_STORE_AUX
+#define SIREN_FREG_STORE_AUX 0
+#endif
 static_assert(FREG_SYNC == 1 || FREG_SYNC == 2, "ring sync interval");
 // Vector-memory operations a wave has issued after the ring refill it must see land (every block
 // issues two phase stores — a null tensor's are still issued and dropped by their resource — and
@@ -52,7 +56,11 @@ static_assert(FREG_SYNC == 1 || FREG_SYNC == 2, "ring sync interval");
 //                1 + 2 x 5 (refills) + 2 x 6 (stores) = 23 are younger;
 //   FREG_SYNC 2: the slot read by block k + 2 was refilled (first of two slots) at the barrier of
 //                block k - 4: at least 1 + 2 + 4 (refills) + 2 x 4 (stores) = 15 are younger.
-#if SIREN_FREG_SYNC == 1
+#ifdef SIREN_FREG_VMN  // timing experiments only: a looser wait (reads may see unlanded slots)
+#define SIREN_FREG_STR2(x) #x
+#define SIREN_FREG_STR(x) SIREN_FREG_STR2(x)
+#define SIREN_FREG_VMWAIT "s_waitcnt vmcnt(" SIREN_FREG_STR(SIREN_FREG_VMN) ")"
+#elif SIREN_FREG_SYNC == 1
 #define SIREN_FREG_VMWAIT "s_waitcnt vmcnt(22)"
 #else
 #define SIREN_FREG_VMWAIT "s_waitcnt vmcnt(15)"
@@ -257,7 +265,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
       __builtin_amdgcn_raw_buffer_store_b128(c, p_rsrc(pl), wave * 16384 + lane * 16, (pfb * 2 + half) * 1024, 0);
       return;
     }
-    __builtin_amdgcn_raw_buffer_store_b128(c, p_rsrc(pl), p_voff, pfb * 64 + half * 32, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(c, p_rsrc(pl), p_voff, pfb * 64 + half * 32, SIREN_FREG_STORE_AUX);
   };
 
   // Epilogue of one accumulator, in 8 parts of 2 elements (part p: elements 2p, 2p + 1, packed

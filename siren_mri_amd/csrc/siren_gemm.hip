@@ -70,6 +70,7 @@ struct NTArgs {
   TopArgs top;         // DX with TOP
   BotArgs bot;         // DX with BOT
   long long* prof;     // debug: [grid.x][8 waves][RING_NPROF] segment cycle counters (null: off)
+  int stagger;         // dx_ring_body_v2: waves 4-7 run each epilogue one tile late (option dx_stagger)
 };
 
 // Largest power-of-two divisor of the 16-byte chunks per row, capped at 16, minus one: the XOR
@@ -917,9 +918,12 @@ DEV f32x16 ring_chain(const bf16x8 (&wf)[16], uint32_t sbase, uint32_t off0) {
 // TOPO > 0 (top hidden layer, outermost_linear, O = TOPO outputs): the A operand dZ_top is not
 // read; the ring carries P_top (in the A image) and the dy tile, and a pass forms
 // dZ_top = (dy W_L) cos(P_top) w0 in place exactly as last_bwd_kernel does.
+// (BOTC == 0: plus the staggered half's private store staging, 4 waves x 32 rows x 80 B)
+constexpr int DX_STAGE_ROW = 80;
 template <int BOTC, int TOPO>
 constexpr int dx_ring_lds_bytes() {
-  return RING_S * (RING_BM * 256 * 2 * 2 + (BOTC > 0 ? RING_BM * BOTC * 4 : 0) + (TOPO > 0 ? RING_BM * TOPO * 4 : 0));
+  return RING_S * (RING_BM * 256 * 2 * 2 + (BOTC > 0 ? RING_BM * BOTC * 4 : 0) + (TOPO > 0 ? RING_BM * TOPO * 4 : 0)) +
+         (BOTC == 0 ? 4 * RING_BM * DX_STAGE_ROW : 0);
 }
 
 // The tiles of one workgroup: t = t0 + i * G for i < niter; `slab` indexes the BOTC first-layer
@@ -1210,7 +1214,7 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
   constexpr int K = 256, N = 256, BM = RING_BM, S = RING_S;
   constexpr int G_BYTES = TOPO > 0 ? BM * TOPO * 4 : 0;
   constexpr int A_BYTES = BM * K * 2, C_BYTES = BM * N * 2, STAGE = A_BYTES + C_BYTES + G_BYTES;
-  static_assert(S * STAGE == dx_ring_lds_bytes<0, TOPO>(), "dx_ring LDS size");
+  static_assert(S * STAGE + 4 * BM * DX_STAGE_ROW == dx_ring_lds_bytes<0, TOPO>(), "dx_ring LDS size");
   constexpr int NKS = K / 16;
   // the ring's DMA is issued by waves 0..NIO-1 only (4 dZ + 4 P pieces each): waves 4-7 lose the
   // VALU/MFMA arbitration to their SIMD partners, and the issue cost lands where the barrier
@@ -1269,6 +1273,8 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
     goff[j] = r * 512 + 16 * c;
   }
 
+  // late half (waves 4-7): private staging of the wave's 32 x 32 output tile, rows of 80 B
+  char* stg = smem + S * STAGE + (wave & 3) * BM * DX_STAGE_ROW;
   auto nval = [&](int64_t t) -> int64_t {
     const int64_t n = rows - t * BM;
     return n < BM ? n : BM;
@@ -1358,8 +1364,27 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
   // i + 2 - S, then followed by the stores of S - 2 iterations and S - 3 DMAs
   constexpr int STEADY_T = (S - 2) * NST + (S - 3) * NDMA;
 
-  // (An in-wave software pipeline — tile i's MFMAs beside tile i - 1's epilogue — measured
-  // slower: the two waves of a SIMD already overlap one's MFMAs with the other's epilogue.)
+  // late half: the epilogue of tile t from registers (its accumulator and the 16 phases read
+  // before the stage was recycled), staged privately, then the same two 16-byte stores per lane
+  auto late_epilogue = [&](int64_t t, const f32x16& acc, const u16x4 (&ph)[4]) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (bf16)((acc[4 * g + e] * PT::cosp(ph[g][e])) * a.w0);
+      *(bf16x4*)(stg + r32 * DX_STAGE_ROW + 16 * g + 8 * h) = v;
+    }
+    const __amdgpu_buffer_rsrc_t rC = make_rsrc((const bf16*)a.C + (rowbase + t * BM) * N, nval(t) * N * 2);
+#pragma unroll
+    for (int j = 0; j < NST; ++j) {
+      const int qd = lane + 64 * j;
+      const u32x4_t v = *(const u32x4_t*)(stg + (qd >> 2) * DX_STAGE_ROW + 16 * (qd & 3));
+      __builtin_amdgcn_raw_buffer_store_b128(v, rC, goff[j], 0, 0);
+    }
+  };
+
+  // Stagger (as dx_ring_body_v2bot): waves 4-7 run each tile's epilogue one tile late, from
+  // registers, so on every SIMD one wave's MFMA chain runs beside its partner's epilogue.
   const bool io = wave < NIO;
   if (io)
     for (int s = 0; s < S - 1; ++s)
@@ -1370,40 +1395,59 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
     if (niter > 0) top_pass(0);
   }
 
-  RingProf prof(a.prof);
-  for (int64_t i = 0; i < niter; ++i) {
-    const int st = (int)(i % S);
-    const int64_t t = t0 + i * G;
-    // this stage's DMA (this wave's part) landed; then every wave's part, and every wave is done
-    // with the stage the next DMA overwrites (tile i - 1: MFMA reads and its store pass)
-    if (io) {
-      if constexpr (TOPO > 0) {
-        if (i + 1 < niter) {
-          if (i >= S - 2 && i + S - 2 < niter) vm_wait<STEADY_T>();
+  auto loop = [&](auto late_tag) {
+    constexpr bool LATE = decltype(late_tag)::value;
+    f32x16 accp;
+    u16x4 php[4];
+    RingProf prof(a.prof);
+    for (int64_t i = 0; i < niter; ++i) {
+      const int st = (int)(i % S);
+      const int64_t t = t0 + i * G;
+      // this stage's DMA (this wave's part) landed; then every wave's part, and every wave is done
+      // with the stage the next DMA overwrites (tile i - 1: MFMA reads and its store pass)
+      if (io) {
+        if constexpr (TOPO > 0) {
+          if (i + 1 < niter) {
+            if (i >= S - 2 && i + S - 2 < niter) vm_wait<STEADY_T>();
+            else vm_drain();
+          }
+        } else {
+          if (i >= S - 1 && i + S - 2 < niter) vm_wait<STEADY>();
           else vm_drain();
         }
-      } else {
-        if (i >= S - 1 && i + S - 2 < niter) vm_wait<STEADY>();
-        else vm_drain();
       }
+      prof.tick(0);
+      lds_barrier();
+      prof.tick(1);
+      // (issuing these pieces between the MFMAs instead measured slower)
+      if (io && i + S - 1 < niter) dma(t0 + (i + S - 1) * G, (int)((i + S - 1) % S));
+      if constexpr (LATE) {
+        if (i > 0) late_epilogue(t - G, accp, php);
+      }
+      prof.tick(2);
+      char* base = smem + st * STAGE;
+      // dZ_{l-1}^T (32 features x 32 rows) = W^T slice . dZ_l^T: B fragments = dZ rows from LDS
+      const f32x16 acc = ring_chain(wf, lds_addr(base), boff0);
+      prof.tick(3);
+      if constexpr (TOPO > 0) {
+        if (i + 1 < niter) top_pass((int)((i + 1) % S));
+      }
+      if constexpr (LATE) {
+        accp = acc;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) php[g] = *(const u16x4*)(base + eoff[g]);
+      } else {
+        epilogue(t, st, acc);
+      }
+      prof.tick(5);
     }
-    prof.tick(0);
-    lds_barrier();
-    prof.tick(1);
-    // (issuing these pieces between the MFMAs instead measured slower)
-    if (io && i + S - 1 < niter) dma(t0 + (i + S - 1) * G, (int)((i + S - 1) % S));
-    prof.tick(2);
-    char* base = smem + st * STAGE;
-    // dZ_{l-1}^T (32 features x 32 rows) = W^T slice . dZ_l^T: B fragments = dZ rows from LDS
-    const f32x16 acc = ring_chain(wf, lds_addr(base), boff0);
-    prof.tick(3);
-    if constexpr (TOPO > 0) {
-      if (i + 1 < niter) top_pass((int)((i + 1) % S));
+    if constexpr (LATE) {
+      if (niter > 0) late_epilogue(t0 + (niter - 1) * G, accp, php);
     }
-    epilogue(t, st, acc);
-    prof.tick(5);
-  }
-  prof.flush(blockIdx.x);
+    prof.flush(blockIdx.x);
+  };
+  if (a.stagger && wave >= 4) loop(std::true_type{});
+  else loop(std::false_type{});
 }
 
 // dx_ring body of the bottom hidden layer with the first layer folded in and P_0 rebuilt from x

@@ -88,6 +88,7 @@ bool g_dx_ring = true;     // 256x256 input-gradient layers on the 4-stage ring 
 bool g_dw_ring = true;     // 256x256 weight-gradient layers on the 4-stage ring kernel
 bool g_pair_ring = true;   // both gradients of a ring layer in one launch (pair_ring_bf16_kernel)
 int g_pair_roles = 3;      // debug timing: which pair_ring roles run (results are wrong unless 3)
+bool g_dx_stagger = false;  // middle/top input-gradient ring: staggered wave halves (measured slower: +5-9 us/step)
 bool g_tail_reduce = true;  // a pair launch reduces the previous pair launch's slabs (no reduce launch)
 long long* g_ring_prof = nullptr;   // debug: pair_ring segment cycle counters, one block per launch
 int g_ring_prof_n = 0;
@@ -724,6 +725,7 @@ int launch_pair(const siren_mlp_desc* d, const Geo& g, const Layout& lo, int kin
   a.w0 = d->w0;
   a.top = ta;
   a.prof = w.prof;
+  a.stagger = g_dx_stagger ? 1 : 0;
   const int64_t bot_stride = split_stride(g, (int64_t)F0 * C + F0);
   if (kind == 3) {
     w.rec_W0 = d->weight[0];
@@ -984,6 +986,7 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
       a.a_vec = 0;
       a.w0 = d->w0;
       a.top = ta;
+      a.stagger = g_dx_stagger ? 1 : 0;
       const int64_t bot_stride = split_stride(g, (int64_t)F0 * C + F0);
       if (is_bot) {
         a.bot.x = x;
@@ -1570,7 +1573,9 @@ int siren_sse_forward(const float* pred, const float* tgt, const float* mask, in
   a.n = n;
   a.mask_n = mask ? mask_n : 1;
   a.weight = weight;
-  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(SSE_MAX_BLOCKS, cdiv(n, 4 * SSE_THREADS)));
+  // 16 elements per thread: few enough blocks that the hand-off counter (one agent-scope add per
+  // block, all on one address) stays off the critical path (262144 elements: 64 blocks)
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(SSE_MAX_BLOCKS, cdiv(n, 16 * SSE_THREADS)));
   hipLaunchKernelGGL(sse_fwd_kernel, dim3(blocks), dim3(SSE_THREADS), 0, (hipStream_t)stream, a);
   return check_launch("sse_forward");
 }
@@ -1666,6 +1671,10 @@ int siren_config_set(const char* key, int64_t value) {
     g_pair_roles = (int)value;
     return SIREN_OK;
   }
+  if (key && strcmp(key, "dx_stagger") == 0 && (value == 0 || value == 1)) {
+    g_dx_stagger = value != 0;
+    return SIREN_OK;
+  }
   if (key && strcmp(key, "pair_tail_reduce") == 0 && (value == 0 || value == 1)) {
     g_tail_reduce = value != 0;
     return SIREN_OK;
@@ -1699,6 +1708,7 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "dw_ring") == 0) return g_dw_ring ? 1 : 0;
   if (key && strcmp(key, "bwd_ring") == 0) return g_bwd_ring ? 1 : 0;
   if (key && strcmp(key, "pair_tail_reduce") == 0) return g_tail_reduce ? 1 : 0;
+  if (key && strcmp(key, "dx_stagger") == 0) return g_dx_stagger ? 1 : 0;
   if (key && strcmp(key, "pair_ring") == 0) return g_pair_ring ? 1 : 0;
   if (key && strcmp(key, "fused_forward_pipe") == 0) return g_fwd_pipe ? 1 : 0;
   if (key && strcmp(key, "fused_forward_reg") == 0) return g_fwd_reg ? 1 : 0;
