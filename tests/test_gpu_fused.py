@@ -234,21 +234,24 @@ def test_backward_deterministic():
         assert torch.equal(dx, runs[0][1])
 
 
+@pytest.mark.parametrize("option", ["pair_tail_reduce", "dx_stagger"])
 @pytest.mark.parametrize("dims,n", [([2, 256, 256, 256, 256, 1], 70000), ([2, 256, 256, 256, 256, 256, 1], 5000),
                                     ([3, 256, 256, 256, 256, 2], 999)])
-def test_pair_tail_reduce_bit_identical(dims, n):
-    """A pair launch that reduces the previous pair launch's slabs in its tail sums them in
-    reduce_multi_kernel's order (same block body): gradients equal bit for bit either way."""
+def test_pair_options_bit_identical(dims, n, option):
+    """pair_tail_reduce: a pair launch that reduces the previous pair launch's slabs in its tail
+    sums them in reduce_multi_kernel's order (same block body). dx_stagger: the late half's
+    epilogue is the same arithmetic on the same values. Gradients equal bit for bit either way."""
     from siren_mri_amd import _native
     params = _params(dims, None, seed=n)
     x = torch.rand(1, n, dims[0], generator=torch.Generator().manual_seed(n)) * 2 - 1
     res = {}
+    default = _native.get_option(option)
     for v in (1, 0):
-        _native.set_option("pair_tail_reduce", v)
+        _native.set_option(option, v)
         try:
             res[v] = _grads(x, params, True, True, None)
         finally:
-            _native.set_option("pair_tail_reduce", 1)
+            _native.set_option(option, default)
     (g1, dx1), (g0, dx0) = res[1], res[0]
     for (a1, b1), (a0, b0) in zip(g1, g0):
         assert torch.equal(a1, a0) and torch.equal(b1, b0)
