@@ -54,8 +54,12 @@ static_assert(FREG_SYNC == 1 || FREG_SYNC == 2, "ring sync interval");
 // every refill of a slot two DMAs):
 //   FREG_SYNC 1: the slot read by block k + 1 was refilled at the barrier of block k - 6: at least
 //                1 + 2 x 5 (refills) + 2 x 6 (stores) = 23 are younger;
-//   FREG_SYNC 2: the slot read by block k + 2 was refilled (first of two slots) at the barrier of
-//                block k - 4: at least 1 + 2 + 4 (refills) + 2 x 4 (stores) = 15 are younger.
+//   FREG_SYNC 2: the slot read by block k + 2 (its first three fragments are prefetched by block
+//                k + 1, before the next barrier) was refilled (first of two slots) at the barrier of
+//                block k - 4: after this wave's LAST DMA into it, at least 2 (the second slot) +
+//                4 (refills at k - 2) + 2 x 4 (stores) = 14 are younger. (vmcnt(n) returns once at
+//                most n are outstanding, in issue order; vmcnt(15) would leave the wave's second
+//                piece of the slot — fragment 1 for wave 0 — unchecked.)
 #ifdef SIREN_FREG_VMN  // timing experiments only: a looser wait (reads may see unlanded slots)
 #define SIREN_FREG_STR2(x) #x
 #define SIREN_FREG_STR(x) SIREN_FREG_STR2(x)
@@ -63,7 +67,7 @@ static_assert(FREG_SYNC == 1 || FREG_SYNC == 2, "ring sync interval");
 #elif SIREN_FREG_SYNC == 1
 #define SIREN_FREG_VMWAIT "s_waitcnt vmcnt(22)"
 #else
-#define SIREN_FREG_VMWAIT "s_waitcnt vmcnt(15)"
+#define SIREN_FREG_VMWAIT "s_waitcnt vmcnt(14)"
 #endif
 
 struct FwdRegArgs {

@@ -22,6 +22,7 @@ def main():
     p.add_argument("values")
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--kclass", type=int, default=0, help="also time this kernel class (bench.KCLASS_NAMES)")
     cli = p.parse_args()
     sys.argv = [sys.argv[0], "--no-psnr", "--no-cpu-baseline"]
     args = bench.parse()
@@ -43,7 +44,13 @@ def main():
                 step()
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) / cli.steps * 1e3
-            print(f"round {r} {cli.name}={v}: {ms:.4f} ms/step", flush=True)
+            kt = ""
+            if cli.kclass:
+                with _native.KernelTimer(cli.kclass) as t:
+                    for _ in range(20):
+                        step()
+                kt = f", kernel class {cli.kclass}: {t.avg_ms * 1e3:.1f} us/launch"
+            print(f"round {r} {cli.name}={v}: {ms:.4f} ms/step{kt}", flush=True)
     _native.set_option(cli.name, default)
 
 
