@@ -1,0 +1,144 @@
+// Standalone timing harness for the register-resident forward (siren_fwdreg.hip) at the metric
+// shape (262,144 rows, 2-256-256-256-256-1, w0 = 30): builds in seconds, so kernel variants
+// (-D flags) can be compared on one box without rebuilding the library.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I siren_mri_amd/csrc [-DSIREN_FREG_DBG=n] \
+//       -o build/fwd_bench tools/fwd_bench.hip && build/fwd_bench [iters]
+// Prints the average kernel time (HIP events) and checksums of y and the phase codes (equal
+// checksums across variants = the same bits).
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <algorithm>
+#include <vector>
+
+#include "siren_valu.hip"
+#include "siren_gemm.hip"
+#include "siren_fused.hip"
+#ifdef FWD_RG2  // an experimental copy with a row-group template argument (4 waves x 64 rows)
+#include FWD_RG2
+#define FWD_KERNEL fused_fwd_reg_kernel<2, 1, 2>
+#define FWD_THREADS 256
+#else
+#include "siren_fwdreg.hip"
+#define FWD_KERNEL fused_fwd_reg_kernel<2, 1>
+#define FWD_THREADS 512
+#endif
+
+using namespace siren;
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+static uint32_t lcg = 12345u;
+static float urand(float a) {  // uniform in [-a, a]
+  lcg = lcg * 1664525u + 1013904223u;
+  return a * (2.f * ((lcg >> 8) * (1.f / 16777216.f)) - 1.f);
+}
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 50;
+  const int64_t side = 512, rows = side * side;
+  const int F = 256, C = 2, O = 1, nh = 3;
+  const float w0 = 30.f;
+  std::vector<float> hx(rows * C), hW0(F * C), hb0(F), hW(nh * F * F), hb(nh * F), hWL(F), hbL(1);
+  for (int64_t i = 0; i < side; ++i)
+    for (int64_t j = 0; j < side; ++j) {
+      hx[(i * side + j) * 2 + 0] = 2.f * i / (side - 1) - 1.f;
+      hx[(i * side + j) * 2 + 1] = 2.f * j / (side - 1) - 1.f;
+    }
+  for (auto& v : hW0) v = urand(0.5f);
+  for (auto& v : hb0) v = urand(0.7f);
+  for (auto& v : hW) v = urand(0.0051f);
+  for (auto& v : hb) v = urand(0.0625f);
+  for (auto& v : hWL) v = urand(0.0051f);
+  hbL[0] = 0.01f;
+
+  float *x, *W0, *b0, *W, *b, *WL, *bL, *y;
+  _Float16 *wreg, *wlreg;
+  char* P;
+  CK(hipMalloc(&x, hx.size() * 4));
+  CK(hipMalloc(&W0, hW0.size() * 4));
+  CK(hipMalloc(&b0, hb0.size() * 4));
+  CK(hipMalloc(&W, hW.size() * 4));
+  CK(hipMalloc(&b, hb.size() * 4));
+  CK(hipMalloc(&WL, hWL.size() * 4));
+  CK(hipMalloc(&bL, 4));
+  CK(hipMalloc(&y, rows * O * 4));
+  CK(hipMalloc(&wreg, (size_t)nh * F * F * 2));
+  CK(hipMalloc(&wlreg, FREG_WL_BYTES));
+  const int64_t pstride = rows * F * 2;
+  CK(hipMalloc(&P, nh * pstride));
+  CK(hipMemcpy(x, hx.data(), hx.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(W0, hW0.data(), hW0.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(b0, hb0.data(), hb0.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(W, hW.data(), hW.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(b, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(WL, hWL.data(), hWL.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(bL, hbL.data(), 4, hipMemcpyHostToDevice));
+  CK(hipMemset(P, 0, nh * pstride));
+
+  RegPrepArgs p;
+  memset(&p, 0, sizeof(p));
+  for (int l = 0; l < nh; ++l) p.W[l] = W + (int64_t)l * F * F;
+  p.WL = WL;
+  p.out = wreg;
+  p.outL = wlreg;
+  p.nb = 1;
+  p.nh = nh;
+  p.O = O;
+  p.k1 = w0 * kInv2Pi;
+  hipLaunchKernelGGL(prep_reg_kernel, dim3(256), dim3(256), 0, 0, p);
+  CK(hipGetLastError());
+
+  FwdRegArgs a;
+  memset(&a, 0, sizeof(a));
+  a.x = x;
+  a.W0 = W0;
+  a.b0 = b0;
+  a.Wreg = wreg;
+  a.WLreg = wlreg;
+  for (int l = 0; l < nh; ++l) a.bias[l] = b + l * F;
+  a.bL = bL;
+  a.P0 = nullptr;
+  a.Pb = P;
+  a.pstride = pstride;
+  a.y = y;
+  a.rows_per_batch = rows;
+  a.batched = 0;
+  a.O = O;
+  a.nh = nh;
+  a.sine_out = 0;
+  a.w0 = w0;
+  const int64_t tiles = (rows + FREG_WG_ROWS - 1) / FREG_WG_ROWS;
+  dim3 grid((unsigned)std::min<int64_t>(tiles, 256)), block(FWD_THREADS);
+  for (int i = 0; i < 5; ++i) hipLaunchKernelGGL((FWD_KERNEL), grid, block, 0, 0, a);
+  CK(hipDeviceSynchronize());
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0, 0));
+  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL((FWD_KERNEL), grid, block, 0, 0, a);
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  std::vector<float> hy(rows);
+  std::vector<uint16_t> hp(nh * rows * F);
+  CK(hipMemcpy(hy.data(), y, rows * 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(hp.data(), P, nh * pstride, hipMemcpyDeviceToHost));
+  double sy = 0.0;
+  for (float v : hy) sy += v;
+  uint64_t sp = 1469598103934665603ull;
+  for (uint16_t v : hp) sp = (sp ^ v) * 1099511628211ull;
+  const double us = ms * 1e3 / iters;
+  printf("forward %.2f us  (%.1f TF/s of %.1f GFLOP)  y-sum %.9e  P-hash %016llx\n", us,
+         2.0 * rows * (C * F + nh * F * F + F * O) / (us * 1e-6) / 1e12, 2.0 * rows * (C * F + nh * F * F + F * O) / 1e9,
+         sy, (unsigned long long)sp);
+  return 0;
+}
