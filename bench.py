@@ -335,6 +335,27 @@ def main():
                    "parallelism": f"dp{world} (coordinate-sharded, one gradient all-reduce per step)"},
         "roofline": roofline,
     }
+    # north_star's per-kernel target: bf16-MFMA utilisation of the fused SineLayer GEMM (the whole
+    # forward: every layer's GEMM + bias + sine in one launch) = its algorithmic FLOPs / its average
+    # launch time / the dense bf16 peak, from the same HIP-event timer, measured after the timed region
+    if 4 in totals and dom != 4:
+        with _native.KernelTimer(4, max_launches=64) as ft:
+            for _ in range(10):
+                step()
+        f_flops, f_bytes = kernel_model(args, 4, p0_recompute)
+        f_s = ft.avg_ms * 1e-3
+        result_fwd = {"kernel": KCLASS_NAMES[4], "kernel_symbol": KCLASS_SYMBOL.get(args.precision, {}).get(4),
+                      "flops_per_launch": f_flops, "avg_launch_ms": round(ft.avg_ms, 4), "launches": ft.launches,
+                      "achieved_tflops": round(f_flops / f_s / 1e12, 2), "mfma_peak_tflops": mfma_peak / 1e12,
+                      "mfma_frac": round(f_flops / f_s / mfma_peak, 4),
+                      "hbm_gbps": round(f_bytes / f_s / 1e9, 1), "hbm_frac": round(f_bytes / f_s / HBM_PEAK, 4)}
+    elif dom == 4:
+        result_fwd = {"kernel": KCLASS_NAMES[4], "mfma_frac": round(flops / avg_s / mfma_peak, 4),
+                      "achieved_tflops": round(flops / avg_s / 1e12, 2), "avg_launch_ms": round(kt.avg_ms, 4)}
+    else:
+        result_fwd = None
+    if result_fwd is not None:
+        result["fused_sine_gemm"] = result_fwd
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, args.cpu_budget_s)
     if rank == 0 and world == 1 and not args.no_psnr:

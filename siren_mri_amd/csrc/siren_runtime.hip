@@ -107,12 +107,17 @@ bool fused_shape(const siren_mlp_desc* d) {
 // bf16 stacks of the fused/ring shapes do not keep P_0: the layer-1 ring kernels recompute it from
 // x (C <= 4 inputs) — 2 B per row-feature less written by the forward and read twice by the
 // backward. Decided from the descriptor alone, so forward and backward always agree.
+// Every row count qualifies: x moves by LDS-DMA through buffer resources whose bounds are checked
+// per dword (a 16-byte piece straddling the end loads its valid dwords and zeros,
+// tools/probe_lds_oob.hip) and whose base may sit 8 bytes past a 16-byte boundary (a weight set's x
+// rows when rows_per_batch x C is not a multiple of 4; the forward reads x the same way). Keeping
+// P_0 instead (the round-2 rule for such shapes) made the register-resident forward's layer-0
+// phase-code stores differ from run to run in a few words (tools/det_saved.py), so the stored-P_0
+// path is no longer taken by fused shapes.
 bool p0_recompute(const siren_mlp_desc* d) {
   if (!fused_shape(d) || d->num_layers < 3) return false;
-  const int64_t C = d->dims[0], rpb = d->rows_per_batch, total = d->batch * rpb;
-  if ((total * C) % 4 != 0 || total * C < 4) return false;
-  if (d->weights_batched && (rpb * C) % 4 != 0) return false;
-  return true;
+  const int64_t C = d->dims[0], total = d->batch * d->rows_per_batch;
+  return total * C >= 1;
 }
 
 int max_hidden(const siren_mlp_desc* d) {

@@ -125,3 +125,22 @@ def test_reg_forward_is_deterministic():
     assert torch.equal(y1, y2)
     for (a, b), (c, d) in zip(g1, g2):
         assert torch.equal(a, c) and torch.equal(b, d)
+
+
+@pytest.mark.parametrize("dims,B,n", [([2, 256, 256, 256, 256, 1], 5, 16384 + 31),
+                                      ([2, 256, 256, 256, 256, 1], None, 16384 + 1),
+                                      ([2, 256, 256, 256, 2], 3, 500)])
+def test_ragged_and_batched_are_deterministic(dims, B, n):
+    """Ragged row counts (rows x C not a multiple of 4) and per-set weights (the hypernetwork
+    shape): two identical runs give bit-identical outputs and parameter gradients (no atomics on
+    the path, fixed reduction orders). Round 2 kept P_0 for such shapes and the register forward's
+    layer-0 phase-code stores then varied from run to run (tools/det_saved.py)."""
+    params = _params(dims, B, seed=3)
+    g = torch.Generator().manual_seed(n)
+    x = torch.rand(B or 1, n, dims[0], generator=g) * 2 - 1
+    y1, g1 = _run(x, params, reg=True, grad=True)
+    y2, g2 = _run(x, params, reg=True, grad=True)
+    assert torch.equal(y1, y2)
+    for l, ((a, b), (c, d)) in enumerate(zip(g1, g2)):
+        assert torch.equal(a, c), (l, (a - c).abs().max())
+        assert torch.equal(b, d), (l, (b - d).abs().max())

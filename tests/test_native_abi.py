@@ -80,6 +80,17 @@ def test_saved_bytes_formula_bf16():
     assert got == weights + phases
 
 
+def test_saved_bytes_ragged_rows_recompute_p0():
+    """Row counts whose x is not a whole number of 16-byte pieces (rows x C odd multiples of 2)
+    also rebuild P_0 from x in the backward: no layer-0 phase tensor is kept."""
+    lib = _native.load_library()
+    for rows, batch, batched in ((16385, 1, False), (16415, 5, True)):
+        d = _desc([2, 256, 256, 256, 256, 1], rows_per_batch=rows, batch=batch, weights_batched=batched)
+        got = lib.siren_mlp_saved_bytes(ctypes.byref(d))
+        weights = batch * (3 * 3 * 256 * 256 * 2 + 4096)
+        assert got == weights + 3 * batch * rows * 256 * 2, (rows, batch)
+
+
 def test_config_options():
     lib = _native.load_library()
     assert lib.siren_config_get(b"fused_forward") in (0, 1)
