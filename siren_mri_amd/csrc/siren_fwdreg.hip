@@ -86,6 +86,9 @@ struct FwdRegArgs {
   int batched;
   int O, nh, sine_out;
   float w0;
+#ifdef SIREN_FREG_CLOCK
+  long long* clk;             // diagnostic builds only: [grid][4] s_memtime / s_memrealtime stamps
+#endif
 };
 
 DEV void freg_barrier() {
@@ -177,6 +180,9 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   const int64_t G = gridDim.x;
   const int64_t t0 = blockIdx.x;
   if (t0 >= ntiles) return;
+#ifdef SIREN_FREG_CLOCK  // diagnostic builds only (MI355X_MICROARCH.md 'DVFS give-back' item 6)
+  const long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
   using T_ = std::true_type;
   using F_ = std::false_type;
@@ -497,6 +503,16 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   }
   // no LDS-DMA may land after the workgroup has released its LDS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef SIREN_FREG_CLOCK
+  if (tid == 0) {
+    const long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    long long* c = a.clk + 4 * (blockIdx.x + (int64_t)gridDim.x * blockIdx.y);
+    c[0] = clk_t0;
+    c[1] = t1;
+    c[2] = clk_r0;
+    c[3] = r1;
+  }
+#endif
 }
 
 // Prepared weights of the register-resident forward (see the header comment):

@@ -115,6 +115,11 @@ int main(int argc, char** argv) {
   a.nh = nh;
   a.sine_out = 0;
   a.w0 = w0;
+#ifdef SIREN_FREG_CLOCK
+  long long* clk;
+  CK(hipMalloc(&clk, 256 * 4 * sizeof(long long)));
+  a.clk = clk;
+#endif
   const int64_t tiles = (rows + FREG_WG_ROWS - 1) / FREG_WG_ROWS;
   dim3 grid((unsigned)std::min<int64_t>(tiles, 256)), block(FWD_THREADS);
   for (int i = 0; i < 5; ++i) hipLaunchKernelGGL((FWD_KERNEL), grid, block, 0, 0, a);
@@ -137,6 +142,22 @@ int main(int argc, char** argv) {
   uint64_t sp = 1469598103934665603ull;
   for (uint16_t v : hp) sp = (sp ^ v) * 1099511628211ull;
   const double us = ms * 1e3 / iters;
+#ifdef SIREN_FREG_CLOCK
+  {  // last launch: per-workgroup shader cycles and in-kernel clock (memtime / realtime x 100 MHz)
+    std::vector<long long> hc(256 * 4);
+    CK(hipMemcpy(hc.data(), clk, hc.size() * sizeof(long long), hipMemcpyDeviceToHost));
+    std::vector<double> cyc, ghz;
+    for (unsigned b = 0; b < grid.x; ++b) {
+      const double dc = (double)(hc[4 * b + 1] - hc[4 * b]), dr = (double)(hc[4 * b + 3] - hc[4 * b + 2]);
+      cyc.push_back(dc);
+      ghz.push_back(dr > 0 ? dc / dr * 0.1 : 0.0);
+    }
+    std::sort(cyc.begin(), cyc.end());
+    std::sort(ghz.begin(), ghz.end());
+    printf("clock: median %.3f GHz (min %.3f, max %.3f); workgroup cycles median %.0f (max %.0f)\n",
+           ghz[ghz.size() / 2], ghz.front(), ghz.back(), cyc[cyc.size() / 2], cyc.back());
+  }
+#endif
   printf("forward %.2f us  (%.1f TF/s of %.1f GFLOP)  y-sum %.9e  P-hash %016llx\n", us,
          2.0 * rows * (C * F + nh * F * F + F * O) / (us * 1e-6) / 1e12, 2.0 * rows * (C * F + nh * F * F + F * O) / 1e9,
          sy, (unsigned long long)sp);
