@@ -13,7 +13,7 @@ import torch.distributed as dist
 from torch.utils.data import DataLoader
 from torch.utils.data.distributed import DistributedSampler
 
-from siren_mri_amd import dataio, loss_functions, meta_modules, training_ddp
+from siren_mri_amd import checkpoints, dataio, loss_functions, meta_modules, training_ddp
 from siren_mri_amd.features import GaussianFourierFeatureTransform
 
 p = base_parser(batch_size=32, lr=5.57e-5, num_epochs=200, epochs_til_ckpt=5, steps_til_summary=100)
@@ -45,7 +45,8 @@ model = meta_modules.ConvolutionalNeuralProcessImplicit2DHypernetFourierFeatures
     num_hidden_layers=hidden_layers, partial_conv=False, conv_kernel_size=conv_kernel_size,
     num_conv_res_blocks=num_conv_res_blocks, w0=w0, precision=opt.precision)
 if opt.checkpoint_path is not None:
-    model.load_state_dict(torch.load(opt.checkpoint_path, map_location="cpu", weights_only=True))
+    # reference checkpoints from its DDP wrapper carry a "module." prefix (training_ddp.py:89,146)
+    checkpoints.load_state_dict_compat(model, opt.checkpoint_path)
 model.to(device)
 
 fourier_transformer = GaussianFourierFeatureTransform(num_input_channels=2, mapping_size_spatial=num_fourier_features,
@@ -54,10 +55,19 @@ B = fourier_transformer.get_B().contiguous()
 dist.broadcast(B, src=0)
 fourier_transformer.set_B(B)
 
+model_dir = f"{opt.logging_root}/{opt.experiment_name}"
 training_ddp.train_ddp(model=model, train_dataloader=dataloader, epochs=opt.num_epochs, lr=opt.lr,
                        steps_til_summary=opt.steps_til_summary, epochs_til_checkpoint=opt.epochs_til_ckpt,
-                       model_dir=f"{opt.logging_root}/{opt.experiment_name}",
+                       model_dir=model_dir,
                        loss_fn=partial(loss_functions.image_hypernetwork_loss, None, kl_weight, fw_weight),
                        summary_fn=psnr_summary(), clip_grad=True, fourier_feat_transformer=fourier_transformer,
                        device=device, accumulation_steps=opt.accumulation_steps, ddp_run=True)
+# every rank's B as <model_dir>/current_B_DDP_mp<rank>.pt, the reference's file names
+# (train_mri_neural_process_ddp.py:254-256; its test script loads them,
+# test_mri_conv_neural_process_kspace_fourierfeat.py:214-215). Written after training: the
+# reference saves them before train_ddp, whose rank 0 then removes model_dir (training_ddp.py:29-31).
+# B is identical on every rank (broadcast above), so rank 0 writes all the files.
+if rank == 0:
+    for r in range(world_size):
+        checkpoints.save_b_matrix(fourier_transformer, model_dir, r)
 dist.destroy_process_group()

@@ -168,3 +168,39 @@ def test_diff_operators_autograd_path_for_non_siren():
     assert torch.allclose(g, 3 * x ** 2)
     lap = diff_operators.laplace(y, x)
     assert torch.allclose(lap, (6 * x).sum(-1, keepdim=True))
+
+
+def test_checkpoint_compat_ddp_prefix_and_b_files(tmp_path):
+    """§8(f) row 4: model files with the reference DDP wrapper's "module." prefix
+    (training_ddp.py:89,146) and without it (training_ddp.py:53, this package's loops) load into
+    a plain SingleBVPNet; B goes to current_B_DDP_mp<rank>.pt as a bare tensor
+    (train_mri_neural_process_ddp.py:254-256) and reads back with weights_only loading."""
+    from siren_mri_amd import checkpoints
+    torch.manual_seed(0)
+    src = modules.SingleBVPNet(type="sine", hidden_features=32, num_hidden_layers=1)
+    torch.manual_seed(1)
+    dst = modules.SingleBVPNet(type="sine", hidden_features=32, num_hidden_layers=1)
+    assert not torch.equal(src.net.net[0][0].weight, dst.net.net[0][0].weight)
+    p_ddp, p_plain = tmp_path / "model_final.pth", tmp_path / "model_epoch_0005.pth"
+    torch.save(checkpoints.ddp_state_dict(src), p_ddp)
+    torch.save(src.state_dict(), p_plain)
+    assert all(k.startswith("module.net.net.") for k in torch.load(p_ddp, weights_only=True))
+    for p in (p_ddp, p_plain, str(p_ddp)):
+        dst2 = modules.SingleBVPNet(type="sine", hidden_features=32, num_hidden_layers=1)
+        checkpoints.load_state_dict_compat(dst2, p)
+        for (k, a), (k2, b) in zip(src.state_dict().items(), dst2.state_dict().items()):
+            assert k == k2 and torch.equal(a, b)
+    # a state_dict with only some prefixed keys is not rewritten (strict loading then fails)
+    mixed = dict(src.state_dict())
+    k0 = next(iter(mixed))
+    mixed["module." + k0] = mixed.pop(k0)
+    with pytest.raises(RuntimeError):
+        checkpoints.load_state_dict_compat(dst, mixed)
+    ft = features.GaussianFourierFeatureTransform(2, mapping_size_spatial=8, scale=21)
+    path = checkpoints.save_b_matrix(ft, str(tmp_path / "run"), 3)
+    assert os.path.basename(path) == "current_B_DDP_mp3.pt"
+    B = torch.load(path, weights_only=True)
+    assert isinstance(B, torch.Tensor) and B.shape == (2, 8) and torch.equal(B, ft.get_B().cpu())
+    ft2 = features.GaussianFourierFeatureTransform(2, mapping_size_spatial=8, scale=21)
+    checkpoints.load_b_matrix(ft2, str(tmp_path / "run"), 3)
+    assert torch.equal(ft2.get_B(), ft.get_B())

@@ -38,3 +38,40 @@ def test_train_mri_neural_process_script(tmp_path):
     losses = run("train_mri_neural_process.py", tmp_path, "--num_epochs", "2", "--batch_size", "4",
                  "--n_slices", "16", "--steps_til_summary", "2")
     assert np.all(np.isfinite(losses))
+
+
+def test_train_mri_neural_process_ddp_script_files(tmp_path):
+    """The DDP counterpart under torchrun (one rank): the reference's file layout, B as
+    current_B_DDP_mp<rank>.pt, and a resume from its own model_final.pth through
+    checkpoints.load_state_dict_compat."""
+    import socket
+
+    import torch
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+
+    def launch(name, *extra):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+               "--master-addr", "127.0.0.1", "--master-port", str(port),
+               os.path.join(ROOT, "experiment_scripts", "train_mri_neural_process_ddp.py"),
+               "--logging_root", str(tmp_path), "--experiment_name", name, "--num_epochs", "1", "--batch_size", "4",
+               "--n_slices", "8", "--steps_til_summary", "1", *extra]
+        r = subprocess.run(cmd, cwd=tmp_path, capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+
+    launch("run")
+    final = tmp_path / "run" / "checkpoints" / "model_final.pth"
+    assert final.exists() and (tmp_path / "run" / "current_B_DDP_mp0.pt").exists()
+    B = torch.load(tmp_path / "run" / "current_B_DDP_mp0.pt", weights_only=True)
+    assert B.shape == (2, 60)
+    sd = torch.load(final, weights_only=True)
+    assert not any(k.startswith("module.") for k in sd)  # loadable by the reference's test scripts
+    # the reference's DDP-wrapper form of the same file resumes too
+    from siren_mri_amd import checkpoints
+    prefixed = tmp_path / "prefixed.pth"
+    torch.save({"module." + k: v for k, v in sd.items()}, prefixed)
+    launch("resume", "--checkpoint_path", str(prefixed))
+    assert (tmp_path / "resume" / "checkpoints" / "model_final.pth").exists()
+    assert checkpoints.strip_ddp_prefix(torch.load(prefixed, weights_only=True)).keys() == sd.keys()
