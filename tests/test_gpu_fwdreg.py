@@ -144,3 +144,22 @@ def test_ragged_and_batched_are_deterministic(dims, B, n):
     for l, ((a, b), (c, d)) in enumerate(zip(g1, g2)):
         assert torch.equal(a, c), (l, (a - c).abs().max())
         assert torch.equal(b, d), (l, (b - d).abs().max())
+
+
+@pytest.mark.parametrize("dims,B,n", [([2, 256, 256, 256, 256, 1], 3, 1001),
+                                      ([3, 256, 256, 256, 2], None, 999),
+                                      ([1, 256, 256, 256, 1], 2, 515)])
+def test_ragged_rows_gradients_match_oracle(dims, B, n):
+    """Ragged shapes (rows x C not a multiple of 4, so a weight set's x rows can start 8 bytes past
+    a 16-byte boundary) rebuild P_0 from x by LDS-DMA in the backward: parameter gradients vs the
+    fp64 oracle's autograd (bf16-mode tolerance)."""
+    params = _params(dims, B, seed=n)
+    g = torch.Generator().manual_seed(n)
+    x = torch.rand(B or 1, n, dims[0], generator=g) * 2 - 1
+    _, g_r = _run(x, params, reg=True, grad=True)
+    ps = [(W.double().requires_grad_(True), b.double().requires_grad_(True)) for W, b in params]
+    y = orc.siren_forward(x.double(), ps)
+    (y.square().sum() * (1.0 / y.numel())).backward()
+    for (dW, db), (W, b) in zip(g_r, ps):
+        assert orc.norm_rel(dW.double(), W.grad) < 5e-2
+        assert orc.norm_rel(db.double(), b.grad) < 5e-2
