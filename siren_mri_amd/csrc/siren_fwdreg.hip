@@ -449,6 +449,15 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
       p_bytes = (int)((rows - r0 < FREG_WG_ROWS ? rows - r0 : FREG_WG_ROWS) * F * 2);
     }
     const int xb = (int)(((t - t0) / G) & 1);
+    // This round's x tile was issued (LDS-DMA, waves 0..C-1) at the previous round's hidden
+    // layer 0 block 0. With two or more hidden layers at least 28 vector-memory operations are
+    // younger at the next layer's first ring sync, whose vmcnt(14) + barrier cover it. With one
+    // hidden layer the ring is never refilled and only the phase stores follow it, so wait for
+    // it here explicitly.
+    if (nh == 1 && t != t0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      freg_barrier();
+    }
     // ---- layer 0 (f32 MFMA, K = C): blocks 0..6 converted here, block 7 beside hidden block 0 ----
     auto layer0 = [&](auto codes_tag) {
       const float* xt = xs[xb] + (wave * FREG_WROWS + j) * C;

@@ -114,8 +114,9 @@ bool fused_shape(const siren_mlp_desc* d) {
 // P_0 instead (the round-2 rule for such shapes) made the register-resident forward's layer-0
 // phase-code stores differ from run to run in a few words (tools/det_saved.py), so the stored-P_0
 // path is no longer taken by fused shapes.
+bool g_keep_p0 = false;  // debug: fused shapes keep P_0 (the stored-P_0 path) instead of rebuilding it
 bool p0_recompute(const siren_mlp_desc* d) {
-  if (!fused_shape(d) || d->num_layers < 3) return false;
+  if (g_keep_p0 || !fused_shape(d) || d->num_layers < 3) return false;
   const int64_t C = d->dims[0], total = d->batch * d->rows_per_batch;
   return total * C >= 1;
 }
@@ -1688,6 +1689,10 @@ int siren_config_set(const char* key, int64_t value) {
     g_pair_ring = value != 0;
     return SIREN_OK;
   }
+  if (key && strcmp(key, "debug_keep_p0") == 0 && (value == 0 || value == 1)) {
+    g_keep_p0 = value != 0;
+    return SIREN_OK;
+  }
   if (key && strcmp(key, "debug_ring_profile") == 0) {  // device pointer or 0
     g_ring_prof = (long long*)(intptr_t)value;
     g_ring_prof_n = 0;
@@ -1715,6 +1720,7 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "pair_tail_reduce") == 0) return g_tail_reduce ? 1 : 0;
   if (key && strcmp(key, "dx_stagger") == 0) return g_dx_stagger ? 1 : 0;
   if (key && strcmp(key, "pair_ring") == 0) return g_pair_ring ? 1 : 0;
+  if (key && strcmp(key, "debug_keep_p0") == 0) return g_keep_p0 ? 1 : 0;
   if (key && strcmp(key, "fused_forward_pipe") == 0) return g_fwd_pipe ? 1 : 0;
   if (key && strcmp(key, "fused_forward_reg") == 0) return g_fwd_reg ? 1 : 0;
   return -1;

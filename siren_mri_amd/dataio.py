@@ -3,15 +3,17 @@
 Restated from the reference:
   get_mgrid                  dataio.py:28-48   row-major grid, x_k = 2 i_k/(S_k - 1) - 1
   lin2img                    dataio.py:51-63   [B, N, C] -> [B, C, H, W]
-  Camera                     dataio.py:474-492 (cameraman, from tests/golden/camera512_u8.npz)
+  Camera                     dataio.py:474-492 (cameraman, siren_mri_amd/assets/camera512_u8.npz)
+  MRIImageDomain             dataio.py:507-525 (data/IRData.mat -> siren_mri_amd/assets/irdata.npz)
   Implicit2DWrapper          dataio.py:746-827 (PIL bilinear resize, /255, Normalize; sobel /
                                                 laplace ground truth via scipy.ndimage)
   ImageGeneralizationWrapper dataio.py:861-986 (CS-Cartesian masks, conv_cnp inputs)
   FastMRIBrainKspace layout  dataio.py:585-664 (fftshift(fft2(slice)) stacked [H, W, 2])
 
 Deviation (bug 0.7): fastMRI .h5 volumes are not available, so
-SyntheticMRIKspace produces k-space of seeded synthetic phantoms (ellipses plus optional
-IRData-like contrast) with the same [H, W, 2] float32 layout; the CS mask RNG is seeded.
+SyntheticMRIKspace produces k-space of seeded phantoms with the same [H, W, 2] float32 layout:
+the reference tree's own IRData slices under the 8 flips/rotations and seeded
+random-ellipse phantoms; the CS mask RNG is seeded.
 """
 from __future__ import annotations
 
@@ -22,7 +24,8 @@ import numpy as np
 import torch
 from torch.utils.data import Dataset
 
-_GOLDEN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
+# data assets shipped with the package (tools/make_assets.py, tests/golden/make_golden.py)
+ASSETS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets")
 
 
 def get_mgrid(sidelen, dim=2):
@@ -45,7 +48,7 @@ def lin2img(tensor, image_resolution=None):
 
 def camera_image() -> np.ndarray:
     """The 512x512 uint8 cameraman (the image skimage.data.camera() returns)."""
-    path = os.path.join(_GOLDEN, "camera512_u8.npz")
+    path = os.path.join(ASSETS, "camera512_u8.npz")
     with np.load(path, allow_pickle=False) as d:
         return d["img"]
 
@@ -66,6 +69,41 @@ class Camera(Dataset):
 
     def __getitem__(self, idx):
         return self.img_downsampled if self.downsample_factor > 1 else self.img
+
+
+def irdata() -> np.ndarray:
+    """IRData [128, 128, 9] float32 (np.squeeze of data/IRData.mat's 'IRData', dataio.py:519-520)."""
+    with np.load(os.path.join(ASSETS, "irdata.npz"), allow_pickle=False) as d:
+        return d["IRData"]
+
+
+class MRIImageDomain(Dataset):
+    """dataio.py:507-525: the 9 IRData magnitude slices, item = [128, 128] float32. `split` is
+    checked as in the reference and otherwise unused (the reference reads one file for all)."""
+
+    def __init__(self, split="train", downsampled=False):
+        assert split in ["train", "test", "val", "val_small"], "Unknown split"
+        self.img_channels = 1
+        self.downsampled = downsampled
+        self.data = irdata()
+
+    def __len__(self):
+        return self.data.shape[2]
+
+    def __getitem__(self, idx):
+        return np.squeeze(self.data[:, :, idx])
+
+
+def irdata_image(idx: int = 0, side: int = 256) -> torch.Tensor:
+    """Config C2's fitting target (harness-defined since BASELINE.json says
+    256x256 and IRData is 128x128): slice idx -> / max -> x2 - 1 -> bilinear resize to side^2
+    (F.interpolate, align_corners=False). Returns [side*side, 1] float32 in the flattened
+    get_mgrid row order (row-major over (i, j))."""
+    import torch.nn.functional as F
+    sl = torch.from_numpy(np.ascontiguousarray(MRIImageDomain()[idx]))
+    sl = sl / sl.max() * 2 - 1
+    img = F.interpolate(sl[None, None], size=(side, side), mode="bilinear", align_corners=False)
+    return img.reshape(-1, 1).contiguous()
 
 
 def smooth_random_image(side: int, n_waves: int = 32, seed: int = 0, max_freq: float = 16.0) -> np.ndarray:
@@ -166,20 +204,40 @@ def _ellipse_phantom(res: int, rs: np.random.RandomState, n_ellipses: int = 8) -
 
 class SyntheticMRIKspace(Dataset):
     """Seeded synthetic stand-in for FastMRIBrainKspace (bug 0.7): item = float32 [H, W, 2] of
-    fftshift(fft2(phantom)) stacked real/imag, the reference's layout (dataio.py:654-664)."""
+    fftshift(fft2(slice)) stacked real/imag, the reference's layout (dataio.py:654-664).
+    Items 0..71 (with irdata=True) are the 9 IRData slices under the 8 flips/rotations of the
+    square (normalised to max 1, bilinear-resized when the resolution is not 128); later items
+    are seeded random-ellipse phantoms."""
 
-    def __init__(self, n_slices: int = 256, image_resolution=(128, 128), seed: int = 0):
+    def __init__(self, n_slices: int = 256, image_resolution=(128, 128), seed: int = 0, irdata: bool = True):
         self.n = n_slices
         self.res = image_resolution
         self.seed = seed
         self.img_channels = 2
+        self._ir = globals()["irdata"]() if irdata else None
 
     def __len__(self):
         return self.n
 
+    def _ir_slice(self, idx):
+        sl = self._ir[:, :, idx % 9].astype(np.float64)
+        t = idx // 9
+        sl = np.rot90(sl, t % 4)
+        if t >= 4:
+            sl = sl[:, ::-1]
+        sl = sl / max(sl.max(), 1e-12)
+        if tuple(self.res) != sl.shape:
+            import torch.nn.functional as F
+            sl = F.interpolate(torch.from_numpy(np.ascontiguousarray(sl))[None, None], size=tuple(self.res),
+                               mode="bilinear", align_corners=False)[0, 0].numpy()
+        return sl
+
     def __getitem__(self, idx):
         rs = np.random.RandomState(self.seed * 100003 + idx)
-        img = _ellipse_phantom(self.res[0], rs)
+        if self._ir is not None and idx < 72:
+            img = self._ir_slice(idx)
+        else:
+            img = _ellipse_phantom(self.res[0], rs)
         k = np.fft.fftshift(np.fft.fft2(img))
         k = k / max(np.abs(k).max(), 1e-12)
         return np.float32(np.dstack((k.real, k.imag)))

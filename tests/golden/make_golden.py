@@ -18,7 +18,7 @@ It imports the reference with in-process stubs for its unused heavy dependencies
   hypernet.npz     ConvolutionalNeuralProcessImplicit2DHypernetFourierFeatures forward (reduced
                    sizes, B=2) on IRData-derived k-space + state_dict + losses
   features.npz     GaussianFourierFeatureTransform + DataConsistencyInKspace
-  camera512_u8.npz the cameraman test image (uint8, from skimage's data dir) used by config 1
+  ../../siren_mri_amd/assets/camera512_u8.npz  the cameraman (uint8, skimage's data dir), config 1 input
 
 The reference's own bugs are worked around exactly as the build documents them:
 high_freq=False off 128^2 (bug 0.2), training.train's final UnboundLocalError is caught after it
@@ -37,6 +37,7 @@ import torch
 
 REF = "/root/reference"
 OUT = os.path.dirname(os.path.abspath(__file__))
+ASSETS = os.path.join(os.path.dirname(os.path.dirname(OUT)), "siren_mri_amd", "assets")
 CAMERA = "/opt/conda/lib/python3.9/site-packages/skimage/data/camera.png"
 
 
@@ -188,7 +189,8 @@ def main():
                         laplace_mse=lapm.item())
 
     # camera image ------------------------------------------------------------------------------
-    np.savez_compressed(os.path.join(OUT, "camera512_u8.npz"), img=camera_u8())
+    # (written into the package's data assets: siren_mri_amd/assets/, the product reads it from there)
+    np.savez_compressed(os.path.join(ASSETS, "camera512_u8.npz"), img=camera_u8())
 
     # config 1: training.train 10 steps (64^2, 3x256 = nh 1) ----------------------------------
     img64 = camera_tensor(64)

@@ -117,7 +117,8 @@ def test_psnr_trajectory_first_steps():
     """Oracle reproduces the reference PSNR trajectory (steps 0/50/100) of SURVEY.md §6."""
     d = load("psnr_c1.npz")
     from PIL import Image
-    u8 = load("camera512_u8.npz")["img"]
+    from siren_mri_amd.dataio import camera_image
+    u8 = camera_image()
     img = np.asarray(Image.fromarray(u8).resize((64, 64), Image.BILINEAR), dtype=np.float32) / 255.0
     img = torch.from_numpy((img - 0.5) / 0.5)
     gt = {"img": img.reshape(1, -1, 1)}
