@@ -1,26 +1,44 @@
 """Benchmark: SIREN fitting throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision bf16|fp32]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config m|c1|c2|c3|c4]
+                    [--scaling weak|strong] [--precision bf16|fp32] [--no-graph]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[1]'s metric configuration): the train_img.py
-fit — a 512x512 coordinate grid (262,144 coords per GPU per step, full batch) through a
-5x256 SIREN (SingleBVPNet: 2-256-256-256-256-1, w0=30), image_mse + Adam(lr=1e-4). One step =
-forward + loss + backward + (N>1: one RCCL all-reduce of the 198,401 grads) + Adam. Synthetic
-target: a smooth random image (sum of 32 sinusoids). Multi-GPU is weak scaling: every rank owns
-its own 512^2 block of coordinates (a 512 x 512N image), one gradient all-reduce per step.
+Workloads (BASELINE.json configs); the default is M, the metric's:
+  m   train_img.py fit step: 512^2 coordinate grid (262,144 coords per GPU per step, full batch),
+      SingleBVPNet 2-256-256-256-256-1 (w0=30), image_mse + Adam(1e-4), bf16 kernels. Synthetic
+      target: a smooth random image (sum of 32 sinusoids).
+  c1  64^2 cameraman, 2-256-256-1 ("3x256" = num_hidden_layers 1), image_mse + Adam, bf16.
+  c2  256^2 IRData slice 0 (/max, x2-1, bilinear 256^2), 5x256, image_mse + Adam, bf16.
+  c3  512^2 + gradients_mse (analytic gradient and its double backward), 5x256, fp32.
+  c4  hypernetwork MRI neural process (reference config hyperoptIV_homebrew): 32 k-space slices
+      of 128^2 per GPU per step, conv encoder (bf16 channels-last) -> hypernetwork -> SIREN
+      16-256-256-256-256-2 with per-slice weights (bf16) -> data consistency, image_hypernetwork_loss,
+      clip_grad_norm_(1.0), Adam(5.57e-5).
+One step = forward + loss + backward (+ N>1: the gradient all-reduce over RCCL) + Adam.
 
-Prints ONE JSON line on rank 0 with: value (coord-samples/s, whole job), roofline of the
-dominant kernel (HIP events around each of its launches inside the timed region; algorithmic
-FLOPs / bytes per launch from kernel_model), cpu_baseline (the CPU oracle timed on this host, rank 0, N=1 only),
-and psnr (64^2 cameraman, 500 steps, this path vs the reference's golden trajectory).
+Scaling: weak (default; every rank owns its own full-size problem: a 512^2 block of a 512 x 512N
+image, or its own 32 slices) or strong (--scaling strong: ONE global grid split into contiguous
+row blocks by training_ddp.shard_rows; the summed gradient all-reduce makes it the single-GPU fit).
+
+The timed region replays a hipGraph holding exactly K captured steps (--no-graph: K eager steps);
+the dominant kernel's launches inside it are bracketed by captured HIP event pairs on the launch
+stream, so its average duration comes from the timed region itself.
+
+Prints ONE JSON line on rank 0: value (coord-samples/s, whole job), roofline of the dominant
+kernel (MFMA-bound per SURVEY.md §8(d): algorithmic FLOPs per launch / launch time / dense peak;
+PMC HBM traffic from profiles/pmc_traffic.json), the step's FLOP roofline, cpu_baseline (the CPU
+oracle on this host, rank 0, N=1 only), psnr (M: 64^2 cameraman, 500 steps vs the reference's
+golden trajectory) and, for the default run, short measurements of configs c1..c4 ("configs").
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
+import subprocess
 import sys
 import time
 
@@ -31,13 +49,14 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PEAK = {"bf16": (2.5e15, "TFLOP/s"), "fp32": (157.3e12, "TFLOP/s")}
+PEAK = {"bf16": 2.5e15, "fp32": 157.3e12}  # dense MFMA (MI355X_MICROARCH.md; no sparsity)
 HBM_PEAK = 8.0e12
 KCLASS_NAMES = {
     1: "nt_bf16_kernel<fwd> (per-layer forward GEMM + bias/w0/phase epilogue)",
     2: "nt_*_kernel<dx> (per-layer input-gradient GEMM + cos epilogue)",
     3: "tn_dw_kernel (per-layer weight-gradient split-K GEMM)",
-    4: "fused_fwd_pipe_kernel (whole forward: layer 0, hidden MFMA layers, output layer)",
+    4: "fused_fwd_reg_kernel (whole forward, activations in registers: layer 0 on the f32 MFMA, "
+       "hidden and output layers on the f16 MFMA)",
     5: "bwd_ring_bf16_kernel (middle layer dX + dW)",
     6: "dx_ring_bf16_kernel<0,false,false,0> (middle-layer input gradient)",
     7: "dw_ring_bf16_kernel<0,0> (middle-layer weight gradient)",
@@ -49,24 +68,49 @@ KCLASS_NAMES = {
     13: "pair_ring_bf16_kernel<top> (top hidden layer + output layer: dX and dW roles)",
     14: "pair_ring_bf16_kernel<bottom> (layer 1 + first layer, P_0 rebuilt: dX and dW roles)",
 }
+# kernel symbol of each class at the M shape (C = 2 inputs, O = 1 output), as rocprofv3 names it
+KCLASS_SYMBOL = {
+    "bf16": {1: "siren::nt_bf16_kernel<0, 256, false, false>", 2: "siren::nt_bf16_kernel<1, 256, false, false>",
+             3: "siren::tn_dw_kernel<1, false, false>", 4: "siren::fused_fwd_reg_kernel<2, 1>",
+             5: "siren::bwd_ring_bf16_kernel", 6: "siren::dx_ring_bf16_kernel<0, false, false, 0>",
+             7: "siren::dw_ring_bf16_kernel<0, 0>", 8: "siren::dx_ring_bf16_kernel<2, true, true, 0>",
+             9: "siren::dw_ring_bf16_kernel<2, 0>", 10: "siren::dx_ring_bf16_kernel<0, false, false, 1>",
+             11: "siren::dw_ring_bf16_kernel<0, 1>",
+             12: "siren::pair_ring_bf16_kernel<0, false, false, 0, 0>",
+             13: "siren::pair_ring_bf16_kernel<0, false, false, 1, 0>",
+             14: "siren::pair_ring_bf16_kernel<2, true, true, 0, 2>"},
+    "fp32": {1: "siren::nt_f32_kernel<0>", 2: "siren::nt_f32_kernel<1>", 3: "siren::tn_dw_kernel<0, false, false>"},
+}
+CONFIG_DEFAULT_STEPS = {"m": (50, 10), "c1": (50, 10), "c2": (50, 10), "c3": (20, 5), "c4": (10, 3)}
+C4 = dict(num_fourier_features=8, kl_weight=2.78e-8, fw_weight=6.4e-6, lr=5.57e-5, fourier_features_scale=21,
+          latent_dim=128, hidden_features_hyper=128, hidden_layers_hyper=2, hidden_layers=3, hidden_features=256,
+          conv_kernel_size=7, num_conv_res_blocks=5, w0=30, slices=32, res=128)
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--side", type=int, default=512)
-    p.add_argument("--hidden", type=int, default=256)
-    p.add_argument("--num-hidden-layers", type=int, default=3)
-    p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--steps", type=int, default=None)
+    p.add_argument("--warmup", type=int, default=None)
+    p.add_argument("--config", default="m", choices=["m", "c1", "c2", "c3", "c4"])
+    p.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    p.add_argument("--precision", default=None, choices=["bf16", "fp32"],
+                   help="SIREN arithmetic (default: bf16, fp32 for c3)")
+    p.add_argument("--no-graph", action="store_true", help="time eager steps instead of a hipGraph replay")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-psnr", action="store_true")
-    p.add_argument("--cpu-budget-s", type=float, default=20.0)
-    return p.parse_args()
+    p.add_argument("--no-other-configs", action="store_true")
+    p.add_argument("--cpu-budget-s", type=float, default=12.0, help="CPU seconds per config of the CPU baseline")
+    a = p.parse_args()
+    st, wu = CONFIG_DEFAULT_STEPS[a.config]
+    a.steps = st if a.steps is None else a.steps
+    a.warmup = wu if a.warmup is None else a.warmup
+    if a.precision is None:
+        a.precision = "fp32" if a.config == "c3" else "bf16"
+    return a
 
 
-def setup_dist(args):
+def setup_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -76,23 +120,71 @@ def setup_dist(args):
     return world, rank, torch.device("cuda", local)
 
 
-def build_step(args, dev, rank, world):
+# ------------------------------------------------------------------------------ algorithmic counts
+def siren_fwd_flops(dims):
+    """Per coordinate: sum over layers of 2 in out (SURVEY.md §8(a) 'Algorithmic counts')."""
+    return sum(2 * dims[i] * dims[i + 1] for i in range(len(dims) - 1))
+
+
+def siren_grad_flops(dims):
+    """Per coordinate, forward with C tangent streams (layer 0's tangent is W_0's column, no GEMM)."""
+    C, S = dims[0], 1 + dims[0]
+    return 2 * C * dims[1] + S * sum(2 * dims[i] * dims[i + 1] for i in range(1, len(dims) - 1))
+
+
+def encoder_flops_fwd(k, res_blocks, latent, res):
+    """ConvImgEncoder forward per slice (modules.py:340-380, 433-450): conv_theta 2->latent/2 (k),
+    conv latent/2->latent (k), res_blocks x 2 convs latent->latent (5x5), 1x1, FC over pixels."""
+    px = res * res
+    f = 2 * k * k * 2 * (latent // 2) * px + 2 * k * k * (latent // 2) * latent * px
+    f += res_blocks * 2 * (2 * 25 * latent * latent * px) + 2 * latent * latent * px + 2 * latent * px
+    return f
+
+
+# ------------------------------------------------------------------------------ workloads
+class Workload:
+    """step(): one training step; coords: coordinate samples per rank per step; flops: algorithmic
+    FLOPs per rank per step of the SIREN (encoder separately); kdims: the SIREN dims."""
+
+    def __init__(self, name, step, coords, flops, dims, precision, workload, data, extra=None):
+        self.name, self.step, self.coords, self.flops, self.dims = name, step, coords, flops, dims
+        self.precision, self.workload, self.data, self.extra = precision, workload, data, extra or {}
+
+
+def build_fit(cfg, args, dev, rank, world, precision):
+    """M / C1 / C2: the train_img.py fit (image_mse, Adam 1e-4) of one image."""
     from siren_mri_amd import dataio, loss_functions, modules, training
-    from siren_mri_amd.training_ddp import GradAllReducer
+    from siren_mri_amd.training_ddp import GradAllReducer, shard_rows
+    side, nh = {"m": (512, 3), "c1": (64, 1), "c2": (256, 3)}[cfg]
     torch.manual_seed(0)
-    model = modules.SingleBVPNet(type="sine", mode="mlp", hidden_features=args.hidden,
-                                 num_hidden_layers=args.num_hidden_layers, sidelength=(args.side, args.side),
-                                 precision=args.precision).to(dev)
-    coords = dataio.get_mgrid(args.side)[None].to(dev)
-    img = dataio.smooth_random_image(args.side, seed=rank)
-    gt = {"img": torch.from_numpy(img).reshape(1, -1, 1).to(dev)}
+    model = modules.SingleBVPNet(type="sine", mode="mlp", hidden_features=256, num_hidden_layers=nh,
+                                 sidelength=(side, side), precision=precision).to(dev)
+    grid = dataio.get_mgrid(side)
+    if cfg == "m":
+        img = torch.from_numpy(dataio.smooth_random_image(side, seed=rank if args.scaling == "weak" else 0))
+        data = f"synthetic (smooth random {side}^2 image: 32 sinusoids; coords = get_mgrid({side}))"
+    elif cfg == "c1":
+        img = dataio.Implicit2DWrapper(dataio.Camera(), sidelength=side)[0][1]["img"]
+        data = "cameraman 64^2 (PIL bilinear), coords = get_mgrid(64)"
+    else:
+        img = dataio.irdata_image(0, side)
+        data = "IRData slice 0 (data/IRData.mat) / max, x2-1, bilinear 256^2; coords = get_mgrid(256)"
+    img = img.reshape(-1, 1)
+    if args.scaling == "strong" and world > 1:
+        lo, hi = shard_rows(grid.shape[0], rank, world)
+    else:
+        lo, hi = 0, grid.shape[0]
+    coords = grid[lo:hi][None].to(dev)
+    tgt = img[lo:hi][None].to(dev)
     opt = training.make_adam(model.parameters(), 1e-4)
     reducer = GradAllReducer(model.parameters(), op="sum") if world > 1 else None
     model_input = {"coords": coords}
 
     def step():
         out = model(model_input)
-        loss = loss_functions.image_mse(None, out, gt, high_freq=False)["img_loss"]
+        # image_mse's reduction (sum / 128^2) over this rank's coordinates: in a strong-scaling
+        # shard the partial sums over the ranks add up to the whole image's loss
+        loss = loss_functions.weighted_sse(out["model_out"], tgt)
         loss.backward()
         if reducer is not None:
             reducer()
@@ -100,98 +192,379 @@ def build_step(args, dev, rank, world):
         opt.zero_grad(set_to_none=True)
         return loss
 
-    return step, model
+    dims = [2] + [256] * (nh + 1) + [1]
+    n = hi - lo
+    wl = (f"train_img.py fit step: {side}x{side} grid{' (strong: this rank ' + str(n) + ' rows)' if args.scaling == 'strong' and world > 1 else ''}, "
+          f"SingleBVPNet {'-'.join(map(str, dims))} (w0=30), image_mse + Adam(1e-4), full batch")
+    return Workload(cfg, step, n, 3 * siren_fwd_flops(dims) * n, dims, precision, wl, data,
+                    {"optimizer": opt, "side": side})
 
 
-def kernel_model(args, kclass, p0_recompute):
-    """Algorithmic FLOPs and HBM bytes of ONE launch of a kernel class at the bench workload
-    (DESIGN.md §5): R rows, F = hidden width, e = bytes per stored activation element (2 in bf16
-    mode: 16-bit phases / bf16 gradients; 4 in fp32 mode), C = 2 inputs, O = 1 output. Bytes are
-    the kernel's essential inputs and outputs once each (split-K partial slabs are not counted:
-    they are an implementation choice, visible in the PMC traffic)."""
-    R = args.side * args.side
-    F, nh = args.hidden, args.num_hidden_layers
-    e = 2 if args.precision == "bf16" else 4
-    C, O = 2, 1
-    gemm = 2.0 * R * F * F
-    dw_out = 4 * (F * F + F)
-    if kclass == 1:            # P_l = enc(w0 (sin(P_{l-1}) W^T + b)): read P_{l-1}, write P_l
-        return gemm, R * F * 2 * e
-    if kclass in (2, 6):       # dZ_{l-1} = (dZ_l W) cos(P_{l-1}) w0: read dZ_l, P_{l-1}; write dZ_{l-1}
-        return gemm, R * F * 3 * e
-    if kclass in (3, 7):       # dW_l = dZ_l^T sin(P_{l-1}), db_l: read dZ_l, P_{l-1}; write dW_l, db_l
-        return gemm, R * F * 2 * e + dw_out
-    if kclass == 4:            # x in, the kept sine layers' phases out, y out
-        planes = nh if p0_recompute else nh + 1
-        return 2.0 * R * (C * F + nh * F * F + F * O), R * (4 * C + planes * F * e + 4 * O)
-    if kclass == 5:            # 6 + 7 in one pass
-        return 2 * gemm, R * F * 3 * e + dw_out
-    if kclass == 8:            # read dZ_1, x (P_0 rebuilt from x, or read); write dx, dW_0/db_0
-        return (gemm + 3 * 2.0 * R * C * F,
-                R * (F * e + 4 * C + 4 * C + (0 if p0_recompute else F * e)) + 4 * (F * C + F))
-    if kclass == 9:            # read dZ_1, x; write dW_1, db_1
-        return gemm + 2.0 * R * C * F, R * (F * e + 4 * C) + dw_out
-    if kclass == 10:           # read P_top, dy, P_{top-1}; write dZ_{top-1}
-        return gemm + 2.0 * R * F * O, R * (3 * F * e + 4 * O)
-    if kclass == 11:           # read P_top, dy, P_{top-1}; write dW, db, dW_L, db_L
-        return gemm + 4.0 * R * F * O, R * (2 * F * e + 4 * O) + dw_out + 4 * (F * O + O)
-    if kclass == 12:           # 6 + 7 with dZ_l and P_{l-1} read once per pair
-        return 2 * gemm, R * F * 3 * e + dw_out
-    if kclass == 13:           # 10 + 11: read P_top, dy, P_{top-1} once; write dZ_{top-1}, dW, dW_L
-        return (2 * gemm + 6.0 * R * F * O,
-                R * (3 * F * e + 4 * O) + dw_out + 4 * (F * O + O))
-    if kclass == 14:           # 8 + 9: read dZ_1, x once; write dx, dW_1, dW_0
-        return (2 * gemm + 4 * 2.0 * R * C * F,
-                R * (F * e + 4 * C + 4 * C) + dw_out + 4 * (F * C + F))
-    raise ValueError(kclass)
+def build_c3(args, dev, rank, world, precision):
+    """C3: train_poisson_grad_img.py-style fit, gradients_mse at 512^2, fp32."""
+    from siren_mri_amd import dataio, loss_functions, modules, training
+    from siren_mri_amd.training_ddp import GradAllReducer, shard_rows
+    side = 512
+    torch.manual_seed(0)
+    model = modules.SingleBVPNet(type="sine", hidden_features=256, num_hidden_layers=3, precision=precision).to(dev)
+    _, gt = dataio.Implicit2DWrapper(dataio.Camera(), sidelength=side, compute_diff="gradients")[0]
+    grid = dataio.get_mgrid(side)
+    lo, hi = shard_rows(grid.shape[0], rank, world) if (args.scaling == "strong" and world > 1) else (0, grid.shape[0])
+    coords = grid[lo:hi][None].to(dev)
+    gtg = {"gradients": gt["gradients"][lo:hi][None].to(dev)}
+    opt = training.make_adam(model.parameters(), 1e-4)
+    reducer = GradAllReducer(model.parameters(), op="mean") if world > 1 else None
+    model_input = {"coords": coords}
+
+    def step():
+        out = model(model_input)
+        loss = loss_functions.gradients_mse(out, gtg)["gradients_loss"]
+        loss.backward()
+        if reducer is not None:
+            reducer()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    dims = [2, 256, 256, 256, 256, 1]
+    n = hi - lo
+    return Workload("c3", step, n, 3 * siren_grad_flops(dims) * n, dims, precision,
+                    f"train_poisson_grad_img.py-style fit step: {side}x{side} grid, SingleBVPNet 5x256, "
+                    "gradients_mse (analytic gradient + its double backward) + Adam(1e-4)",
+                    "cameraman 512^2, gt gradients = sobel(10 img) along axes 1, 2 (dataio.py:779-782)",
+                    {"optimizer": opt})
 
 
-def timed_region(step, steps, world):
+def c4_batch(dev, n_slices, seed=0):
+    from siren_mri_amd import dataio
+    ds = dataio.SyntheticMRIKspace(n_slices=max(n_slices, 1), image_resolution=(C4["res"],) * 2, seed=seed)
+    coord = dataio.Implicit2DWrapper(ds, sidelength=(C4["res"],) * 2, image=False)
+    gen = dataio.ImageGeneralizationWrapper(coord, test_sparsity="CS_cartesian", generalization_mode="conv_cnp")
+    items = [gen[i] for i in range(n_slices)]
+    inp = {k: torch.stack([it[0][k] for it in items]).to(dev) for k in items[0][0]}
+    gt = {k: torch.stack([it[1][k] for it in items]).to(dev) for k in items[0][1]}
+    return inp, gt
+
+
+def build_c4(args, dev, rank, world, precision, encoder_precision="bf16"):
+    from functools import partial
+    from siren_mri_amd import loss_functions, meta_modules, training
+    from siren_mri_amd.features import GaussianFourierFeatureTransform
+    from siren_mri_amd.training_ddp import GradAllReducer
+    torch.manual_seed(0)
+    nff = C4["num_fourier_features"]
+    model = meta_modules.ConvolutionalNeuralProcessImplicit2DHypernetFourierFeatures(
+        in_features=2 * nff, out_features=2, image_resolution=(C4["res"],) * 2, fourier_features_size=2 * nff,
+        latent_dim=C4["latent_dim"], hidden_features=C4["hidden_features"],
+        hyper_hidden_features=C4["hidden_features_hyper"], hyper_hidden_layers=C4["hidden_layers_hyper"],
+        num_hidden_layers=C4["hidden_layers"], conv_kernel_size=C4["conv_kernel_size"],
+        num_conv_res_blocks=C4["num_conv_res_blocks"], w0=C4["w0"], precision=precision,
+        encoder_precision=encoder_precision).to(dev)
+    torch.manual_seed(0)
+    ff = GaussianFourierFeatureTransform(2, nff, scale=C4["fourier_features_scale"], device=dev)
+    inp, gt = c4_batch(dev, C4["slices"], seed=rank)
+    loss_fn = partial(loss_functions.image_hypernetwork_loss, None, C4["kl_weight"], C4["fw_weight"])
+    opt = training.make_adam(model.parameters(), C4["lr"])
+    reducer = GradAllReducer(model.parameters(), op="mean") if world > 1 else None
+    params = [p for p in model.parameters() if p.requires_grad]
+
+    def step():
+        mi = dict(inp)
+        mi["coords"] = ff(inp["coords"])
+        out = model(mi)
+        losses = loss_fn(out, gt)
+        loss = sum(v.mean() for v in losses.values())
+        if reducer is not None:
+            reducer.begin()
+        loss.backward()
+        if reducer is not None:
+            reducer()
+        torch.nn.utils.clip_grad_norm_(params, max_norm=1.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    dims = [2 * nff] + [C4["hidden_features"]] * (C4["hidden_layers"] + 1) + [2]
+    n = C4["slices"] * C4["res"] ** 2
+    enc = 3 * encoder_flops_fwd(C4["conv_kernel_size"], C4["num_conv_res_blocks"], C4["latent_dim"], C4["res"]) * C4["slices"]
+    return Workload("c4", step, n, 3 * siren_fwd_flops(dims) * n, dims, precision,
+                    f"train_mri_neural_process step (reference config hyperoptIV_homebrew): {C4['slices']} slices "
+                    f"of {C4['res']}^2 k-space per GPU, conv encoder ({encoder_precision}, k=7, 5 res blocks) -> "
+                    f"hypernetwork -> SIREN {'-'.join(map(str, dims))} per-slice weights ({precision}) -> DC, "
+                    "image_hypernetwork_loss, clip 1.0, Adam(5.57e-5)",
+                    "synthetic k-space (IRData slices x flips/rotations + seeded ellipses, fftshift(fft2)), "
+                    "seeded CS-Cartesian masks, FF B = randn(2, 8) * 21 (seed 0)",
+                    {"optimizer": opt, "encoder_flops_per_step": enc, "encoder_precision": encoder_precision,
+                     "model": model, "inp": inp})
+
+
+def build(cfg, args, dev, rank, world, precision=None):
+    precision = precision or ("fp32" if cfg == "c3" else args.precision)
+    if cfg in ("m", "c1", "c2"):
+        return build_fit(cfg, args, dev, rank, world, precision)
+    if cfg == "c3":
+        return build_c3(args, dev, rank, world, precision)
+    return build_c4(args, dev, rank, world, precision)
+
+
+# ------------------------------------------------------------------------------ timing
+def enable_graph_mode(wl):
+    opt = wl.extra.get("optimizer")
+    if opt is not None and hasattr(opt, "enable_graph_mode"):
+        opt.enable_graph_mode()
+
+
+def capture(step, nsteps):
+    """A hipGraph of `nsteps` consecutive steps (captured on a side stream, torch's private pool)."""
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(nsteps):
+                step()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    return g
+
+
+def timed(fn, world):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
+    fn()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     return time.perf_counter() - t0
 
 
-def cpu_baseline(args, budget_s):
-    """The CPU oracle (oracle/siren_oracle.py, the reference algorithm on PyTorch-CPU fp32)
-    running the same 512^2 5x256 fit step, timed on this host's cores."""
-    from oracle import siren_oracle as orc
-    torch.manual_seed(0)
-    model = orc.OracleSiren(hidden_features=args.hidden, num_hidden_layers=args.num_hidden_layers, seed=0)
-    coords = orc.get_mgrid(args.side)[None]
-    from siren_mri_amd import dataio
-    gt = {"img": torch.from_numpy(dataio.smooth_random_image(args.side, seed=0)).reshape(1, -1, 1)}
-    opt = torch.optim.Adam(lr=1e-4, params=model.parameters())
+def max_over_ranks(v, dev, world):
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
-    def step():
-        out = model({"coords": coords})
-        loss = orc.image_mse(None, out, gt, high_freq=False)["img_loss"]
-        loss.backward()
-        opt.step()
-        opt.zero_grad()
 
-    step()  # warm-up
+def run_timed(wl, args, dev, world, kclass=None, max_launches=4096):
+    """Warm-up, then EXACTLY args.steps timed steps (one replay of a K-step hipGraph, or K eager
+    steps); with kclass, that kernel class's launches inside the timed region are timed by HIP
+    event pairs (captured into the graph). Returns (elapsed_s, graph_used, KernelTimer or None)."""
+    from siren_mri_amd import _native
+    use_graph = not args.no_graph
+    for _ in range(max(args.warmup, 3 if use_graph else 0)):
+        wl.step()
+    torch.cuda.synchronize()
+    kt = None
+    if use_graph:
+        try:
+            enable_graph_mode(wl)
+            wl.step()  # an eager step in graph mode creates the optimizer's device step counter
+            g1 = capture(wl.step, 1)
+            for _ in range(2):
+                g1.replay()
+            torch.cuda.synchronize()
+            if kclass is not None:
+                kt = _native.KernelTimer(kclass, max_launches=max_launches)
+                kt.__enter__()
+            gk = capture(wl.step, args.steps)
+            elapsed = timed(gk.replay, world)
+            if kt is not None:
+                kt.__exit__(None, None, None)
+            return elapsed, True, kt
+        except Exception as e:  # noqa: BLE001 - reported, then timed eagerly
+            print(f"bench: hipGraph capture failed ({type(e).__name__}: {e}); timing eager steps", file=sys.stderr)
+            if kt is not None:
+                _native.lib().siren_timing_disable()
+            kt = None
+            torch.cuda.synchronize()
+    if kclass is not None:
+        kt = _native.KernelTimer(kclass, max_launches=max_launches)
+        kt.__enter__()
+
+    def loop():
+        for _ in range(args.steps):
+            wl.step()
+    elapsed = timed(loop, world)
+    if kt is not None:
+        kt.__exit__(None, None, None)
+    return elapsed, False, kt
+
+
+def dominant_class(wl):
+    """The kernel class with the largest time per step (3 eager steps per class; every class is one
+    template instantiation at a given shape, so its average launch is one rocprofv3 row)."""
+    from siren_mri_amd import _native
+    totals = {}
+    for kc in sorted(KCLASS_NAMES):
+        with _native.KernelTimer(kc) as t:
+            for _ in range(3):
+                wl.step()
+        if t.launches:
+            totals[kc] = (t.total_ms / 3, t.launches // 3)
+    return totals
+
+
+def kernel_flops(wl, kclass):
+    """Algorithmic FLOPs of ONE launch of a kernel class (bf16 fused path): R rows
+    of the launch's weight sets, F = hidden width, C inputs, O outputs, nh hidden 256x256 layers."""
+    d = wl.dims
+    R, C, F, O, nh = wl.coords, d[0], d[1], d[-1], len(d) - 3
+    gemm = 2.0 * R * F * F
+    table = {
+        1: gemm, 2: gemm, 3: gemm, 5: 2 * gemm, 6: gemm, 7: gemm, 12: 2 * gemm,
+        4: 2.0 * R * (C * F + nh * F * F + F * O),                  # the whole forward
+        8: gemm + 3 * 2.0 * R * C * F, 9: gemm + 2.0 * R * C * F,
+        10: gemm + 2.0 * R * F * O, 11: gemm + 4.0 * R * F * O,
+        13: 2 * gemm + 6.0 * R * F * O,                              # top pair: dZ, dW + output layer
+        14: 2 * gemm + 4 * 2.0 * R * C * F,                          # bottom pair: dZ_1, dW_1 + layer 0
+    }
+    return table[kclass]
+
+
+def traffic_from_profile(kclass, wl, side):
+    """HBM bytes per launch of the kernel from the committed PMC pass (profiles/pmc_traffic.json:
+    FETCH_SIZE + WRITE_SIZE per launch, gfx950 correction applied by tools/pmc_summary.py), or None
+    when this workload/kernel was not profiled."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    sym = KCLASS_SYMBOL.get(wl.precision, {}).get(kclass)
+    if sym is None or not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        nh = len(wl.dims) - 3
+        ent = d.get(f"{wl.precision}:{side}:{wl.dims[1]}:{nh}", {}).get(sym)
+        return None if ent is None else round(ent["bytes"] / 1e9, 4)
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+# ------------------------------------------------------------------------------ CPU baseline
+def cpu_threads():
+    """Threads for the CPU baseline: os.cpu_count(), bounded by what this process
+    may actually run on (its affinity mask and its cgroup CPU quota — on the GPU box os.cpu_count()
+    reports the whole machine while the job owns a share of it)."""
+    n = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else n
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    use = min(n, aff, quota or n)
+    return use, {"os_cpu_count": n, "affinity": aff, "cgroup_quota_cpus": quota}
+
+
+def cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return platform.processor() or "unknown"
+
+
+def _cpu_time(step, budget_s, warm=3, timed_n=5):
+    """3 warm-ups + 5 timed steps, fewer when a step exceeds budget_s / 8."""
+    t0 = time.perf_counter()
+    step()
+    first = time.perf_counter() - t0
+    w = 1 + (warm - 1 if first * (warm + timed_n) <= budget_s else 0)
+    for _ in range(w - 1):
+        step()
     times = []
     t_start = time.perf_counter()
-    while len(times) < 5 and (time.perf_counter() - t_start) < budget_s:
+    while len(times) < timed_n and (len(times) < 2 or time.perf_counter() - t_start + first <= budget_s):
         t0 = time.perf_counter()
         step()
         times.append(time.perf_counter() - t0)
-    med = float(np.median(times))
-    return {"value": args.side * args.side / med, "unit": "coord-samples/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": f"oracle SingleBVPNet restatement (PyTorch-CPU fp32, autograd, Adam), 1 warm-up + "
-                      f"{len(times)} timed full {args.side}x{args.side} steps, median {med:.3f} s/step, "
-                      f"{torch.get_num_threads()} threads on {os.cpu_count()} visible CPUs"}
+    return float(np.median(times)), w, len(times)
 
 
+def cpu_step(cfg):
+    """The CPU oracle (oracle/siren_oracle.py: the reference algorithm on PyTorch-CPU fp32) running
+    one training step of config cfg; returns (step, coords per step, sample description)."""
+    from oracle import siren_oracle as orc
+    from siren_mri_amd import dataio
+    if cfg in ("m", "c1", "c2"):
+        side, nh = {"m": (512, 3), "c1": (64, 1), "c2": (256, 3)}[cfg]
+        model = orc.OracleSiren(hidden_features=256, num_hidden_layers=nh, seed=0)
+        coords = orc.get_mgrid(side)[None]
+        img = (torch.from_numpy(dataio.smooth_random_image(side, seed=0)) if cfg == "m" else
+               dataio.Implicit2DWrapper(dataio.Camera(), sidelength=side)[0][1]["img"] if cfg == "c1" else
+               dataio.irdata_image(0, side))
+        gt = {"img": img.reshape(1, -1, 1)}
+        opt = torch.optim.Adam(lr=1e-4, params=model.parameters())
+
+        def step():
+            loss = orc.image_mse(None, model({"coords": coords}), gt, high_freq=False)["img_loss"]
+            loss.backward()
+            opt.step()
+            opt.zero_grad()
+        return step, side * side, f"full {side}^2 step, {nh + 2} linear layers"
+    if cfg == "c3":
+        model = orc.OracleSiren(hidden_features=256, num_hidden_layers=3, seed=0)
+        coords = orc.get_mgrid(512)[None]
+        _, gt = dataio.Implicit2DWrapper(dataio.Camera(), sidelength=512, compute_diff="gradients")[0]
+        gtg = {"gradients": gt["gradients"][None]}
+        opt = torch.optim.Adam(lr=1e-4, params=model.parameters())
+
+        def step():
+            loss = orc.gradients_mse(model({"coords": coords}), gtg)["gradients_loss"]
+            loss.backward()
+            opt.step()
+            opt.zero_grad()
+        return step, 512 * 512, "full 512^2 gradients_mse step (autograd double backward)"
+    # c4: the encoder + hypernetwork modules on the CPU, the hypo-net SIREN through the oracle
+    from functools import partial
+    from siren_mri_amd import meta_modules
+    nff, ns = C4["num_fourier_features"], 2
+    torch.manual_seed(0)
+    model = meta_modules.ConvolutionalNeuralProcessImplicit2DHypernetFourierFeatures(
+        in_features=2 * nff, out_features=2, image_resolution=(C4["res"],) * 2, fourier_features_size=2 * nff,
+        latent_dim=C4["latent_dim"], hidden_features=C4["hidden_features"],
+        hyper_hidden_features=C4["hidden_features_hyper"], hyper_hidden_layers=C4["hidden_layers_hyper"],
+        num_hidden_layers=C4["hidden_layers"], conv_kernel_size=C4["conv_kernel_size"],
+        num_conv_res_blocks=C4["num_conv_res_blocks"], w0=C4["w0"])
+    B = torch.randn(2, nff) * C4["fourier_features_scale"]
+    inp, gt = c4_batch(torch.device("cpu"), ns)
+    L = C4["hidden_layers"] + 2
+    opt = torch.optim.Adam(lr=C4["lr"], params=model.parameters())
+    loss_fn = partial(orc.image_hypernetwork_loss, None, C4["kl_weight"], C4["fw_weight"])
+
+    def step():
+        emb = model.encoder(inp["img_sparse"])
+        hp = model.hyper_net(emb)
+        x = orc.fourier_features(inp["coords"], B)
+        y = orc.siren_forward(x, [(hp[f"net.net.{i}.0.weight"], hp[f"net.net.{i}.0.bias"]) for i in range(L)])
+        y = orc.data_consistency(y, inp["img_sparse"], inp["dc_mask"])
+        losses = loss_fn({"model_out": y, "latent_vec": emb, "hypo_params": hp}, gt)
+        sum(v.mean() for v in losses.values()).backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        opt.zero_grad()
+    return step, ns * C4["res"] ** 2, f"{ns} of the 32 slices per step (rate per coordinate sample), fp32"
+
+
+def cpu_baseline(cfg, budget_s):
+    threads, cpus = cpu_threads()
+    torch.set_num_threads(threads)
+    step, coords, what = cpu_step(cfg)
+    med, warm, n = _cpu_time(step, budget_s)
+    return {"value": coords / med, "unit": "coord-samples/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle restatement (PyTorch-CPU fp32, autograd, Adam): {what}; {warm} warm-up + {n} timed "
+                      f"steps, median {med:.3f} s/step; {torch.get_num_threads()} threads",
+            "cpu_model": cpu_model(), **cpus}
+
+
+# ------------------------------------------------------------------------------ PSNR leg
 def psnr_check(args, dev):
     """64^2 cameraman, 3 hidden layers, Adam 1e-4, seed 0: PSNR at steps 0/50/100/200/500 vs the
     reference's trajectory recorded in tests/golden/psnr_c1.npz (image_mse, high_freq=False)."""
@@ -222,144 +595,154 @@ def psnr_check(args, dev):
             "config": "64x64 cameraman, SingleBVPNet 3 hidden x 256, Adam 1e-4, seed 0"}
 
 
-# kernel symbol of each class at the bench shape (C = 2 inputs, O = 1 output), as rocprofv3 names it
-KCLASS_SYMBOL = {
-    "bf16": {1: "siren::nt_bf16_kernel<0, 256, false, false>", 2: "siren::nt_bf16_kernel<1, 256, false, false>",
-             3: "siren::tn_dw_kernel<1, false, false>", 4: "siren::fused_fwd_pipe_kernel<2, 1>",
-             5: "siren::bwd_ring_bf16_kernel", 6: "siren::dx_ring_bf16_kernel<0, false, false, 0>",
-             7: "siren::dw_ring_bf16_kernel<0, 0>", 8: "siren::dx_ring_bf16_kernel<2, true, true, 0>",
-             9: "siren::dw_ring_bf16_kernel<2, 0>", 10: "siren::dx_ring_bf16_kernel<0, false, false, 1>",
-             11: "siren::dw_ring_bf16_kernel<0, 1>",
-             12: "siren::pair_ring_bf16_kernel<0, false, false, 0, 0>",
-             13: "siren::pair_ring_bf16_kernel<0, false, false, 1, 0>",
-             14: "siren::pair_ring_bf16_kernel<2, true, true, 0, 2>"},
-    "fp32": {1: "siren::nt_f32_kernel<0>", 2: "siren::nt_f32_kernel<1>", 3: "siren::tn_dw_kernel<0, false, false>"},
-}
+# ------------------------------------------------------------------------------ per-config line
+def measure(cfg, args, dev, rank, world, with_kernels=True):
+    from siren_mri_amd import _native
+    wl = build(cfg, args, dev, rank, world)
+    for _ in range(2):
+        wl.step()
+    torch.cuda.synchronize()
+    totals = dominant_class(wl) if (with_kernels and wl.precision == "bf16") else {}
+    dom = max(totals, key=lambda k: totals[k][0]) if totals else None
+    per_step = totals[dom][1] if dom else 0
+    elapsed, graph, kt = run_timed(wl, args, dev, world, kclass=dom, max_launches=max(64, (per_step + 1) * args.steps))
+    elapsed = max_over_ranks(elapsed, dev, world)
+    ms = elapsed / args.steps * 1e3
+    step_flops = wl.flops
+    peak = PEAK[wl.precision]
+    res = {"config": cfg, "ms_per_step": ms, "coords_per_gpu_step": wl.coords,
+           "value": world * wl.coords * args.steps / elapsed, "graph": graph, "precision": wl.precision,
+           "workload": wl.workload, "data": wl.data,
+           "step_roofline": {"bound": "mfma", "flops_per_step_per_gpu": step_flops,
+                             "achieved_tflops": round(step_flops / (ms * 1e-3) / 1e12, 2),
+                             "peak_tflops": peak / 1e12, "frac": round(step_flops / (ms * 1e-3) / peak, 4)}}
+    if "encoder_flops_per_step" in wl.extra:
+        res["encoder"] = {"flops_per_step_per_gpu": wl.extra["encoder_flops_per_step"],
+                          "precision": wl.extra["encoder_precision"],
+                          "share_of_step_flops": round(wl.extra["encoder_flops_per_step"] /
+                                                       (wl.extra["encoder_flops_per_step"] + step_flops), 4)}
+        res["encoder"].update(time_encoder(wl, args))
+    if dom is not None and kt is not None and kt.launches:
+        avg_s = kt.avg_ms * 1e-3
+        flops = kernel_flops(wl, dom)
+        side = wl.extra.get("side")
+        traffic = traffic_from_profile(dom, wl, side) if side else None
+        res["roofline"] = {
+            "bound": "mfma", "kernel": KCLASS_NAMES[dom], "kernel_symbol": KCLASS_SYMBOL.get(wl.precision, {}).get(dom),
+            "achieved": round(flops / avg_s / 1e12, 2), "peak": round(peak / 1e12, 1), "unit": "TFLOP/s",
+            "frac": round(flops / avg_s / peak, 4), "flops_per_launch": flops,
+            "avg_launch_ms": round(kt.avg_ms, 4), "launches": kt.launches,
+            "timing": "HIP event pairs around every launch of the kernel inside the timed region "
+                      + ("(captured into the hipGraph)" if graph else "(eager steps)"),
+            "traffic": traffic, "traffic_unit": "GB per launch (HBM, rocprofv3 PMC FETCH_SIZE + WRITE_SIZE)",
+            "hbm_gbps_of_traffic": round(traffic * 1e9 / avg_s / 1e9, 1) if traffic else None,
+            "kernel_ms_per_step": {KCLASS_NAMES[k].split(" ")[0] + f"[{k}]": round(v[0], 4) for k, v in totals.items()}}
+        if traffic:
+            # algorithmic I/O of the whole path: 12 B per coordinate (coords 8 B,
+            # target 4 B) + parameters, gradients and Adam state once each (5 x 4 B per parameter)
+            nparam = sum(wl.dims[i] * wl.dims[i + 1] + wl.dims[i + 1] for i in range(len(wl.dims) - 1))
+            alg = 12 * wl.coords + 20 * nparam
+            res["roofline"]["traffic_vs_algorithmic_io"] = {
+                "algorithmic_io_bytes_per_step": alg,
+                "dominant_kernel_traffic_over_step_io": round(traffic * 1e9 / alg, 1)}
+    return res, wl, dom, totals
 
 
-def traffic_from_profile(kclass, args):
-    """HBM bytes per launch of the kernel from the committed PMC pass (profiles/pmc_traffic.json,
-    written by tools/pmc_bench.sh + tools/pmc_summary.py: FETCH_SIZE x2 (gfx950 correction) +
-    WRITE_SIZE, KB -> bytes), or None when this workload/kernel was not profiled."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    sym = KCLASS_SYMBOL.get(args.precision, {}).get(kclass)
-    if sym is None or not os.path.exists(path):
-        return None
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        ent = d.get(f"{args.precision}:{args.side}:{args.hidden}:{args.num_hidden_layers}", {}).get(sym)
-        return None if ent is None else round(ent["bytes"] / 1e9, 4)
-    except (OSError, ValueError, KeyError):
-        return None
+def time_encoder(wl, args):
+    """The conv encoder's forward + backward alone on the same batch (HIP events), for the C4 split."""
+    model, inp = wl.extra["model"], wl.extra["inp"]
+    enc = model.encoder
+    for _ in range(2):
+        enc(inp["img_sparse"]).sum().backward()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = max(3, min(args.steps, 10))
+    e0.record()
+    for _ in range(n):
+        enc(inp["img_sparse"]).sum().backward()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / n
+    model.zero_grad(set_to_none=False)
+    f = wl.extra["encoder_flops_per_step"]
+    return {"fwd_bwd_ms": round(ms, 3), "achieved_tflops": round(f / (ms * 1e-3) / 1e12, 1),
+            "frac_of_bf16_peak" if wl.extra["encoder_precision"] == "bf16" else "frac_of_fp32_peak":
+                round(f / (ms * 1e-3) / PEAK[wl.extra["encoder_precision"]], 4)}
 
 
 def main():
     args = parse()
-    world, rank, dev = setup_dist(args)
+    world, rank, dev = setup_dist()
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     from siren_mri_amd import _native
     _native.load_library()
 
-    step, model = build_step(args, dev, rank, world)
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    # pick the dominant kernel (largest time per step) from a short untimed probe (3 steps per
-    # class; every class is one kernel template instantiation, so its average launch duration is
-    # the rocprofv3 row of that kernel)
-    totals = {}
-    for kc in sorted(KCLASS_NAMES):
-        with _native.KernelTimer(kc) as t:
-            for _ in range(3):
-                step()
-        if t.launches:
-            totals[kc] = t.total_ms
-    dom = max(totals, key=totals.get)
-    p0_recompute = args.precision == "bf16" and bool(_native.get_option("fused_forward"))
-    if bool(_native.get_option("fused_forward_reg")):  # class 4 is the register-resident forward
-        KCLASS_NAMES[4] = ("fused_fwd_reg_kernel (whole forward, activations in registers: layer 0 on the "
-                           "f32 MFMA, hidden and output layers on the f16 MFMA)")
-        KCLASS_SYMBOL["bf16"][4] = "siren::fused_fwd_reg_kernel<2, 1>"
-
-    with _native.KernelTimer(dom, max_launches=max(64, 8 * args.steps)) as kt:
-        elapsed = timed_region(step, args.steps, world)
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
-
-    coords_per_rank = args.side * args.side
-    value = world * coords_per_rank * args.steps / elapsed
-    avg_s = kt.avg_ms * 1e-3
-    flops, nbytes = kernel_model(args, dom, p0_recompute)
-    mfma_peak, _ = PEAK[args.precision]
-    # the binding roofline: whichever resource the algorithmic work needs longer on at peak
-    if nbytes / HBM_PEAK >= flops / mfma_peak:
-        bound, work, peak, unit, scale = "hbm", nbytes, HBM_PEAK, "GB/s", 1e9
-    else:
-        bound, work, peak, unit, scale = "mfma", flops, mfma_peak, "TFLOP/s", 1e12
-    achieved = work / avg_s if avg_s > 0 else float("nan")
-    roofline = {"bound": bound, "kernel": KCLASS_NAMES[dom], "kernel_symbol": KCLASS_SYMBOL.get(args.precision, {}).get(dom),
-                "achieved": round(achieved / scale, 2),
-                "peak": round(peak / scale, 1), "unit": unit, "frac": round(achieved / peak, 4),
-                "traffic": traffic_from_profile(dom, args),
-                "traffic_unit": "GB per launch (HBM, PMC)",
-                "algorithmic_bytes_per_launch": nbytes, "flops_per_launch": flops,
-                "achieved_tflops": round(flops / avg_s / 1e12, 2) if avg_s > 0 else None,
-                "avg_launch_ms": round(kt.avg_ms, 4), "launches": kt.launches,
-                "kernel_ms_per_step": {KCLASS_NAMES[k].split(" ")[0] + f"[{k}]": round(v / 3, 4)
-                                       for k, v in totals.items()}}
+    res, wl, dom, totals = measure(args.config, args, dev, rank, world)
+    nparams = sum(p.numel() for p in wl.extra["optimizer"].param_groups[0]["params"])
     result = {
         "metric": "coord-samples/sec/step, 5x256 SIREN on 512^2 grid; PSNR vs ref",
-        "value": value,
+        "value": res["value"],
         "unit": "coord-samples/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": res["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": args.precision,
+        "dtype": wl.precision,
         "precision_detail": ("forward hidden GEMMs fp16 x fp16 -> fp32, backward GEMMs bf16 x bf16 -> fp32, "
                              "phases stored as 16-bit revolutions, weights / loss / Adam fp32"
-                             if args.precision == "bf16" else "fp32 throughout"),
-        "data": "synthetic (smooth random 512^2 image per rank: 32 sinusoids; coords = get_mgrid(512))",
-        "config": {"workload": f"train_img.py fit step: {args.side}x{args.side} coordinate grid per GPU, "
-                               f"SingleBVPNet 2-{'-'.join([str(args.hidden)] * (args.num_hidden_layers + 1))}-1 "
-                               f"(w0=30), image_mse + Adam(1e-4), full batch",
-                   "coords_per_gpu_step": coords_per_rank, "global_batch": world * coords_per_rank,
-                   "parallelism": f"dp{world} (coordinate-sharded, one gradient all-reduce per step)"},
-        "roofline": roofline,
+                             if wl.precision == "bf16" else "fp32 throughout"),
+        "data": res["data"],
+        "config": {"workload": res["workload"], "config": args.config,
+                   "coords_per_gpu_step": wl.coords, "global_batch": world * wl.coords,
+                   "parallelism": f"dp{world} ({'strong: one grid split by rows' if args.scaling == 'strong' else 'weak: one problem per GPU'}"
+                                  f", one gradient all-reduce per step)",
+                   "params": nparams, "timed_region": "hipGraph replay of K captured steps" if res["graph"] else "K eager steps"},
+        "step_roofline": res["step_roofline"],
     }
+    if "roofline" in res:
+        result["roofline"] = res["roofline"]
+    if "encoder" in res:
+        result["encoder"] = res["encoder"]
     # north_star's per-kernel target: bf16-MFMA utilisation of the fused SineLayer GEMM (the whole
-    # forward: every layer's GEMM + bias + sine in one launch) = its algorithmic FLOPs / its average
-    # launch time / the dense bf16 peak, from the same HIP-event timer, measured after the timed region
-    if 4 in totals and dom != 4:
-        with _native.KernelTimer(4, max_launches=64) as ft:
-            for _ in range(10):
-                step()
-        f_flops, f_bytes = kernel_model(args, 4, p0_recompute)
-        f_s = ft.avg_ms * 1e-3
-        result_fwd = {"kernel": KCLASS_NAMES[4], "kernel_symbol": KCLASS_SYMBOL.get(args.precision, {}).get(4),
-                      "flops_per_launch": f_flops, "avg_launch_ms": round(ft.avg_ms, 4), "launches": ft.launches,
-                      "achieved_tflops": round(f_flops / f_s / 1e12, 2), "mfma_peak_tflops": mfma_peak / 1e12,
-                      "mfma_frac": round(f_flops / f_s / mfma_peak, 4),
-                      "hbm_gbps": round(f_bytes / f_s / 1e9, 1), "hbm_frac": round(f_bytes / f_s / HBM_PEAK, 4)}
-    elif dom == 4:
-        result_fwd = {"kernel": KCLASS_NAMES[4], "mfma_frac": round(flops / avg_s / mfma_peak, 4),
-                      "achieved_tflops": round(flops / avg_s / 1e12, 2), "avg_launch_ms": round(kt.avg_ms, 4)}
-    else:
-        result_fwd = None
-    if result_fwd is not None:
-        result["fused_sine_gemm"] = result_fwd
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, args.cpu_budget_s)
-    if rank == 0 and world == 1 and not args.no_psnr:
+    # forward: every layer's GEMM + bias + sine in one launch), from the same HIP-event timer
+    if wl.precision == "bf16" and 4 in totals:
+        if dom == 4 and "roofline" in res:
+            f_ms, f_n = res["roofline"]["avg_launch_ms"], res["roofline"]["launches"]
+        else:
+            with _native.KernelTimer(4, max_launches=64) as ft:
+                for _ in range(10):
+                    wl.step()
+            f_ms, f_n = ft.avg_ms, ft.launches
+        f_flops = kernel_flops(wl, 4)
+        result["fused_sine_gemm"] = {
+            "kernel": KCLASS_NAMES[4], "kernel_symbol": KCLASS_SYMBOL["bf16"][4], "flops_per_launch": f_flops,
+            "avg_launch_ms": round(f_ms, 4), "launches": f_n, "achieved_tflops": round(f_flops / (f_ms * 1e-3) / 1e12, 2),
+            "mfma_peak_tflops": PEAK["bf16"] / 1e12, "mfma_frac": round(f_flops / (f_ms * 1e-3) / PEAK["bf16"], 4)}
+    del wl
+    torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and not args.no_psnr and args.config == "m":
         result["psnr"] = psnr_check(args, dev)
+    if world == 1 and not args.no_other_configs and args.config == "m":
+        oargs = argparse.Namespace(**vars(args))
+        others = {}
+        for cfg in ("c1", "c2", "c3", "c4"):
+            oargs.steps, oargs.warmup = CONFIG_DEFAULT_STEPS[cfg]
+            try:
+                r, owl, _, _ = measure(cfg, oargs, dev, rank, world, with_kernels=(cfg != "c4"))
+                others[cfg] = r
+                del owl
+            except Exception as e:  # noqa: BLE001 - a failing side config must not lose the metric line
+                others[cfg] = {"error": f"{type(e).__name__}: {e}"}
+            torch.cuda.empty_cache()
+        result["configs"] = others
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget_s)
+        if args.config == "m" and not args.no_other_configs:
+            result["cpu_baselines"] = {c: cpu_baseline(c, args.cpu_budget_s) for c in ("c1", "c2", "c3", "c4")}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

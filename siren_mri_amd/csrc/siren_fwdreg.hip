@@ -49,6 +49,10 @@ constexpr int FREG_SYNC = SIREN_FREG_SYNC;
 #define SIREN_FREG_STORE_AUX 0
 #endif
 static_assert(FREG_SYNC == 1 || FREG_SYNC == 2, "ring sync interval");
+// diagnostic builds: what follows each phase-code store (0 nothing, 1 16 wait states, 2 vmcnt(0))
+#ifndef SIREN_FREG_STORE_FENCE
+#define SIREN_FREG_STORE_FENCE 0
+#endif
 // Vector-memory operations a wave has issued after the ring refill it must see land (every block
 // issues two phase stores — a null tensor's are still issued and dropped by their resource — and
 // every refill of a slot two DMAs):
@@ -276,6 +280,11 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
       return;
     }
     __builtin_amdgcn_raw_buffer_store_b128(c, p_rsrc(pl), p_voff, pfb * 64 + half * 32, SIREN_FREG_STORE_AUX);
+#if SIREN_FREG_STORE_FENCE == 1
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+#elif SIREN_FREG_STORE_FENCE == 2
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
   };
 
   // Epilogue of one accumulator, in 8 parts of 2 elements (part p: elements 2p, 2p + 1, packed

@@ -86,6 +86,18 @@ class _WeightedSSE(torch.autograd.Function):
         return out.view(ctx.shape), None, None, None
 
 
+def weighted_sse(pred, tgt, weight=_KSPACE_WEIGHT, mask=None):
+    """sum |m (pred - tgt)|^2 * weight over any shape (image_mse's reduction without the
+    lin2img reshape): the loss of a coordinate shard of an image in a sharded fit, whose partial
+    sums over the ranks' shards add up to image_mse of the whole image."""
+    if pred.is_cuda and pred.dtype == torch.float32 and tgt.dtype == torch.float32 and not tgt.requires_grad:
+        return _WeightedSSE.apply(pred, tgt.to(pred.device), mask, weight)
+    diff = pred - tgt
+    if mask is not None:
+        diff = mask * diff
+    return (diff.abs() ** 2).sum() * weight
+
+
 def image_mse(mask, model_output, gt, high_freq=True):
     """Weighted k-space SSE: sum |m * (pred - gt)|^2 / 128^2 (a sum over the batch)."""
     pred = lin2img(model_output["model_out"])

@@ -70,19 +70,22 @@ class HyperNetwork(nn.Module):
 
 
 class ConvolutionalNeuralProcessImplicit2DHypernetFourierFeatures(nn.Module):
-    """k-space neural process: conv encoder -> HyperNetwork -> SIREN (batched weights) -> DC."""
+    """k-space neural process: conv encoder -> HyperNetwork -> SIREN (batched weights) -> DC.
+    precision: the SIREN stack's arithmetic (native kernels); encoder_precision: the conv
+    encoder's ('fp32' = reference, 'bf16' = MIOpen bf16 channels-last, see ConvImgEncoder)."""
 
     def __init__(self, in_features, out_features, image_resolution=None, partial_conv=False,
                  fourier_features_size=512, latent_dim=256, hidden_features=256, num_hidden_layers=5,
                  hyper_hidden_features=512, hyper_hidden_layers=1, conv_kernel_size=3,
-                 num_conv_res_blocks=4, w0=30, precision=None):
+                 num_conv_res_blocks=4, w0=30, precision=None, encoder_precision="fp32"):
         super().__init__()
         self.dc = data_consistency.DataConsistencyInKspace(noise_lvl=None)
         if partial_conv:
             raise NotImplementedError("PartialConvImgEncoder is outside the SIREN path")
         self.encoder = modules.ConvImgEncoder(channel=2, image_resolution=image_resolution,
                                               hidden_size=latent_dim, kernel_size=conv_kernel_size,
-                                              num_conv_res_blocks=num_conv_res_blocks)
+                                              num_conv_res_blocks=num_conv_res_blocks,
+                                              precision=encoder_precision)
         self.hypo_net = modules.SingleBVPNet(out_features=out_features, type="sine",
                                              sidelength=image_resolution,
                                              in_features=fourier_features_size,

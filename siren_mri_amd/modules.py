@@ -291,11 +291,21 @@ class Conv2dResBlock(nn.Module):
 
 class ConvImgEncoder(nn.Module):
     """modules.py:340-380: conv stem -> residual blocks -> 1x1 -> per-channel FC over pixels.
-    Plain PyTorch-ROCm (MIOpen convolutions); the SIREN it feeds is the native path."""
+    Plain PyTorch-ROCm (MIOpen convolutions); the SIREN it feeds is the native path.
 
-    def __init__(self, channel, image_resolution, hidden_size=256, kernel_size=3, num_conv_res_blocks=4):
+    precision='fp32' is the reference's arithmetic. precision='bf16'  runs
+    the convolutions in bf16 on MIOpen with channels-last (NHWC) activations and weights — the
+    layout MIOpen's bf16 implicit-GEMM kernels take without transposes — under autocast, with
+    fp32 master weights and gradients; the final per-channel FC over the 128^2 pixels (a 16,384-term
+    dot product per channel) stays fp32."""
+
+    def __init__(self, channel, image_resolution, hidden_size=256, kernel_size=3, num_conv_res_blocks=4,
+                 precision="fp32"):
         super().__init__()
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"ConvImgEncoder precision {precision!r}: 'fp32' or 'bf16'")
         self.hidden_size = hidden_size
+        self.precision = precision
         padding = kernel_size // 2
         self.conv_theta = nn.Conv2d(channel, hidden_size // 2, kernel_size, 1, padding)
         self.relu = nn.ReLU(inplace=True)
@@ -306,8 +316,21 @@ class ConvImgEncoder(nn.Module):
         self.relu_2 = nn.ReLU(inplace=True)
         self.fc = nn.Linear(image_resolution[0] * image_resolution[1], 1)
         self.image_resolution = image_resolution
+        self._nhwc = False
 
     def forward(self, I):
+        if self.precision == "bf16" and I.is_cuda:
+            if not self._nhwc:
+                # conv weights to channels-last once (their .grad follows the parameter's layout)
+                for m in self.modules():
+                    if isinstance(m, nn.Conv2d):
+                        m.weight.data = m.weight.data.contiguous(memory_format=torch.channels_last)
+                self._nhwc = True
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                o = self.relu(self.conv_theta(I.contiguous(memory_format=torch.channels_last)))
+                o = self.relu_2(self.cnn(o))
+            o = o.float().contiguous().view(o.shape[0], self.hidden_size, -1)
+            return self.fc(o).squeeze(-1)
         o = self.relu(self.conv_theta(I))
         o = self.cnn(o)
         return self.fc(self.relu_2(o).view(o.shape[0], self.hidden_size, -1)).squeeze(-1)

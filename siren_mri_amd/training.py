@@ -18,7 +18,7 @@ Deliberate deviations:
     reference's input() raises EOFError and nothing is lost — here a FileExistsError says so,
     unless overwrite=True (or hyperopt_run=True, as in the reference) was passed;
   * with accumulation_steps > 1 and a data-parallel grad_reducer, each micro-step's exchange
-    carries only the gradient added since the previous exchange (see _reduce_micro_step).
+    carries only the gradient added since the previous exchange (see the note above validate).
 """
 from __future__ import annotations
 
@@ -100,15 +100,18 @@ def make_adam(params, lr):
 def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_checkpoint, model_dir, loss_fn,
           summary_fn, val_dataloader=None, double_precision=False, clip_grad=False, use_lbfgs=False,
           loss_schedules=None, fourier_feat_transformer=None, device=None, hyperopt_run=False,
-          accumulation_steps=1, grad_reducer=None, write_outputs=True, overwrite=False):
+          accumulation_steps=1, grad_reducer=None, write_outputs=True, overwrite=False, model_dir_hook=None):
     """Fit `model` (training.py:19-146). `grad_reducer`, if given, is the data-parallel gradient
-    exchange of training_ddp (see _reduce_micro_step for when it runs). With write_outputs=False
-    (non-zero data-parallel ranks) nothing is written to disk."""
+    exchange of training_ddp (see the note above validate for when it runs). With write_outputs=False
+    (non-zero data-parallel ranks) nothing is written to disk. model_dir_hook(model_dir) runs once the
+    model directory has been prepared (writing ranks only)."""
     optim = make_adam(model.parameters(), lr)
     dev = model_device(model) if device is None else torch.device(device)
     if write_outputs:
         summaries_dir, checkpoints_dir = prepare_model_dir(model_dir, hyperopt_run, overwrite)
         writer = make_writer(summaries_dir)
+        if model_dir_hook is not None:
+            model_dir_hook(model_dir)
     else:
         checkpoints_dir, writer = None, _NullWriter()
 
@@ -150,11 +153,12 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
             train_loss = train_loss / accumulation_steps
             last_micro = (step + 1) % accumulation_steps == 0 or (step + 1 == n_batches)
             window_start = step % accumulation_steps == 0
-            if grad_reducer is not None and clip_grad and not window_start:
-                grad_reducer.snapshot()
+            exchange = grad_reducer is not None and (clip_grad or last_micro)
+            if exchange:
+                grad_reducer.begin(delta=clip_grad and not window_start)
             train_loss.backward()
-            if grad_reducer is not None:
-                _reduce_micro_step(grad_reducer, clip_grad, last_micro, window_start)
+            if exchange:
+                grad_reducer()
             if clip_grad:
                 max_norm = 1.0 if isinstance(clip_grad, bool) else clip_grad
                 torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
@@ -180,23 +184,16 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
     return None if last_loss is None else float(last_loss.detach()) * accumulation_steps
 
 
-def _reduce_micro_step(grad_reducer, clip_grad, last_micro, window_start):
-    """When the data-parallel exchange runs inside an accumulation window (training.py:90-103).
-
-    The reference's DDP all-reduces (averages) the accumulated .grad after every backward
-    (training_ddp.py:96-109, no no_sync), and clips every micro-step. Exchanging the whole
-    accumulated gradient each micro-step is right only for an average and only because the earlier
-    part is already identical on every rank; with a sum it would add the earlier micro-steps W times
-    over. So:
-      * without clipping, only the micro-step followed by optim.step() exchanges (DDP no_sync
-        semantics: one collective per optimizer step, identical result for 'mean' and 'sum');
-      * with clipping (which needs the exchanged gradient every micro-step, as in the reference),
-        each exchange carries only what this backward added (the .grad minus the snapshot taken
-        before it), so 'sum' and 'mean' both give sum/average over ranks of every micro-step."""
-    if clip_grad:
-        grad_reducer(delta=not window_start)
-    elif last_micro:
-        grad_reducer()
+# When the data-parallel exchange runs inside an accumulation window (training.py:90-103): the
+# reference's DDP all-reduces (averages) the accumulated .grad after every backward
+# (training_ddp.py:96-109, no no_sync) and clips every micro-step. Exchanging the whole accumulated
+# gradient each micro-step is right only for an average and only because the earlier part is
+# already identical on every rank; with a sum it would add the earlier micro-steps W times over. So:
+#   * without clipping, only the micro-step followed by optim.step() exchanges (DDP no_sync
+#     semantics: one collective per optimizer step, identical result for 'mean' and 'sum');
+#   * with clipping (which needs the exchanged gradient every micro-step, as in the reference), each
+#     exchange after the window's first carries only what its backward added (GradAllReducer.begin
+#     with delta=True), so 'sum' and 'mean' both give sum/average over ranks of every micro-step.
 
 
 @torch.no_grad()

@@ -4,10 +4,11 @@ One process per GPU over torch.distributed ('nccl' = RCCL on ROCm, over xGMI; 'g
 The reference wraps the model in DDP (train_mri_neural_process_ddp.py:238) and lets its
 backward hooks all-reduce ~25 MB buckets. Here the exchange is explicit and minimal:
 
-  * GradAllReducer flattens every parameter gradient into ONE contiguous buffer after backward
-    and issues ONE all-reduce (averaged, DDP semantics, or summed, for coordinate-sharded fits
-    whose loss is a sum over coordinates) — for the 5x256 SIREN that is a single 793.6 KB
-    message per step; for the config-5 hypernetwork model (31.3 M params) a few large buckets.
+  * GradAllReducer keeps every parameter gradient in a persistent flat bucket buffer and issues
+    one all-reduce per bucket (averaged, DDP semantics, or summed, for coordinate-sharded fits
+    whose loss is a sum over coordinates) — for the 5x256 SIREN a single 793.6 KB message per
+    step; for the config-5 hypernetwork model (31.3 M params) 32 MB buckets launched from
+    backward hooks as soon as each is complete, overlapping the rest of the backward.
   * parameters are broadcast from rank 0 once at construction (the DDP constructor's broadcast).
   * shard_rows / DistributedSampler split the coordinate grid or the slice list across ranks.
 
@@ -45,20 +46,34 @@ def shard_rows(n_rows: int, rank: int, world_size: int):
 
 
 class GradAllReducer:
-    """Single flattened all-reduce of all parameter gradients (see module docstring)."""
+    """Bucketed gradient all-reduce over persistent flat buffers (see the module docstring).
 
-    def __init__(self, params, op: str = "mean", group=None, bucket_bytes: int = 256 << 20,
-                 broadcast: bool = True):
+    * Every parameter's gradient lives in a slot of a flat per-bucket buffer (``p.grad`` is a view
+      of it after the first exchange), so an exchange moves no gradient bytes besides the
+      collective itself; a gradient autograd created as a fresh tensor is copied into its slot once.
+    * Buckets hold parameters in reverse registration order (autograd produces the last layers'
+      gradients first). After ``begin()``, a post-accumulate-grad hook counts the gradients of each
+      bucket as autograd finishes them and launches that bucket's all-reduce (async, RCCL's own
+      stream) as soon as it is complete, so the exchange overlaps the rest of the backward;
+      ``__call__`` launches whatever is left (unused parameters' slots are zero-filled, their
+      ``.grad`` stays None), waits, and applies the mean.
+    * Accumulation windows with a per-micro-step exchange (clipping, training_ddp.py:96-109):
+      ``begin(delta=True)`` (or ``snapshot()``) makes the next exchange carry only what the coming
+      backward adds. For 'mean' nothing is needed (the window's earlier part is identical on every
+      rank, so its average is itself); for 'sum' the accumulated gradient is scaled by 1/world in
+      place, so the sum over ranks restores it once — no copy of the gradient set is kept."""
+
+    def __init__(self, params, op: str = "mean", group=None, bucket_bytes: int = 32 << 20,
+                 broadcast: bool = True, overlap: bool = True):
         self.params = [p for p in params if p.requires_grad]
         if op not in ("mean", "sum"):
             raise ValueError("op must be 'mean' or 'sum'")
         self.op = op
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        # group parameters into buckets of <= bucket_bytes (one for small models)
         self.buckets = []
         cur, size = [], 0
-        for p in self.params:
+        for p in reversed(self.params):
             nbytes = p.numel() * p.element_size()
             if cur and size + nbytes > bucket_bytes:
                 self.buckets.append(cur)
@@ -67,63 +82,113 @@ class GradAllReducer:
             size += nbytes
         if cur:
             self.buckets.append(cur)
-        self._flat = [None] * len(self.buckets)
-        self._base = None  # snapshot of the accumulated gradient (micro-step deltas)
+        self._flat = []
+        self._views = {}
+        self._slot = {}
+        for i, bucket in enumerate(self.buckets):
+            numel = sum(p.numel() for p in bucket)
+            flat = torch.zeros(numel, dtype=bucket[0].dtype, device=bucket[0].device)
+            self._flat.append(flat)
+            off = 0
+            for p in bucket:
+                self._views[p] = flat[off:off + p.numel()].view_as(p)
+                self._slot[p] = i
+                off += p.numel()
+        self._armed = False
+        self._ready = [0] * len(self.buckets)
+        self._seen = [set() for _ in self.buckets]
+        self._work = [None] * len(self.buckets)
+        self._hooks = []
         if broadcast and self.world > 1:
             with torch.no_grad():
                 for p in self.params:
                     dist.broadcast(p.data, src=0, group=group)
+        if overlap and self.world > 1:
+            for p in self.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    def _bind(self, p):
+        """Move p's gradient into its slot (no-op when it already is the slot)."""
+        v = self._views[p]
+        g = p.grad
+        if g is None:
+            return False
+        if g.data_ptr() != v.data_ptr():
+            v.copy_(g)
+            p.grad = v
+        return True
+
+    @torch.no_grad()
+    def _on_grad(self, p):
+        if not self._armed:
+            return
+        i = self._slot[p]
+        if self._work[i] is not None or p in self._seen[i]:
+            return
+        self._bind(p)
+        self._seen[i].add(p)
+        if len(self._seen[i]) == len(self.buckets[i]):
+            self._launch(i)
+
+    def _launch(self, i):
+        self._work[i] = dist.all_reduce(self._flat[i], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     @torch.no_grad()
     def snapshot(self):
-        """Remember the current (already exchanged) gradient; the next call with delta=True
-        exchanges only what was added since."""
+        """The next exchange carries only what is added to the gradients from now on."""
+        if self.world == 1 or self.op == "mean":
+            return
+        for p in self.params:
+            if p.grad is not None:
+                self._bind(p)
+                p.grad.mul_(1.0 / self.world)
+
+    def begin(self, delta: bool = False):
+        """Arm the backward hooks for an exchange after the coming backward (optional: without it
+        everything is exchanged by __call__)."""
         if self.world == 1:
             return
-        self._base = [[None if p.grad is None else p.grad.detach().clone() for p in b] for b in self.buckets]
+        if delta:
+            self.snapshot()
+        self._seen = [set() for _ in self.buckets]
+        self._work = [None] * len(self.buckets)
+        self._armed = True
 
     @torch.no_grad()
     def __call__(self, delta: bool = False):
         if self.world == 1:
             return
-        base = self._base if delta else None
-        self._base = None
+        if not self._armed:
+            self.begin(delta)
+        self._armed = False
+        used = {}
         for i, bucket in enumerate(self.buckets):
-            grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in bucket]
-            if base is not None:
-                grads = [g if b is None else g - b for g, b in zip(grads, base[i])]
-            numel = sum(g.numel() for g in grads)
-            flat = self._flat[i]
-            if flat is None or flat.numel() != numel or flat.device != grads[0].device:
-                flat = torch.empty(numel, dtype=grads[0].dtype, device=grads[0].device)
-                self._flat[i] = flat
-            off = 0
-            views = []
-            for g in grads:
-                n = g.numel()
-                flat[off:off + n].copy_(g.reshape(-1))
-                views.append((off, n))
-                off += n
-            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+            if self._work[i] is None:
+                for p in bucket:
+                    if p not in self._seen[i]:
+                        used[p] = self._bind(p)
+                        if not used[p]:
+                            self._views[p].zero_()
+                self._launch(i)
+        for i, w in enumerate(self._work):
+            w.wait()
             if self.op == "mean":
-                flat.mul_(1.0 / self.world)
-            for j, (p, (o, n)) in enumerate(zip(bucket, views)):
-                red = flat[o:o + n].view_as(p)
-                if base is not None and base[i][j] is not None:
-                    red = red + base[i][j]
-                if p.grad is None:
-                    p.grad = red.clone()
-                else:
-                    p.grad.copy_(red)
+                self._flat[i].mul_(1.0 / self.world)
+        for p in self.params:
+            if used.get(p, True) and p.grad is None:
+                p.grad = self._views[p]
+        self._work = [None] * len(self.buckets)
 
 
 def train_ddp(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_checkpoint, model_dir, loss_fn,
               summary_fn, val_dataloader=None, double_precision=False, clip_grad=False, use_lbfgs=False,
               loss_schedules=None, fourier_feat_transformer=None, device=0, ddp_run=False, accumulation_steps=1,
-              grad_op: str = "mean"):
+              grad_op: str = "mean", model_dir_hook=None):
     """training_ddp.py:23-152: the train loop with a per-step gradient all-reduce, the sampler's
     epoch set for shuffling, and rank-0-only I/O. `model` may be a plain module (preferred) or a
-    torch DDP wrapper (then DDP performs the exchange and no extra all-reduce is issued)."""
+    torch DDP wrapper (then DDP performs the exchange and no extra all-reduce is issued).
+    model_dir_hook(model_dir), if given, runs on rank 0 right after the model directory is prepared
+    (files that must exist before the first step, e.g. the Fourier matrices)."""
     is_ddp_wrapper = isinstance(model, torch.nn.parallel.DistributedDataParallel)
     module = model.module if is_ddp_wrapper else model
     rank = dist.get_rank() if dist.is_initialized() else 0
@@ -154,5 +219,5 @@ def train_ddp(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til
                          # rank 0 replaces model_dir unconditionally, as training_ddp.py:29-33 does
                          hyperopt_run=True,
                          accumulation_steps=accumulation_steps, grad_reducer=reducer,
-                         write_outputs=(rank == 0))
+                         write_outputs=(rank == 0), model_dir_hook=model_dir_hook)
     return out

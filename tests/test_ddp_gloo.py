@@ -232,3 +232,58 @@ def test_model_dir_not_deleted_without_consent(tmp_path, monkeypatch):
     assert (d / "checkpoints" / "model_final.pth").read_bytes() == b"keep"
     prepare_model_dir(str(d), overwrite=True)
     assert not (d / "checkpoints" / "model_final.pth").exists()
+
+
+def _overlap_worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    from siren_mri_amd.training_ddp import ddp_setup, GradAllReducer
+    ddp_setup(rank, world, backend="gloo")
+    model = orc.OracleSiren(hidden_features=32, num_hidden_layers=2, seed=rank + 1)
+    # ~4 KB buckets: several buckets, so the early (top-layer) ones launch from the hooks
+    red = GradAllReducer(model.parameters(), op="mean", bucket_bytes=4096)
+    coords = orc.get_mgrid(8)[None] * (1 + rank)
+    launched_during_backward = []
+    for step in range(2):
+        red.begin()
+        loss = model({"coords": coords})["model_out"].square().sum()
+        loss.backward()
+        launched_during_backward.append(sum(w is not None for w in red._work))
+        red()
+        grads = [p.grad.detach().clone() for p in model.parameters()]
+        in_slots = all(any(p.grad.data_ptr() == v.data_ptr() for v in [red._views[p]]) for p in model.parameters())
+        # the reference: average of both ranks' gradients of the same (broadcast) parameters
+        ref = []
+        for r in range(world):
+            m2 = orc.OracleSiren(hidden_features=32, num_hidden_layers=2, seed=0)
+            m2.load_state_dict(model.state_dict())
+            m2({"coords": orc.get_mgrid(8)[None] * (1 + r)})["model_out"].square().sum().backward()
+            ref.append([p.grad for p in m2.parameters()])
+        err = max(orc.norm_rel(g, (a + b) / 2) for g, a, b in zip(grads, ref[0], ref[1]))
+        with torch.no_grad():
+            for p in model.parameters():
+                p -= 1e-3 * p.grad
+        model.zero_grad(set_to_none=True)
+    out_q.put((rank, len(red.buckets), launched_during_backward, in_slots, err))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bucketed_allreduce_overlaps_backward_without_copies():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for nb, launched, in_slots, err in res.values():
+        assert nb > 2
+        assert all(k == nb for k in launched), launched  # every bucket launched from the hooks
+        assert in_slots
+        assert err < 1e-6

@@ -65,13 +65,18 @@ def test_train_mri_neural_process_ddp_script_files(tmp_path):
     final = tmp_path / "run" / "checkpoints" / "model_final.pth"
     assert final.exists() and (tmp_path / "run" / "current_B_DDP_mp0.pt").exists()
     B = torch.load(tmp_path / "run" / "current_B_DDP_mp0.pt", weights_only=True)
-    assert B.shape == (2, 60)
+    assert B.shape == (2, 8)  # the reference's active config: 8 Fourier features
     sd = torch.load(final, weights_only=True)
     assert not any(k.startswith("module.") for k in sd)  # loadable by the reference's test scripts
     # the reference's DDP-wrapper form of the same file resumes too
     from siren_mri_amd import checkpoints
     prefixed = tmp_path / "prefixed.pth"
     torch.save({"module." + k: v for k, v in sd.items()}, prefixed)
-    launch("resume", "--checkpoint_path", str(prefixed))
+    launch("resume", "--checkpoint_path", str(prefixed), "--b_path", str(tmp_path / "run" / "current_B_DDP_mp0.pt"))
     assert (tmp_path / "resume" / "checkpoints" / "model_final.pth").exists()
+    # the resumed run trains with the saved B (not a fresh draw) and writes it again
+    assert torch.equal(torch.load(tmp_path / "resume" / "current_B_DDP_mp0.pt", weights_only=True), B)
+    # a resume straight from the run's own checkpoint finds B in its run directory
+    launch("run", "--checkpoint_path", str(final), "--overwrite")
+    assert torch.equal(torch.load(tmp_path / "run" / "current_B_DDP_mp0.pt", weights_only=True), B)
     assert checkpoints.strip_ddp_prefix(torch.load(prefixed, weights_only=True)).keys() == sd.keys()
