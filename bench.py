@@ -22,9 +22,13 @@ Scaling: weak (default; every rank owns its own full-size problem: a 512^2 block
 image, or its own 32 slices) or strong (--scaling strong: ONE global grid split into contiguous
 row blocks by training_ddp.shard_rows; the summed gradient all-reduce makes it the single-GPU fit).
 
-The timed region replays a hipGraph holding exactly K captured steps (--no-graph: K eager steps);
-the dominant kernel's launches inside it are bracketed by captured HIP event pairs on the launch
-stream, so its average duration comes from the timed region itself.
+Timed regions (each EXACTLY K steps between barrier + synchronize): one replay of a hipGraph
+holding K captured steps, and K eager steps. --timing auto (default) runs both and reports the
+faster as `value` (both in config.ms_per_step_by_region): graph replay removes the host's
+per-step launch work, which decides small grids (C1, C2), while eager back-to-back launches are
+faster for the 512^2 step on ROCm 7 (graph kernel nodes add a few us each). The dominant
+kernel's launches are bracketed by HIP event pairs on its launch stream in the eager region (ROCm
+reports no elapsed time between events recorded inside a graph).
 
 Prints ONE JSON line on rank 0: value (coord-samples/s, whole job), roofline of the dominant
 kernel (MFMA-bound per SURVEY.md §8(d): algorithmic FLOPs per launch / launch time / dense peak;
@@ -96,7 +100,10 @@ def parse():
     p.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     p.add_argument("--precision", default=None, choices=["bf16", "fp32"],
                    help="SIREN arithmetic (default: bf16, fp32 for c3)")
-    p.add_argument("--no-graph", action="store_true", help="time eager steps instead of a hipGraph replay")
+    p.add_argument("--timing", default="auto", choices=["auto", "graph", "eager"],
+                   help="timed region: a hipGraph replay of K captured steps, K eager steps, or (auto) both, "
+                        "reporting the faster")
+    p.add_argument("--no-graph", action="store_true", help="same as --timing eager")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-psnr", action="store_true")
     p.add_argument("--no-other-configs", action="store_true")
@@ -107,6 +114,8 @@ def parse():
     a.warmup = wu if a.warmup is None else a.warmup
     if a.precision is None:
         a.precision = "fp32" if a.config == "c3" else "bf16"
+    if a.no_graph:
+        a.timing = "eager"
     return a
 
 
@@ -348,16 +357,18 @@ def max_over_ranks(v, dev, world):
 
 
 def run_timed(wl, args, dev, world, kclass=None, max_launches=4096):
-    """Warm-up, then EXACTLY args.steps timed steps (one replay of a K-step hipGraph, or K eager
-    steps); with kclass, that kernel class's launches inside the timed region are timed by HIP
-    event pairs (captured into the graph). Returns (elapsed_s, graph_used, KernelTimer or None)."""
+    """Warm-up, then timed regions of EXACTLY args.steps steps each: one replay of a hipGraph
+    holding the K captured steps (--timing graph/auto), and K eager steps (--timing eager/auto),
+    during which the dominant kernel class (kclass) is timed by HIP event pairs on its launch
+    stream around each launch (ROCm reports no elapsed time between events recorded inside a
+    graph). Returns (elapsed_s of the reported region, region name, KernelTimer or None,
+    {region: elapsed_s})."""
     from siren_mri_amd import _native
-    use_graph = not args.no_graph
-    for _ in range(max(args.warmup, 3 if use_graph else 0)):
+    for _ in range(args.warmup):
         wl.step()
     torch.cuda.synchronize()
-    kt = None
-    if use_graph:
+    regions = {}
+    if args.timing in ("graph", "auto"):
         try:
             enable_graph_mode(wl)
             wl.step()  # an eager step in graph mode creates the optimizer's device step counter
@@ -365,20 +376,13 @@ def run_timed(wl, args, dev, world, kclass=None, max_launches=4096):
             for _ in range(2):
                 g1.replay()
             torch.cuda.synchronize()
-            if kclass is not None:
-                kt = _native.KernelTimer(kclass, max_launches=max_launches)
-                kt.__enter__()
             gk = capture(wl.step, args.steps)
-            elapsed = timed(gk.replay, world)
-            if kt is not None:
-                kt.__exit__(None, None, None)
-            return elapsed, True, kt
+            regions["graph"] = timed(gk.replay, world)
+            del gk, g1
         except Exception as e:  # noqa: BLE001 - reported, then timed eagerly
             print(f"bench: hipGraph capture failed ({type(e).__name__}: {e}); timing eager steps", file=sys.stderr)
-            if kt is not None:
-                _native.lib().siren_timing_disable()
-            kt = None
             torch.cuda.synchronize()
+    kt = None
     if kclass is not None:
         kt = _native.KernelTimer(kclass, max_launches=max_launches)
         kt.__enter__()
@@ -386,10 +390,14 @@ def run_timed(wl, args, dev, world, kclass=None, max_launches=4096):
     def loop():
         for _ in range(args.steps):
             wl.step()
-    elapsed = timed(loop, world)
+    regions["eager"] = timed(loop, world)
     if kt is not None:
         kt.__exit__(None, None, None)
-    return elapsed, False, kt
+    # the same choice on every rank: the max over ranks of each region
+    regions = {k: max_over_ranks(v, dev, world) for k, v in regions.items()}
+    name = min(regions, key=regions.get) if args.timing == "auto" else (
+        "graph" if "graph" in regions and args.timing == "graph" else "eager")
+    return regions[name], name, kt, regions
 
 
 def dominant_class(wl):
@@ -605,13 +613,15 @@ def measure(cfg, args, dev, rank, world, with_kernels=True):
     totals = dominant_class(wl) if (with_kernels and wl.precision == "bf16") else {}
     dom = max(totals, key=lambda k: totals[k][0]) if totals else None
     per_step = totals[dom][1] if dom else 0
-    elapsed, graph, kt = run_timed(wl, args, dev, world, kclass=dom, max_launches=max(64, (per_step + 1) * args.steps))
-    elapsed = max_over_ranks(elapsed, dev, world)
+    elapsed, region, kt, regions = run_timed(wl, args, dev, world, kclass=dom,
+                                             max_launches=max(64, (per_step + 1) * args.steps))
+    graph = region == "graph"
     ms = elapsed / args.steps * 1e3
     step_flops = wl.flops
     peak = PEAK[wl.precision]
     res = {"config": cfg, "ms_per_step": ms, "coords_per_gpu_step": wl.coords,
            "value": world * wl.coords * args.steps / elapsed, "graph": graph, "precision": wl.precision,
+           "ms_per_step_by_region": {k: round(v / args.steps * 1e3, 4) for k, v in regions.items()},
            "workload": wl.workload, "data": wl.data,
            "step_roofline": {"bound": "mfma", "flops_per_step_per_gpu": step_flops,
                              "achieved_tflops": round(step_flops / (ms * 1e-3) / 1e12, 2),
@@ -632,8 +642,8 @@ def measure(cfg, args, dev, rank, world, with_kernels=True):
             "achieved": round(flops / avg_s / 1e12, 2), "peak": round(peak / 1e12, 1), "unit": "TFLOP/s",
             "frac": round(flops / avg_s / peak, 4), "flops_per_launch": flops,
             "avg_launch_ms": round(kt.avg_ms, 4), "launches": kt.launches,
-            "timing": "HIP event pairs around every launch of the kernel inside the timed region "
-                      + ("(captured into the hipGraph)" if graph else "(eager steps)"),
+            "timing": "HIP event pairs on the launch stream around every launch of the kernel over a timed "
+                      "region of K eager steps" + (" (the reported value is the hipGraph region's)" if graph else ""),
             "traffic": traffic, "traffic_unit": "GB per launch (HBM, rocprofv3 PMC FETCH_SIZE + WRITE_SIZE)",
             "hbm_gbps_of_traffic": round(traffic * 1e9 / avg_s / 1e9, 1) if traffic else None,
             "kernel_ms_per_step": {KCLASS_NAMES[k].split(" ")[0] + f"[{k}]": round(v[0], 4) for k, v in totals.items()}}
@@ -700,7 +710,9 @@ def main():
                    "coords_per_gpu_step": wl.coords, "global_batch": world * wl.coords,
                    "parallelism": f"dp{world} ({'strong: one grid split by rows' if args.scaling == 'strong' else 'weak: one problem per GPU'}"
                                   f", one gradient all-reduce per step)",
-                   "params": nparams, "timed_region": "hipGraph replay of K captured steps" if res["graph"] else "K eager steps"},
+                   "params": nparams, "timed_region": ("hipGraph replay of K captured steps" if res["graph"] else "K eager steps")
+                   + (" (--timing auto: the faster of the two regions)" if args.timing == "auto" else ""),
+                   "ms_per_step_by_region": res["ms_per_step_by_region"]},
         "step_roofline": res["step_roofline"],
     }
     if "roofline" in res:

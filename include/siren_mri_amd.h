@@ -197,6 +197,32 @@ int siren_sse_backward(const float* d, const float* mask, int64_t n, int64_t mas
                        float* out, void* stream);
 
 /*
+ * k-space epilogue of the hypernetwork SIREN (configs 4/5) on the SIREN's output layout.
+ *   pred, tgt, out, dpred, d : [batch, npix, channels] float32 (SingleBVPNet model_out rows)
+ *   k0, mask                 : [batch, channels, npix] float32 (NCHW planes: img_sparse, dc_mask)
+ *   hf                       : [npix] float32 per-pixel loss mask (the 128x128 high-frequency mask
+ *                              1 - circle(r=20) of utils.py:25-40), or NULL
+ * siren_dc_forward   replaces DataConsistencyInKspace.forward (data_consistency.py:32-48):
+ *                    out = (1 - m) pred + m k0 (noise <= 0), (1 - m) pred + m (pred + noise k0) / (1 + noise)
+ *                    (the reference's operation order, no contraction: bit-identical).
+ * siren_dc_backward  its backward: dpred = g ((1 - m) [+ m / (1 + noise)]).
+ * siren_kspace_sse_forward  image_mse (loss_functions.py:66-101) of DC(pred) (k0 and mask given) or
+ *                    of pred (both NULL): d = hf (y - tgt), *loss = weight sum d^2 (deterministic
+ *                    order); workspace as siren_sse_forward's (siren_sse_workspace_bytes()).
+ * siren_kspace_sse_backward dL/dpred = g[0] scale hf d coef(m) (scale = 2 weight; coef = 1 without DC),
+ *                    i.e. image_mse's and the data consistency's backward in one pass.
+ */
+int siren_dc_forward(const float* pred, const float* k0, const float* mask, int64_t batch, int64_t npix,
+                     int channels, float noise, float* out, void* stream);
+int siren_dc_backward(const float* g, const float* mask, int64_t batch, int64_t npix, int channels, float noise,
+                      float* dpred, void* stream);
+int siren_kspace_sse_forward(const float* pred, const float* k0, const float* mask, const float* tgt,
+                             const float* hf, int64_t batch, int64_t npix, int channels, float noise, float weight,
+                             float* d, float* loss, void* workspace, int64_t ws_bytes, void* stream);
+int siren_kspace_sse_backward(const float* d, const float* mask, const float* hf, int64_t batch, int64_t npix,
+                              int channels, float noise, const float* g, float scale, float* dpred, void* stream);
+
+/*
  * Process-wide execution options (no reference counterpart; used by tests and benchmarks to
  * compare code paths). Keys:
  *   "fused_forward"  1 (default): bf16 stacks of equal power-of-two hidden widths run their

@@ -44,6 +44,10 @@ EXPORTED_SYMBOLS = (
     "siren_sse_workspace_bytes",
     "siren_sse_forward",
     "siren_sse_backward",
+    "siren_dc_forward",
+    "siren_dc_backward",
+    "siren_kspace_sse_forward",
+    "siren_kspace_sse_backward",
     "siren_last_error",
     "siren_version",
 )
@@ -163,6 +167,14 @@ def _declare(lib):
     lib.siren_sse_forward.restype = ctypes.c_int
     lib.siren_sse_backward.argtypes = [vp, vp, i64, i64, vp, f32, vp, vp]
     lib.siren_sse_backward.restype = ctypes.c_int
+    lib.siren_dc_forward.argtypes = [vp, vp, vp, i64, i64, ci, f32, vp, vp]
+    lib.siren_dc_forward.restype = ci
+    lib.siren_dc_backward.argtypes = [vp, vp, i64, i64, ci, f32, vp, vp]
+    lib.siren_dc_backward.restype = ci
+    lib.siren_kspace_sse_forward.argtypes = [vp, vp, vp, vp, vp, i64, i64, ci, f32, f32, vp, vp, vp, i64, vp]
+    lib.siren_kspace_sse_forward.restype = ci
+    lib.siren_kspace_sse_backward.argtypes = [vp, vp, vp, i64, i64, ci, f32, vp, f32, vp, vp]
+    lib.siren_kspace_sse_backward.restype = ci
     lib.siren_last_error.argtypes = []
     lib.siren_last_error.restype = ctypes.c_char_p
     lib.siren_version.argtypes = []

@@ -140,6 +140,66 @@ DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t bytes) {
                                            (int)(bytes > 0x7fffffff ? 0x7fffffff : bytes), 0x00020000);
 }
 
+// Buffer stores whose data registers may be rewritten right after them. Measured on MI355X
+// (tools/det_p0.py, profiles/r3_store_hazard.txt): in the register-resident forward, with LDS-DMA
+// traffic in flight, a buffer_store_dwordx4 followed by a VALU write of its first data VGPR
+// (v_cvt_pknorm_u16_f32, one wait state later as hipcc 7.2 schedules it; also with 16 s_nop wait
+// states in between) stored the NEW value in lanes 12-15 of each 16-lane group, nondeterministically
+// (the corrupted dword equals the one the next epilogue part writes). An s_waitcnt vmcnt(0) after
+// the store, or an s_waitcnt expcnt(0) right after it, removes it: the store's data read from the
+// VGPRs is tracked by EXP_CNT, and the compiler does not wait for it. So these stores are issued as
+// inline asm together with that wait (which returns once the data has left the VGPRs — it does
+// not wait for the write itself). The asm stores still count in vmcnt, which the kernels' counted
+// ring waits include.
+#ifndef SIREN_STORE_EXPCNT
+#define SIREN_STORE_EXPCNT 1
+#endif
+DEV void store_b128_sync(const u32x4_t& v, __amdgpu_buffer_rsrc_t r, uint32_t voff) {
+#if SIREN_STORE_EXPCNT
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_waitcnt expcnt(0)" ::"v"(v), "v"(voff), "s"(r)
+               : "memory");
+#else
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, 0, 0);
+#endif
+}
+// diagnostic builds (siren_gemm.hip ring stores): 0 builtin store, 1 store_b128_sync, 2 asm store
+// without the wait, 3 builtin store + a separate expcnt(0)
+#ifndef SIREN_GEMM_STORE
+#define SIREN_GEMM_STORE 1
+#endif
+DEV void store_b128_gemm(const u32x4_t& v, __amdgpu_buffer_rsrc_t r, uint32_t voff) {
+#if SIREN_GEMM_STORE == 1
+  store_b128_sync(v, r, voff);
+#elif SIREN_GEMM_STORE == 2
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen" ::"v"(v), "v"(voff), "s"(r) : "memory");
+#elif SIREN_GEMM_STORE == 3
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, 0, 0);
+  asm volatile("s_waitcnt expcnt(0)" ::: "memory");
+#else
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, 0, 0);
+#endif
+}
+DEV void store_b32_sync(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff) {
+#if SIREN_STORE_EXPCNT
+  asm volatile("buffer_store_dword %0, %1, %2, 0 offen\n\ts_waitcnt expcnt(0)" ::"v"(v), "v"(voff), "s"(r)
+               : "memory");
+#else
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, 0, 0);
+#endif
+}
+DEV void store_b32_gemm(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff) {
+#if SIREN_GEMM_STORE == 1
+  store_b32_sync(v, r, voff);
+#elif SIREN_GEMM_STORE == 2
+  asm volatile("buffer_store_dword %0, %1, %2, 0 offen" ::"v"(v), "v"(voff), "s"(r) : "memory");
+#elif SIREN_GEMM_STORE == 3
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, 0, 0);
+  asm volatile("s_waitcnt expcnt(0)" ::: "memory");
+#else
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, 0, 0);
+#endif
+}
+
 // The same transposing reads as inline asm, for kernels that also fill LDS by DMA
 // (global_load_lds): hipcc 7.2's wait-count pass treats the ds_read_b64_tr_b16 builtin as possibly
 // aliasing every LDS-DMA still in flight and puts an s_waitcnt vmcnt(0) in front of it, which

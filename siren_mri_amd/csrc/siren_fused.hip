@@ -505,7 +505,7 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
       ph[e] = PT::enc_scaled(z[e], ba[e], kph);
       ph[e + 4] = PT::enc_scaled(z[e + 4], bb[e], kph);
     }
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, ph), rs, (r * F + 8 * cc) * 2, 0, 0);
+    store_b128_sync(__builtin_bit_cast(u32x4_t, ph), rs, (r * F + 8 * cc) * 2);
     h16x8 hv;
 #pragma unroll
     for (int e = 0; e < 8; ++e) hv[e] = (_Float16)PT::sinp(ph[e]);
@@ -548,7 +548,7 @@ void fused_fwd_pipe_kernel(FusedFwdArgs a) {
     const int r = i / CPW, cc = CPW * (tl >> 6) + (i % CPW);
     char* hp = Hs[h] + h_off(r, cc);
     const u16x8 ph = *(const u16x8*)hp;
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, ph), rs, (r * F + 8 * cc) * 2, 0, 0);
+    store_b128_sync(__builtin_bit_cast(u32x4_t, ph), rs, (r * F + 8 * cc) * 2);
     if constexpr (!last) {
       h16x8 hv;
 #pragma unroll

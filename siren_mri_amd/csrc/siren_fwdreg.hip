@@ -49,10 +49,6 @@ constexpr int FREG_SYNC = SIREN_FREG_SYNC;
 #define SIREN_FREG_STORE_AUX 0
 #endif
 static_assert(FREG_SYNC == 1 || FREG_SYNC == 2, "ring sync interval");
-// diagnostic builds: what follows each phase-code store (0 nothing, 1 16 wait states, 2 vmcnt(0))
-#ifndef SIREN_FREG_STORE_FENCE
-#define SIREN_FREG_STORE_FENCE 0
-#endif
 // Vector-memory operations a wave has issued after the ring refill it must see land (every block
 // issues two phase stores — a null tensor's are still issued and dropped by their resource — and
 // every refill of a slot two DMAs):
@@ -279,12 +275,9 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
       __builtin_amdgcn_raw_buffer_store_b128(c, p_rsrc(pl), wave * 16384 + lane * 16, (pfb * 2 + half) * 1024, 0);
       return;
     }
-    __builtin_amdgcn_raw_buffer_store_b128(c, p_rsrc(pl), p_voff, pfb * 64 + half * 32, SIREN_FREG_STORE_AUX);
-#if SIREN_FREG_STORE_FENCE == 1
-    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-#elif SIREN_FREG_STORE_FENCE == 2
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
+    // data-read-ordered store (siren_common.h store_b128_sync: a plain store here lost its first
+    // dword to the next epilogue part's write in a few lanes, nondeterministically)
+    store_b128_sync(c, p_rsrc(pl), p_voff + pfb * 64 + half * 32);
   };
 
   // Epilogue of one accumulator, in 8 parts of 2 elements (part p: elements 2p, 2p + 1, packed
@@ -437,7 +430,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
       if (o < O) {
         float z = accO[e];
         if (a.sine_out) z = Prec<kPrecBF16>::sinr(w0 * z);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, z), ry, (yrow * O + o) * 4, 0, 0);
+        store_b32_sync(__builtin_bit_cast(uint32_t, z), ry, (yrow * O + o) * 4);
       }
     }
   };

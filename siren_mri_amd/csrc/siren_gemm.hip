@@ -1328,7 +1328,7 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
 #pragma unroll
     for (int j = 0; j < NST; ++j) {
       const u32x4_t v = *(const u32x4_t*)(base + soff[j]);
-      __builtin_amdgcn_raw_buffer_store_b128(v, rC, goff[j], 0, 0);
+      store_b128_gemm(v, rC, goff[j]);
     }
   };
 
@@ -1379,7 +1379,7 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
     for (int j = 0; j < NST; ++j) {
       const int qd = lane + 64 * j;
       const u32x4_t v = *(const u32x4_t*)(stg + (qd >> 2) * DX_STAGE_ROW + 16 * (qd & 3));
-      __builtin_amdgcn_raw_buffer_store_b128(v, rC, goff[j], 0, 0);
+      store_b128_gemm(v, rC, goff[j]);
     }
   };
 
@@ -1578,7 +1578,7 @@ DEV void dx_ring_body_v2bot(const NTArgs& a, char* smem, const int64_t t0, const
       }
       const __amdgpu_buffer_rsrc_t rD = make_rsrc(a.C ? (float*)a.C + (rowbase + t * BM) * C : nullptr,
                                                   a.C ? nval(t) * C * 4 : 0);
-      if (lane < SR * C) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rD, idx * 4, 0, 0);
+      if (lane < SR * C) store_b32_gemm(__builtin_bit_cast(uint32_t, v), rD, idx * 4);
     }
   };
 

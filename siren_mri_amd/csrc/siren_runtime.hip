@@ -15,6 +15,7 @@
 #include "siren_fwdreg.hip"
 #include "siren_adam.hip"
 #include "siren_loss.hip"
+#include "siren_kspace.hip"
 
 using namespace siren;
 
@@ -1602,6 +1603,59 @@ int siren_sse_backward(const float* d, const float* mask, int64_t n, int64_t mas
   const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(4096, cdiv(n, 4 * SSE_THREADS)));
   hipLaunchKernelGGL(sse_bwd_kernel, dim3(blocks), dim3(SSE_THREADS), 0, (hipStream_t)stream, a);
   return check_launch("sse_backward");
+}
+
+int siren_dc_forward(const float* pred, const float* k0, const float* mask, int64_t batch, int64_t npix,
+                     int channels, float noise, float* out, void* stream) {
+  if (batch < 0 || npix < 0 || channels < 1 || channels > KS_MAXC || (batch * npix > 0 && (!pred || !k0 || !mask || !out)))
+    return fail(SIREN_EINVAL, "dc_forward: bad arguments (batch=%lld, npix=%lld, channels=%d)", (long long)batch,
+                (long long)npix, channels);
+  if (batch * npix == 0) return SIREN_OK;
+  DcArgs a{pred, k0, mask, out, batch, npix, channels, noise, 0};
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(4096, cdiv(batch * npix, KS_THREADS)));
+  hipLaunchKernelGGL(dc_kernel, dim3(blocks), dim3(KS_THREADS), 0, (hipStream_t)stream, a);
+  return check_launch("dc_forward");
+}
+
+int siren_dc_backward(const float* g, const float* mask, int64_t batch, int64_t npix, int channels, float noise,
+                      float* dpred, void* stream) {
+  if (batch < 0 || npix < 0 || channels < 1 || channels > KS_MAXC || (batch * npix > 0 && (!g || !mask || !dpred)))
+    return fail(SIREN_EINVAL, "dc_backward: bad arguments");
+  if (batch * npix == 0) return SIREN_OK;
+  DcArgs a{g, nullptr, mask, dpred, batch, npix, channels, noise, 1};
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(4096, cdiv(batch * npix, KS_THREADS)));
+  hipLaunchKernelGGL(dc_kernel, dim3(blocks), dim3(KS_THREADS), 0, (hipStream_t)stream, a);
+  return check_launch("dc_backward");
+}
+
+int siren_kspace_sse_forward(const float* pred, const float* k0, const float* mask, const float* tgt,
+                             const float* hf, int64_t batch, int64_t npix, int channels, float noise, float weight,
+                             float* d, float* loss, void* workspace, int64_t ws_bytes, void* stream) {
+  if (batch < 0 || npix < 0 || channels < 1 || channels > KS_MAXC || !loss || (!k0) != (!mask) ||
+      (batch * npix > 0 && (!pred || !tgt || !d)))
+    return fail(SIREN_EINVAL, "kspace_sse_forward: bad arguments (batch=%lld, npix=%lld, channels=%d)",
+                (long long)batch, (long long)npix, channels);
+  if (!workspace || ws_bytes < siren_sse_workspace_bytes())
+    return fail(SIREN_EINVAL, "kspace_sse_forward: workspace of %lld bytes, need %lld", (long long)ws_bytes,
+                (long long)siren_sse_workspace_bytes());
+  KsseFwdArgs a{pred, k0, mask, tgt, hf, d, loss, (float*)workspace,
+                (unsigned*)((char*)workspace + SSE_MAX_BLOCKS * 4), batch, npix, channels, noise, weight};
+  // 8 coordinates per thread: few blocks for the hand-off counter (32 x 16384 coordinates: 256)
+  const unsigned blocks =
+      (unsigned)std::max<int64_t>(1, std::min<int64_t>(KS_MAX_BLOCKS, cdiv(batch * npix, 8 * KS_THREADS)));
+  hipLaunchKernelGGL(ksse_fwd_kernel, dim3(blocks), dim3(KS_THREADS), 0, (hipStream_t)stream, a);
+  return check_launch("kspace_sse_forward");
+}
+
+int siren_kspace_sse_backward(const float* d, const float* mask, const float* hf, int64_t batch, int64_t npix,
+                              int channels, float noise, const float* g, float scale, float* dpred, void* stream) {
+  if (batch < 0 || npix < 0 || channels < 1 || channels > KS_MAXC || (batch * npix > 0 && (!d || !g || !dpred)))
+    return fail(SIREN_EINVAL, "kspace_sse_backward: bad arguments");
+  if (batch * npix == 0) return SIREN_OK;
+  KsseBwdArgs a{d, mask, hf, g, dpred, batch, npix, channels, noise, scale};
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(4096, cdiv(batch * npix, KS_THREADS)));
+  hipLaunchKernelGGL(ksse_bwd_kernel, dim3(blocks), dim3(KS_THREADS), 0, (hipStream_t)stream, a);
+  return check_launch("kspace_sse_backward");
 }
 
 int siren_adam_step(const siren_adam_desc* d, void* stream) {

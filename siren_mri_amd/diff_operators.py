@@ -58,11 +58,18 @@ def set_analytic(enabled: bool) -> None:
 
 
 def gradient(y, x, grad_outputs=None):
-    if grad_outputs is None and _ANALYTIC:
+    """sum_c g_c dy_c/dx (g = grad_outputs, ones by default), differentiable. For a SIREN output
+    the analytic path takes any g that is constant across the output channels (every g when there
+    is one output, as in every BASELINE config): the sum is then g times the unweighted one."""
+    if _ANALYTIC:
         src = _lookup(y, x)
         if src is not None:
             from .jvp import siren_gradient
-            return siren_gradient(x, *src)
+            if grad_outputs is None:
+                return siren_gradient(x, *src)
+            g = grad_outputs
+            if g.shape == y.shape and (y.shape[-1] == 1 or bool((g == g[..., :1]).all())):
+                return siren_gradient(x, *src) * g[..., :1]
     if grad_outputs is None:
         grad_outputs = torch.ones_like(y)
     return torch.autograd.grad(y, [x], grad_outputs=grad_outputs, create_graph=True)[0]

@@ -1,4 +1,4 @@
-"""Analytic SIREN derivatives as autograd Functions (native tangent-stream kernels).
+"""Analytic SIREN derivatives as PyTorch custom ops (native tangent-stream kernels).
 
 siren_gradient(x, fcblock, params) == diff_operators.gradient(y, x) for y = fcblock(x)
     (diff_operators.py:39-43): sum over output channels of dy/dx, shape of x. Differentiable:
@@ -7,93 +7,162 @@ siren_gradient(x, fcblock, params) == diff_operators.gradient(y, x) for y = fcbl
 siren_laplace(x, fcblock, params) == diff_operators.laplace(y, x) (diff_operators.py:27-36):
     sum over outputs and input dims of d2y/dx2. Differentiable: its backward adds the Laplacian
     adjoint stream (what laplace_mse's triple backward computes through autograd).
+
+Custom ops (torch.library.Library "siren_mri_amd", with fake kernels and an Autograd-key
+formula), over the C ABI siren_jvp_forward/backward:
+  siren_mri_amd::sine_mlp_jvp(x, W[], b[], w0, prec, batched, order, keep) -> (out, saved)
+  siren_mri_amd::sine_mlp_jvp_bwd(dout, x, W[], b[], saved, w0, prec, batched, order, need_dx)
+        -> (dx, dW[], db[])
 """
 from __future__ import annotations
 
 import ctypes
+from typing import List, Tuple
 
 import torch
-from torch.autograd.function import once_differentiable
+from torch import Tensor
 
 from . import _native
-from .ops import _Geometry, _flat_params, _require_device, get_default_precision
+from .ops import _LIB, _Geometry, _geo_of, _require_device, get_default_precision
 
 
-def _desc(geo, ws, bs, fcblock, prec):
-    return _native.make_desc(geo.dims, ws, bs, w0=fcblock.w0, prec=prec, outermost_linear=True,
+def _desc(geo, ws, bs, w0, prec):
+    return _native.make_desc(geo.dims, ws, bs, w0=w0, prec=prec, outermost_linear=True,
                              weights_batched=geo.batched, batch=geo.batch, rows_per_batch=geo.rows)
 
 
-class _SirenJVP(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, cfg, x, *params):
-        fcblock, prec, order, n_layers, grad_on = cfg
-        weights, biases = list(params[:n_layers]), list(params[n_layers:])
-        _require_device(x)
-        geo = _Geometry(x, weights)
-        ws, bs = _flat_params(weights, biases, geo)
-        xc = x.contiguous()
-        dev = x.device
-        desc = _desc(geo, ws, bs, fcblock, prec)
-        L = _native.lib()
-        keep = grad_on and any(ctx.needs_input_grad)
-        saved_bytes = L.siren_jvp_saved_bytes(ctypes.byref(desc), order)
-        if saved_bytes < 0:
-            raise _native.NativeError(f"siren_jvp: {_native.last_error()}")
-        ws_bytes = L.siren_jvp_workspace_bytes(ctypes.byref(desc), order)
-        saved = torch.empty(saved_bytes, dtype=torch.uint8, device=dev) if keep else None
-        work = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-        grad = torch.empty(xc.shape, dtype=torch.float32, device=dev)
-        lap = torch.empty(xc.shape[:-1] + (1,), dtype=torch.float32, device=dev) if order == 2 else None
-        rc = L.siren_jvp_forward(ctypes.byref(desc), order, xc.data_ptr(), grad.data_ptr(),
-                                 lap.data_ptr() if lap is not None else None,
-                                 saved.data_ptr() if saved is not None else None, saved_bytes if keep else 0,
-                                 work.data_ptr(), ws_bytes, _native.stream_handle(dev))
-        _native.check(rc, "siren_jvp_forward")
-        ctx.cfg, ctx.geo, ctx.saved_buf, ctx.saved_bytes = cfg, geo, saved, saved_bytes
-        ctx.save_for_backward(xc, *ws, *bs)
-        return grad if order == 1 else lap
+def _jvp_sizes(geo, prec, order):
+    L = _native.lib()
+    d = _native.describe_only(geo.dims, prec=prec, weights_batched=geo.batched, batch=geo.batch,
+                              rows_per_batch=geo.rows)
+    saved = L.siren_jvp_saved_bytes(ctypes.byref(d), order)
+    if saved < 0:
+        raise _native.NativeError(f"siren_jvp: {_native.last_error()}")
+    return saved, L.siren_jvp_workspace_bytes(ctypes.byref(d), order)
+
+
+_LIB.define("sine_mlp_jvp(Tensor x, Tensor[] weights, Tensor[] biases, float w0, int prec, bool batched, int order, "
+            "bool keep) -> (Tensor, Tensor)")
+_LIB.define("sine_mlp_jvp_bwd(Tensor dout, Tensor x, Tensor[] weights, Tensor[] biases, Tensor saved, float w0, "
+            "int prec, bool batched, int order, bool need_dx) -> (Tensor, Tensor[], Tensor[])")
+
+
+def sine_mlp_jvp(x: Tensor, weights: List[Tensor], biases: List[Tensor], w0: float, prec: int, batched: bool,
+                 order: int, keep: bool) -> Tuple[Tensor, Tensor]:
+    """siren_jvp_forward: order 1 -> sum_c dy_c/dx (shape of x); order 2 -> the Laplacian [.., 1]."""
+    _require_device(x)
+    geo = _geo_of(x, weights, batched)
+    ws = [w.contiguous() for w in weights]
+    bs = [b.contiguous() for b in biases]
+    xc = x.contiguous()
+    dev = x.device
+    desc = _desc(geo, ws, bs, w0, prec)
+    saved_bytes, ws_bytes = _jvp_sizes(geo, prec, order)
+    saved = torch.empty(saved_bytes if keep else 0, dtype=torch.uint8, device=dev)
+    work = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    grad = torch.empty(xc.shape, dtype=torch.float32, device=dev)
+    lap = torch.empty(xc.shape[:-1] + (1,), dtype=torch.float32, device=dev) if order == 2 else None
+    rc = _native.lib().siren_jvp_forward(ctypes.byref(desc), order, xc.data_ptr(), grad.data_ptr(),
+                                         lap.data_ptr() if lap is not None else None,
+                                         saved.data_ptr() if keep else None, saved_bytes if keep else 0,
+                                         work.data_ptr(), ws_bytes, _native.stream_handle(dev))
+    _native.check(rc, "siren_jvp_forward")
+    return (grad if order == 1 else lap), saved
+
+
+def _sine_mlp_jvp_fake(x, weights, biases, w0, prec, batched, order, keep):
+    geo = _geo_of(x, weights, batched)
+    saved_bytes, _ = _jvp_sizes(geo, prec, order)
+    out = x.new_empty(x.shape) if order == 1 else x.new_empty(x.shape[:-1] + (1,))
+    return out, x.new_empty((saved_bytes if keep else 0,), dtype=torch.uint8)
+
+
+def sine_mlp_jvp_bwd(dout: Tensor, x: Tensor, weights: List[Tensor], biases: List[Tensor], saved: Tensor, w0: float,
+                     prec: int, batched: bool, order: int,
+                     need_dx: bool) -> Tuple[Tensor, List[Tensor], List[Tensor]]:
+    """siren_jvp_backward: the adjoint of the tangent streams -> (dx or empty, dW, db)."""
+    if saved.numel() == 0:
+        raise RuntimeError("siren_mri_amd: sine_mlp_jvp_bwd needs the saved buffer of a forward with keep=True")
+    geo = _geo_of(x, weights, batched)
+    ws = [w.contiguous() for w in weights]
+    bs = [b.contiguous() for b in biases]
+    xc = x.contiguous()
+    dev = x.device
+    desc = _desc(geo, ws, bs, w0, prec)
+    saved_bytes, ws_bytes = _jvp_sizes(geo, prec, order)
+    work = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    dW = [torch.empty_like(w) for w in ws]
+    db = [torch.empty_like(b) for b in bs]
+    dx = torch.empty_like(xc) if need_dx else xc.new_empty((0,))
+    VP = ctypes.c_void_p * len(ws)
+    rc = _native.lib().siren_jvp_backward(ctypes.byref(desc), order, xc.data_ptr(),
+                                          dout.contiguous().float().data_ptr(), saved.data_ptr(), saved_bytes,
+                                          work.data_ptr(), ws_bytes, VP(*[g.data_ptr() for g in dW]),
+                                          VP(*[g.data_ptr() for g in db]), dx.data_ptr() if need_dx else None,
+                                          _native.stream_handle(dev))
+    _native.check(rc, "siren_jvp_backward")
+    return dx, dW, db
+
+
+def _sine_mlp_jvp_bwd_fake(dout, x, weights, biases, saved, w0, prec, batched, order, need_dx):
+    return (torch.empty_like(x) if need_dx else x.new_empty((0,)),
+            [torch.empty_like(w) for w in weights], [torch.empty_like(b) for b in biases])
+
+
+class _SineMLPJVPAutograd(torch.autograd.Function):
+    """Autograd formula of sine_mlp_jvp: its backward is sine_mlp_jvp_bwd (lists passed flattened)."""
 
     @staticmethod
-    @once_differentiable
-    def backward(ctx, dout):
-        fcblock, prec, order, n_layers, _ = ctx.cfg
-        if ctx.saved_buf is None:
-            raise RuntimeError(
-                "siren_mri_amd: the native tangent-stream backward runs once per forward; backward "
-                "through the same graph a second time (retain_graph=True) is not supported")
-        geo = ctx.geo
+    def forward(ctx, meta, x, *params):
+        w0, prec, batched, order, n, keep = meta
+        with torch._C._AutoDispatchBelowAutograd():
+            out, saved = torch.ops.siren_mri_amd.sine_mlp_jvp(x, list(params[:n]), list(params[n:]), w0, prec,
+                                                              batched, order, keep)
+        ctx.meta = meta
+        ctx.save_for_backward(x, saved, *params)
+        ctx.mark_non_differentiable(saved)
+        return out, saved
+
+    @staticmethod
+    def backward(ctx, dout, _dsaved):
+        w0, prec, batched, order, n, keep = ctx.meta
+        if not keep:
+            raise RuntimeError("siren_mri_amd: the tangent-stream forward ran without keeping its streams "
+                               "(grad mode was off); it cannot be differentiated")
         t = ctx.saved_tensors
-        xc, ws, bs = t[0], list(t[1:1 + n_layers]), list(t[1 + n_layers:])
-        dev = xc.device
-        desc = _desc(geo, ws, bs, fcblock, prec)
-        L = _native.lib()
-        ws_bytes = L.siren_jvp_workspace_bytes(ctypes.byref(desc), order)
-        work = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-        dW = [torch.empty_like(w) for w in ws]
-        db = [torch.empty_like(b) for b in bs]
-        dx = torch.empty_like(xc) if ctx.needs_input_grad[1] else None
-        VP = ctypes.c_void_p * n_layers
-        rc = L.siren_jvp_backward(ctypes.byref(desc), order, xc.data_ptr(), dout.contiguous().float().data_ptr(),
-                                  ctx.saved_buf.data_ptr(), ctx.saved_bytes, work.data_ptr(), ws_bytes,
-                                  VP(*[g.data_ptr() for g in dW]), VP(*[g.data_ptr() for g in db]),
-                                  dx.data_ptr() if dx is not None else None, _native.stream_handle(dev))
-        _native.check(rc, "siren_jvp_backward")
-        ctx.saved_buf = None
-        if geo.squeeze_w:
-            dW = [g.unsqueeze(0) for g in dW]
-            db = [g.unsqueeze(0) for g in db]
-        # the output bias does not reach dy/dx or the Laplacian: autograd leaves its .grad as None in the reference
+        x, saved, ws, bs = t[0], t[1], list(t[2:2 + n]), list(t[2 + n:])
+        need_dx = ctx.needs_input_grad[1]
+        dx, dW, db = torch.ops.siren_mri_amd.sine_mlp_jvp_bwd(dout, x, ws, bs, saved, w0, prec, batched, order,
+                                                              need_dx)
+        db = list(db)
+        # the output bias does not reach dy/dx or the Laplacian: autograd leaves its .grad None in the reference
         db[-1] = None
-        return (None, dx, *dW, *db)
+        return (None, dx if need_dx else None, *dW, *db)
+
+
+def _sine_mlp_jvp_autograd(x, weights, biases, w0, prec, batched, order, keep):
+    return _SineMLPJVPAutograd.apply((w0, prec, batched, order, len(weights), keep), x, *weights, *biases)
+
+
+_LIB.impl("sine_mlp_jvp", sine_mlp_jvp, "CUDA")
+_LIB.impl("sine_mlp_jvp_bwd", sine_mlp_jvp_bwd, "CUDA")
+_LIB.impl("sine_mlp_jvp", _sine_mlp_jvp_autograd, "Autograd")
+torch.library.register_fake("siren_mri_amd::sine_mlp_jvp", _sine_mlp_jvp_fake, lib=_LIB)
+torch.library.register_fake("siren_mri_amd::sine_mlp_jvp_bwd", _sine_mlp_jvp_bwd_fake, lib=_LIB)
 
 
 def _apply(x, fcblock, params, order):
     from .meta import get_subdict
     ws, bs = fcblock.layer_params(get_subdict(params, "net") if params is not None else None)
     prec = _native.precision_code(fcblock.precision or get_default_precision())
-    cfg = (fcblock, prec, order, len(ws), torch.is_grad_enabled())
-    return _SirenJVP.apply(cfg, x, *ws, *bs)
+    _require_device(x)
+    geo = _Geometry(x, ws)
+    if geo.squeeze_w:
+        ws, bs = [w[0] for w in ws], [b[0] for b in bs]
+    keep = torch.is_grad_enabled() and (x.requires_grad or any(t.requires_grad for t in list(ws) + list(bs)))
+    out, _ = torch.ops.siren_mri_amd.sine_mlp_jvp(x, list(ws), list(bs), float(fcblock.w0), prec, geo.batched,
+                                                  order, keep)
+    return out
 
 
 def siren_gradient(x, fcblock, params=None):

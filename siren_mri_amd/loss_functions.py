@@ -8,6 +8,9 @@
   gradients_mse            loss_functions.py:330-335
   laplace_mse              loss_functions.py:350-355
 
+image_mse runs on the native k-space op (siren_kspace.hip), with the data consistency of a native
+DataConsistencyInKspace output folded in.
+
 Deliberate deviation (bug 0.2): the reference builds its high-frequency mask
 on a fixed 128x128 grid, so image_mse(high_freq=True) raises for any other image size; here the
 mask applies when the image is 128x128 and the loss is the plain SSE otherwise.
@@ -17,6 +20,7 @@ from __future__ import annotations
 import torch
 
 from . import _native, diff_operators
+from .data_consistency import dc_source
 from .dataio import lin2img
 from .utils import create_circular_mask_torch
 
@@ -86,6 +90,108 @@ class _WeightedSSE(torch.autograd.Function):
         return out.view(ctx.shape), None, None, None
 
 
+# image_mse on the SIREN output layout [B, N, C], optionally with data consistency folded in
+# (siren_kspace.hip): siren_mri_amd::kspace_sse(pred, k0?, mask?, tgt, hf?, noise, weight) -> (loss, d)
+from .ops import _LIB  # noqa: E402
+
+_LIB.define("kspace_sse(Tensor pred, Tensor? k0, Tensor? mask, Tensor tgt, Tensor? hf, float noise, float weight) "
+            "-> (Tensor, Tensor)")
+_LIB.define("kspace_sse_bwd(Tensor d, Tensor? mask, Tensor? hf, Tensor g, float noise, float scale) -> Tensor")
+
+
+def _kspace_sse_cuda(pred, k0, mask, tgt, hf, noise, weight):
+    b, n, c = pred.shape
+    pc, tc = pred.contiguous(), tgt.contiguous()
+    kc = k0.contiguous() if k0 is not None else None
+    mc = mask.contiguous() if mask is not None else None
+    hc = hf.contiguous() if hf is not None else None
+    d = torch.empty_like(pc)
+    loss = torch.empty((), dtype=torch.float32, device=pred.device)
+    ws = _sse_workspace(pred.device)
+    rc = _native.lib().siren_kspace_sse_forward(
+        pc.data_ptr(), kc.data_ptr() if kc is not None else None, mc.data_ptr() if mc is not None else None,
+        tc.data_ptr(), hc.data_ptr() if hc is not None else None, b, n, c, float(noise), float(weight), d.data_ptr(),
+        loss.data_ptr(), ws.data_ptr(), ws.numel(), _native.stream_handle(pred.device))
+    _native.check(rc, "siren_kspace_sse_forward")
+    return loss, d
+
+
+def _kspace_sse_bwd_cuda(d, mask, hf, g, noise, scale):
+    b, n, c = d.shape
+    out = torch.empty_like(d)
+    mc = mask.contiguous() if mask is not None else None
+    hc = hf.contiguous() if hf is not None else None
+    gc = g.contiguous().to(torch.float32)
+    rc = _native.lib().siren_kspace_sse_backward(d.data_ptr(), mc.data_ptr() if mc is not None else None,
+                                                 hc.data_ptr() if hc is not None else None, b, n, c, float(noise),
+                                                 gc.data_ptr(), float(scale), out.data_ptr(),
+                                                 _native.stream_handle(d.device))
+    _native.check(rc, "siren_kspace_sse_backward")
+    return out
+
+
+class _KspaceSSEAutograd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred, k0, mask, tgt, hf, noise, weight):
+        with torch._C._AutoDispatchBelowAutograd():
+            loss, d = torch.ops.siren_mri_amd.kspace_sse(pred, k0, mask, tgt, hf, noise, weight)
+        ctx.save_for_backward(d, mask, hf)
+        ctx.noise, ctx.weight = noise, weight
+        ctx.mark_non_differentiable(d)
+        return loss, d
+
+    @staticmethod
+    def backward(ctx, g, _gd):
+        d, mask, hf = ctx.saved_tensors
+        dpred = torch.ops.siren_mri_amd.kspace_sse_bwd(d, mask, hf, g, ctx.noise, 2.0 * ctx.weight)
+        return dpred, None, None, None, None, None, None
+
+
+_LIB.impl("kspace_sse", _kspace_sse_cuda, "CUDA")
+_LIB.impl("kspace_sse_bwd", _kspace_sse_bwd_cuda, "CUDA")
+_LIB.impl("kspace_sse", lambda pred, k0, mask, tgt, hf, noise, weight:
+          _KspaceSSEAutograd.apply(pred, k0, mask, tgt, hf, noise, weight), "Autograd")
+torch.library.register_fake("siren_mri_amd::kspace_sse", lambda pred, k0, mask, tgt, hf, noise, weight:
+                            (pred.new_empty(()), torch.empty_like(pred)), lib=_LIB)
+torch.library.register_fake("siren_mri_amd::kspace_sse_bwd", lambda d, mask, hf, g, noise, scale: torch.empty_like(d),
+                            lib=_LIB)
+
+_FUSE_DC = True
+
+
+def set_kspace_fusion(enabled: bool) -> None:
+    """Fold a native DataConsistencyInKspace output's DC into image_mse's loss op (default on)."""
+    global _FUSE_DC
+    _FUSE_DC = bool(enabled)
+
+
+def _hf_flat(device):
+    key = ("flat", device)
+    m = _MASKS.get(key)
+    if m is None:
+        m = _high_freq_mask(device).reshape(-1).contiguous()
+        _MASKS[key] = m
+    return m
+
+
+def _kspace_image_mse(out, tgt, high_freq):
+    """image_mse on [B, N, C] (N a square): the native k-space op, or None when not applicable."""
+    if not (out.is_cuda and out.dtype == torch.float32 and out.dim() == 3 and tgt.shape == out.shape
+            and tgt.dtype == torch.float32 and tgt.device == out.device and not tgt.requires_grad
+            and out.shape[-1] <= 8):
+        return None
+    n = out.shape[1]
+    side = int(round(n ** 0.5))
+    if side * side != n:
+        return None
+    hf = _hf_flat(out.device) if (high_freq and side == 128) else None
+    src = dc_source(out) if _FUSE_DC else None
+    if src is not None and src[0].shape == out.shape:
+        pred, k0, mask, noise = src
+        return torch.ops.siren_mri_amd.kspace_sse(pred, k0, mask, tgt, hf, noise, _KSPACE_WEIGHT)[0]
+    return torch.ops.siren_mri_amd.kspace_sse(out, None, None, tgt, hf, 0.0, _KSPACE_WEIGHT)[0]
+
+
 def weighted_sse(pred, tgt, weight=_KSPACE_WEIGHT, mask=None):
     """sum |m (pred - tgt)|^2 * weight over any shape (image_mse's reduction without the
     lin2img reshape): the loss of a coordinate shard of an image in a sharded fit, whose partial
@@ -99,7 +205,12 @@ def weighted_sse(pred, tgt, weight=_KSPACE_WEIGHT, mask=None):
 
 
 def image_mse(mask, model_output, gt, high_freq=True):
-    """Weighted k-space SSE: sum |m * (pred - gt)|^2 / 128^2 (a sum over the batch)."""
+    """Weighted k-space SSE: sum |m * (pred - gt)|^2 / 128^2 (a sum over the batch). On the GPU
+    the native k-space op reads model_out / gt in their [B, N, C] layout (no lin2img copies); a
+    model_out produced by the native DataConsistencyInKspace has the DC folded into the op."""
+    fused = _kspace_image_mse(model_output["model_out"], gt["img"], high_freq)
+    if fused is not None:
+        return {"img_loss": fused}
     pred = lin2img(model_output["model_out"])
     tgt = lin2img(gt["img"])
     hf = _high_freq_mask(pred.device) if (high_freq and pred.shape[-2:] == (128, 128)) else None

@@ -1,4 +1,4 @@
-"""Autograd wrappers of the native SIREN layer stack.
+"""The native SIREN layer stack as PyTorch custom ops (torch.library, namespace siren_mri_amd).
 
 ``siren_mlp(x, weights, biases, w0=..., precision=..., outermost_linear=...)`` is the fused
 replacement of ``FCBlock.forward`` with nonlinearity='sine' (modules.py:92-97): the whole
@@ -6,16 +6,30 @@ replacement of ``FCBlock.forward`` with nonlinearity='sine' (modules.py:92-97): 
 one native backward call. Weights may be shared ([out, in]) or batched per sample
 ([B, out, in], the hypernetwork case of meta_modules.py:42-54, 198-225).
 
+Custom ops (SURVEY.md §8(b) 'Custom-op layer'), each a thin wrapper of the C ABI in
+include/siren_mri_amd.h, registered with the dispatcher together with fake (meta) kernels, so
+FakeTensor tracing / torch.compile see shapes without running anything:
+  siren_mri_amd::sine_mlp_fwd(x, W[], b[], w0, prec, outermost_linear, batched, keep)
+        -> (y, saved)                         siren_mlp_forward
+  siren_mri_amd::sine_mlp_bwd(dy, x, W[], b[], saved, w0, prec, outermost_linear, batched, need_dx)
+        -> (dx, dW[], db[])                   siren_mlp_backward
+`saved` is the uint8 buffer of prepared weights and stored phases the backward reads (never
+writes), so a graph may be back-propagated more than once (retain_graph=True). The autograd
+formula of sine_mlp_fwd (its Autograd dispatch key) is sine_mlp_bwd; a second
+differentiation of that backward (double backward through an autograd graph) is not provided:
+derivatives of a SIREN's output w.r.t. its input go through the analytic tangent-stream ops
+(jvp.py, diff_operators.gradient/laplace).
+
 No CPU or eager-PyTorch fallback exists: a CPU tensor, a float64 tensor or an unsupported
 shape raises.
 """
 from __future__ import annotations
 
 import ctypes
-from typing import Sequence
+from typing import List, Sequence, Tuple
 
 import torch
-from torch.autograd.function import once_differentiable
+from torch import Tensor
 
 from . import _native
 
@@ -93,102 +107,163 @@ def _flat_params(weights, biases, geo: _Geometry):
 _SIZES = {}
 
 
-def _sizes(L, desc, geo: _Geometry, prec: int, outermost_linear: bool, need_saved: bool):
+def _sizes(geo: _Geometry, prec: int, outermost_linear: bool):
     """(saved, workspace) bytes of a geometry after siren_mlp_check. They depend only on the
-    geometry and options (not on the pointers), so they are asked once per geometry."""
+    geometry and options (not on the pointers), so they are asked once per geometry, with a
+    pointer-free descriptor (also what the fake kernels use)."""
     key = (tuple(geo.dims), geo.batch, geo.rows, geo.batched, prec, outermost_linear,
            _native.options_epoch())
     hit = _SIZES.get(key)
     if hit is None:
+        L = _native.lib()
+        desc = _native.describe_only(geo.dims, prec=prec, outermost_linear=outermost_linear,
+                                     weights_batched=geo.batched, batch=geo.batch, rows_per_batch=geo.rows)
         _native.check(L.siren_mlp_check(ctypes.byref(desc)), "siren_mlp_check")
         hit = (L.siren_mlp_saved_bytes(ctypes.byref(desc)), L.siren_mlp_workspace_bytes(ctypes.byref(desc)))
         if len(_SIZES) > 256:
             _SIZES.clear()
         _SIZES[key] = hit
-    return (hit[0] if need_saved else 0), hit[1]
+    return hit
 
 
-class _SirenMLPFunction(torch.autograd.Function):
+def _geo_of(x, weights, batched):
+    geo = _Geometry(x, weights)
+    if geo.batched != batched:
+        raise RuntimeError("siren_mri_amd: weight batching does not match the op's `batched` flag")
+    return geo
+
+
+# --------------------------------------------------------------------------- custom ops
+# Registered with the low-level torch.library.Library API (schema + CUDA kernel + fake kernel +
+# an Autograd-key formula): the dispatcher round trip costs ~15 us per call on the host, against
+# ~100 us for the torch.library.custom_op wrapper, which would make small fits host-bound.
+_LIB = torch.library.Library("siren_mri_amd", "DEF")
+_LIB.define("sine_mlp_fwd(Tensor x, Tensor[] weights, Tensor[] biases, float w0, int prec, bool outermost_linear, "
+            "bool batched, bool keep) -> (Tensor, Tensor)")
+_LIB.define("sine_mlp_bwd(Tensor dy, Tensor x, Tensor[] weights, Tensor[] biases, Tensor saved, float w0, int prec, "
+            "bool outermost_linear, bool batched, bool need_dx) -> (Tensor, Tensor[], Tensor[])")
+
+
+def sine_mlp_fwd(x: Tensor, weights: List[Tensor], biases: List[Tensor], w0: float, prec: int,
+                 outermost_linear: bool, batched: bool, keep: bool) -> Tuple[Tensor, Tensor]:
+    """siren_mlp_forward: y = the SIREN stack on x; saved = the backward's buffer (empty unless keep)."""
+    _require_device(x)
+    geo = _geo_of(x, weights, batched)
+    ws = [w.contiguous() for w in weights]
+    bs = [b.contiguous() for b in biases]
+    xc = x.contiguous()
+    dev = x.device
+    desc = _native.make_desc(geo.dims, ws, bs, w0=w0, prec=prec, outermost_linear=outermost_linear,
+                             weights_batched=geo.batched, batch=geo.batch, rows_per_batch=geo.rows)
+    saved_bytes, ws_bytes = _sizes(geo, prec, outermost_linear)
+    saved = torch.empty(saved_bytes if keep else 0, dtype=torch.uint8, device=dev)
+    work = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    y = torch.empty(geo.lead_shape + (geo.dims[-1],), dtype=torch.float32, device=dev)
+    rc = _native.lib().siren_mlp_forward(ctypes.byref(desc), xc.data_ptr(), y.data_ptr(),
+                                         saved.data_ptr() if keep else None, saved_bytes if keep else 0,
+                                         work.data_ptr(), ws_bytes, _native.stream_handle(dev))
+    _native.check(rc, "siren_mlp_forward")
+    return y, saved
+
+
+def _sine_mlp_fwd_fake(x, weights, biases, w0, prec, outermost_linear, batched, keep):
+    geo = _geo_of(x, weights, batched)
+    saved_bytes, _ = _sizes(geo, prec, outermost_linear)
+    return (x.new_empty(geo.lead_shape + (geo.dims[-1],), dtype=torch.float32),
+            x.new_empty((saved_bytes if keep else 0,), dtype=torch.uint8))
+
+
+def sine_mlp_bwd(dy: Tensor, x: Tensor, weights: List[Tensor], biases: List[Tensor], saved: Tensor, w0: float,
+                 prec: int, outermost_linear: bool, batched: bool,
+                 need_dx: bool) -> Tuple[Tensor, List[Tensor], List[Tensor]]:
+    """siren_mlp_backward: (dx or an empty tensor, dW per layer, db per layer)."""
+    if saved.numel() == 0:
+        raise RuntimeError("siren_mri_amd: sine_mlp_bwd needs the saved buffer of a forward run with keep=True")
+    geo = _geo_of(x, weights, batched)
+    ws = [w.contiguous() for w in weights]
+    bs = [b.contiguous() for b in biases]
+    xc = x.contiguous()
+    dev = x.device
+    dyc = dy.contiguous().to(torch.float32)
+    desc = _native.make_desc(geo.dims, ws, bs, w0=w0, prec=prec, outermost_linear=outermost_linear,
+                             weights_batched=geo.batched, batch=geo.batch, rows_per_batch=geo.rows)
+    saved_bytes, ws_bytes = _sizes(geo, prec, outermost_linear)
+    work = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    dW = [torch.empty_like(w) for w in ws]
+    db = [torch.empty_like(b) for b in bs]
+    dx = torch.empty_like(xc) if need_dx else xc.new_empty((0,))
+    n = len(ws)
+    VP = ctypes.c_void_p * n
+    rc = _native.lib().siren_mlp_backward(ctypes.byref(desc), xc.data_ptr(), dyc.data_ptr(), saved.data_ptr(),
+                                          saved_bytes, work.data_ptr(), ws_bytes,
+                                          VP(*[t.data_ptr() for t in dW]), VP(*[t.data_ptr() for t in db]),
+                                          dx.data_ptr() if need_dx else None, _native.stream_handle(dev))
+    _native.check(rc, "siren_mlp_backward")
+    return dx, dW, db
+
+
+def _sine_mlp_bwd_fake(dy, x, weights, biases, saved, w0, prec, outermost_linear, batched, need_dx):
+    return (torch.empty_like(x) if need_dx else x.new_empty((0,)),
+            [torch.empty_like(w) for w in weights], [torch.empty_like(b) for b in biases])
+
+
+class _SineMLPAutograd(torch.autograd.Function):
+    """Autograd formula of sine_mlp_fwd (the Autograd dispatch key): its backward is sine_mlp_bwd.
+    The weight and bias lists are passed flattened so autograd tracks every tensor."""
+
     @staticmethod
-    def forward(ctx, cfg, x, *params):
-        w0, prec, outermost_linear, n_layers, grad_on = cfg
-        weights = list(params[:n_layers])
-        biases = list(params[n_layers:])
-        _require_device(x)
-        geo = _Geometry(x, weights)
-        ws, bs = _flat_params(weights, biases, geo)
-        xc = x.contiguous()
-        dev = x.device
-        desc = _native.make_desc(geo.dims, ws, bs, w0=w0, prec=prec,
-                                 outermost_linear=outermost_linear, weights_batched=geo.batched,
-                                 batch=geo.batch, rows_per_batch=geo.rows)
-        L = _native.lib()
-        need_saved = grad_on and any(ctx.needs_input_grad)
-        saved_bytes, ws_bytes = _sizes(L, desc, geo, prec, outermost_linear, need_saved)
-        saved = torch.empty(max(saved_bytes, 1), dtype=torch.uint8, device=dev) if need_saved else None
-        work = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        y = torch.empty(geo.lead_shape + (geo.dims[-1],), dtype=torch.float32, device=dev)
-        rc = L.siren_mlp_forward(ctypes.byref(desc), xc.data_ptr(), y.data_ptr(),
-                                 saved.data_ptr() if saved is not None else None, saved_bytes,
-                                 work.data_ptr(), ws_bytes, _native.stream_handle(dev))
-        _native.check(rc, "siren_mlp_forward")
-        ctx.cfg = cfg
-        ctx.geo = geo
-        ctx.desc = desc  # its pointers are the tensors saved below
-        ctx.saved_buf = saved
-        ctx.saved_bytes = saved_bytes
-        ctx.save_for_backward(xc, *ws, *bs)
-        return y
+    def forward(ctx, meta, x, *params):
+        w0, prec, outermost_linear, batched, n, keep = meta
+        weights, biases = list(params[:n]), list(params[n:])
+        with torch._C._AutoDispatchBelowAutograd():
+            y, saved = torch.ops.siren_mri_amd.sine_mlp_fwd(x, weights, biases, w0, prec, outermost_linear,
+                                                            batched, keep)
+        ctx.meta = meta
+        ctx.save_for_backward(x, saved, *params)
+        ctx.mark_non_differentiable(saved)
+        return y, saved
 
     @staticmethod
-    @once_differentiable
-    def backward(ctx, dy):
-        w0, prec, outermost_linear, n_layers, _ = ctx.cfg
-        if ctx.saved_buf is None and ctx.saved_bytes:
-            # the saved activations are released at the end of the first backward (they are the
-            # largest allocation of a step); the reference's autograd graph could be re-entered
-            raise RuntimeError(
-                "siren_mri_amd: the native SIREN backward runs once per forward; backward through "
-                "the same graph a second time (retain_graph=True) is not supported")
-        geo = ctx.geo
-        tensors = ctx.saved_tensors
-        xc = tensors[0]
-        ws = list(tensors[1:1 + n_layers])
-        bs = list(tensors[1 + n_layers:])
-        dev = xc.device
-        dyc = dy.contiguous().to(torch.float32)
-        desc = ctx.desc
-        L = _native.lib()
-        ws_bytes = _sizes(L, desc, geo, prec, outermost_linear, False)[1]
-        work = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        dW = [torch.empty_like(w) for w in ws]
-        db = [torch.empty_like(b) for b in bs]
+    def backward(ctx, dy, _dsaved):
+        w0, prec, outermost_linear, batched, n, keep = ctx.meta
+        if not keep:
+            raise RuntimeError("siren_mri_amd: the SIREN forward ran without keeping activations "
+                               "(grad mode was off); it cannot be differentiated")
+        t = ctx.saved_tensors
+        x, saved, ws, bs = t[0], t[1], list(t[2:2 + n]), list(t[2 + n:])
         need_dx = ctx.needs_input_grad[1]
-        dx = torch.empty_like(xc) if need_dx else None
-        VP = ctypes.c_void_p * n_layers
-        dW_ptrs = VP(*[t.data_ptr() for t in dW])
-        db_ptrs = VP(*[t.data_ptr() for t in db])
-        rc = L.siren_mlp_backward(ctypes.byref(desc), xc.data_ptr(), dyc.data_ptr(),
-                                  ctx.saved_buf.data_ptr(), ctx.saved_bytes, work.data_ptr(),
-                                  ws_bytes, dW_ptrs, db_ptrs,
-                                  dx.data_ptr() if dx is not None else None,
-                                  _native.stream_handle(dev))
-        _native.check(rc, "siren_mlp_backward")
-        ctx.saved_buf = None
-        ctx.desc = None
-        if geo.squeeze_w:
-            dW = [g.unsqueeze(0) for g in dW]
-            db = [g.unsqueeze(0) for g in db]
-        return (None, dx, *dW, *db)
+        dx, dW, db = torch.ops.siren_mri_amd.sine_mlp_bwd(dy, x, ws, bs, saved, w0, prec, outermost_linear,
+                                                          batched, need_dx)
+        return (None, dx if need_dx else None, *dW, *db)
+
+
+def _sine_mlp_fwd_autograd(x, weights, biases, w0, prec, outermost_linear, batched, keep):
+    meta = (w0, prec, outermost_linear, batched, len(weights), keep)
+    return _SineMLPAutograd.apply(meta, x, *weights, *biases)
+
+
+_LIB.impl("sine_mlp_fwd", sine_mlp_fwd, "CUDA")
+_LIB.impl("sine_mlp_bwd", sine_mlp_bwd, "CUDA")
+_LIB.impl("sine_mlp_fwd", _sine_mlp_fwd_autograd, "Autograd")
+torch.library.register_fake("siren_mri_amd::sine_mlp_fwd", _sine_mlp_fwd_fake, lib=_LIB)
+torch.library.register_fake("siren_mri_amd::sine_mlp_bwd", _sine_mlp_bwd_fake, lib=_LIB)
 
 
 def siren_mlp(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[torch.Tensor], *,
-              w0: float = 30.0, precision: str | None = None,
-              outermost_linear: bool = True) -> torch.Tensor:
-    """Fused SIREN stack: y = Linear_L(sin(w0 Linear_{L-1}(... sin(w0 Linear_0(x)))))."""
+              w0: float = 30.0, precision: str | None = None, outermost_linear: bool = True,
+              return_saved: bool = False):
+    """Fused SIREN stack: y = Linear_L(sin(w0 Linear_{L-1}(... sin(w0 Linear_0(x))))).
+    return_saved=True also returns the op's saved buffer (diagnostics)."""
     prec = _native.precision_code(precision or _DEFAULT_PRECISION)
     n = len(weights)
     if len(biases) != n:
         raise ValueError("siren_mlp: weights and biases differ in length")
-    cfg = (float(w0), prec, bool(outermost_linear), n, torch.is_grad_enabled())
-    return _SirenMLPFunction.apply(cfg, x, *weights, *biases)
+    _require_device(x)
+    geo = _Geometry(x, weights)
+    ws, bs = list(weights), list(biases)
+    if geo.squeeze_w:
+        ws, bs = [w[0] for w in ws], [b[0] for b in bs]
+    keep = torch.is_grad_enabled() and (x.requires_grad or any(t.requires_grad for t in ws + bs))
+    y, saved = torch.ops.siren_mri_amd.sine_mlp_fwd(x, ws, bs, float(w0), prec, bool(outermost_linear),
+                                                    geo.batched, keep)
+    return (y, saved) if return_saved else y

@@ -52,8 +52,16 @@ class Adam(torch.optim.Adam):
         for p in group["params"]:
             if p.grad is None:
                 continue
-            if (not p.is_cuda or p.dtype != torch.float32 or p.grad.is_sparse or p.grad.dtype != torch.float32
-                    or not p.is_contiguous() or not p.grad.is_contiguous()):
+            if not p.is_cuda or p.dtype != torch.float32 or p.grad.is_sparse or p.grad.dtype != torch.float32:
+                return False
+            # the update is elementwise over the storage: any dense layout (row-major, or the conv
+            # encoder's channels-last weights) works when the gradient and the moments share it
+            if not (p.is_contiguous() or p.is_contiguous(memory_format=torch.channels_last)):
+                return False
+            if p.grad.stride() != p.stride():
+                return False
+            st = self.state.get(p)
+            if st and "exp_avg" in st and (st["exp_avg"].stride() != p.stride() or st["exp_avg_sq"].stride() != p.stride()):
                 return False
         return True
 

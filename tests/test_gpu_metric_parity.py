@@ -170,9 +170,9 @@ def test_fwdreg_one_hidden_layer_several_rounds(rows):
     for rep in range(2):
         junk = torch.full((64 << 20,), rep + 7, dtype=torch.uint8, device=DEV)  # dirty the pool
         del junk
-        y = siren_mlp(x.to(DEV), ws, bs, precision="bf16")
+        y, saved = siren_mlp(x.to(DEV), ws, bs, precision="bf16", return_saved=True)
         torch.cuda.synchronize()
-        outs.append((y.detach().cpu(), y.grad_fn.saved_buf.clone().cpu()))
+        outs.append((y.detach().cpu(), saved.clone().cpu()))
     with torch.no_grad():
         y_ref = orc.siren_forward(x.double(), [(W.double(), b.double()) for W, b in params])
     assert orc.norm_rel(outs[0][0], y_ref) <= 2e-3

@@ -26,9 +26,9 @@ for rep in range(reps):
     junk = torch.full((64 << 20,), rep + 7, dtype=torch.uint8, device=DEV)
     del junk
     wsr = [w.clone().requires_grad_(True) for w in ws]
-    y = siren_mlp(x, wsr, bs, precision="bf16")
+    y, saved = siren_mlp(x, wsr, bs, precision="bf16", return_saved=True)
     torch.cuda.synchronize()
-    bufs.append(y.grad_fn.saved_buf.clone().cpu())
+    bufs.append(saved.clone().cpu())
     ys.append(y.detach().cpu())
 _native.set_option("debug_keep_p0", 0)
 total = bufs[0].numel()
@@ -50,6 +50,16 @@ for k in range(1, reps):
                 row, col = byte // 512, byte % 512
                 desc.append(f"t{row // 256}w{(row % 256) // 32}j{row % 32}:fb{col // 64}h{(col % 64) // 32}hh{(col % 32) // 16}")
             print("   chunks:", len(chunks), " ".join(desc))
+            # for each differing dword: both runs' values and the first dword of the chunk 32 B on
+            # (the codes of elements 8, 9: what the next part of the epilogue writes)
+            dw = sorted(set((d // 4).tolist()))[:8]
+            for q in dw:
+                b0 = a + q * 4
+                v0 = bufs[0][b0:b0 + 4].view(torch.int32).item()
+                vk = bufs[k][b0:b0 + 4].view(torch.int32).item()
+                nx0 = bufs[0][b0 + 32:b0 + 36].view(torch.int32).item()
+                nxk = bufs[k][b0 + 32:b0 + 36].view(torch.int32).item()
+                print(f"   dword@{(b0 - a) % 512}: run0 {v0:#010x} run{k} {vk:#010x} | +32B run0 {nx0:#010x} run{k} {nxk:#010x}")
             r = d[0].item() // 512
             print("   row", r, "run0", bufs[0][a + r * 512:a + r * 512 + 512].view(torch.int16)[:16].tolist())
             print("   row", r, f"run{k}", bufs[k][a + r * 512:a + r * 512 + 512].view(torch.int16)[:16].tolist())
