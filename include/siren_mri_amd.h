@@ -223,6 +223,13 @@ int siren_kspace_sse_backward(const float* d, const float* mask, const float* hf
                               int channels, float noise, const float* g, float scale, float* dpred, void* stream);
 
 /*
+ * Gaussian Fourier features (replaces GaussianFourierFeatureTransform.forward, features.py:31-41):
+ * out [rows, 2 m] = cat(sin(2 pi x B), cos(2 pi x B)) for x [rows, cin], B [cin, m] (device float32),
+ * one launch. Feeds the SIREN's wide first layer (5..16 inputs on the register-resident forward).
+ */
+int siren_fourier_features(const float* x, const float* B, int64_t rows, int cin, int m, float* out, void* stream);
+
+/*
  * Process-wide execution options (no reference counterpart; used by tests and benchmarks to
  * compare code paths). Keys:
  *   "fused_forward"  1 (default): bf16 stacks of equal power-of-two hidden widths run their

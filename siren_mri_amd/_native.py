@@ -48,6 +48,7 @@ EXPORTED_SYMBOLS = (
     "siren_dc_backward",
     "siren_kspace_sse_forward",
     "siren_kspace_sse_backward",
+    "siren_fourier_features",
     "siren_last_error",
     "siren_version",
 )
@@ -175,6 +176,8 @@ def _declare(lib):
     lib.siren_kspace_sse_forward.restype = ci
     lib.siren_kspace_sse_backward.argtypes = [vp, vp, vp, i64, i64, ci, f32, vp, f32, vp, vp]
     lib.siren_kspace_sse_backward.restype = ci
+    lib.siren_fourier_features.argtypes = [vp, vp, i64, ci, ci, vp, vp]
+    lib.siren_fourier_features.restype = ci
     lib.siren_last_error.argtypes = []
     lib.siren_last_error.restype = ctypes.c_char_p
     lib.siren_version.argtypes = []

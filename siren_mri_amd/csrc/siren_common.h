@@ -162,10 +162,15 @@ DEV void store_b128_sync(const u32x4_t& v, __amdgpu_buffer_rsrc_t r, uint32_t vo
   __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, 0, 0);
 #endif
 }
-// diagnostic builds (siren_gemm.hip ring stores): 0 builtin store, 1 store_b128_sync, 2 asm store
-// without the wait, 3 builtin store + a separate expcnt(0)
+// The ring backward kernels (siren_gemm.hip) keep the compiler's buffer stores: there the asm form
+// made the gradients nondeterministic (tools/det_bwd.py, profiles/r3_store_hazard.txt: 5 of 5
+// runs differ at ~1e-3 with the expcnt wait, ~1e-1 without it; the builtin form: 0 of 5 here and in
+// every determinism test). In that code the asm store's descriptor SGPRs are rewritten a few
+// instructions later (s_and_saveexec into them), which the compiler's own stores avoid.
+// Diagnostic builds: 0 builtin store (default), 1 store_b128_sync, 2 asm store without the wait,
+// 3 builtin store + a separate expcnt(0).
 #ifndef SIREN_GEMM_STORE
-#define SIREN_GEMM_STORE 1
+#define SIREN_GEMM_STORE 0
 #endif
 DEV void store_b128_gemm(const u32x4_t& v, __amdgpu_buffer_rsrc_t r, uint32_t voff) {
 #if SIREN_GEMM_STORE == 1

@@ -39,6 +39,12 @@ constexpr int FREG_WROWS = 32;      // rows per wave tile
 constexpr int FREG_WG_ROWS = 256;   // rows per workgroup round (8 waves)
 constexpr int FREG_SLOT = 16384;    // bytes of one block: 16 K steps x 64 lanes x 16 B
 constexpr int FREG_WL_BYTES = 4096; // output-layer fragments, rows 0..7 only: [16 ks][2 h][8 rows][16 B]
+// Wide first layer (5..16 inputs, C template 16: the Fourier-feature inputs of configs 4/5): layer 0
+// is one f16 MFMA K step split into hi + lo halves (W hi x x hi + W hi x x lo + W lo x x hi, each
+// product exact to ~2^-22), its fragments staged in LDS; the LDS that the x tiles and the bias
+// table of the narrow form use pays for them, so at most FREG_WIDE_MAXH hidden layers.
+constexpr int FREG_WIDE_MAXH = 6;
+constexpr int FREG_W0F_BYTES = 16384;  // [8 fb][hi, lo][64 lanes][16 B]
 // Blocks per ring synchronisation (one barrier every FREG_SYNC blocks, 1 or 2).
 #ifndef SIREN_FREG_SYNC
 #define SIREN_FREG_SYNC 2
@@ -85,6 +91,7 @@ struct FwdRegArgs {
   int64_t rows_per_batch;
   int batched;
   int O, nh, sine_out;
+  int cin;                    // inputs of layer 0 (= C, or 5..16 for the wide form C = 16)
   float w0;
 #ifdef SIREN_FREG_CLOCK
   long long* clk;             // diagnostic builds only: [grid][4] s_memtime / s_memrealtime stamps
@@ -133,8 +140,10 @@ DEV void freg_lgkm(h16x8& v) {
 template <int C, int OC>
 __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   constexpr int F = 256, NKS = 16, NB = 8;
-  constexpr int NKK = (C + 1) / 2;  // K pairs of the f32 layer-0 MFMA
-  static_assert(C >= 1 && C <= 4, "1..4 inputs");
+  constexpr bool WIDE = C > 4;
+  constexpr int NKK = WIDE ? 1 : (C + 1) / 2;  // K pairs of the f32 layer-0 MFMA (narrow form)
+  constexpr int MAXH_ = WIDE ? FREG_WIDE_MAXH : FUSED_MAXH;
+  static_assert((C >= 1 && C <= 4) || C == 16, "1..4 inputs, or the wide form (C = 16: 5..16 inputs)");
   // the ring's 8 slots as separate objects: the compiler's wait-count pass then knows that a read
   // of slot fb cannot alias the LDS-DMA just issued into slot fb - 1 (one array would put an
   // s_waitcnt vmcnt(0) in front of every fragment read after a refill)
@@ -153,8 +162,9 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     }
   };
   __shared__ __attribute__((aligned(16))) char wlf[FREG_WL_BYTES + 16];   // + a zero fragment
-  __shared__ __attribute__((aligned(16))) float sbias[(FUSED_MAXH + 1) * F];  // layer 0, hidden 0..nh-1
-  __shared__ __attribute__((aligned(16))) float xs[2][FREG_WG_ROWS * 4];
+  __shared__ __attribute__((aligned(16))) float sbias[(MAXH_ + 1) * F];  // layer 0, hidden 0..nh-1
+  __shared__ __attribute__((aligned(16))) float xs[2][WIDE ? 4 : FREG_WG_ROWS * 4];
+  __shared__ __attribute__((aligned(16))) char w0f[WIDE ? FREG_W0F_BYTES : 16];  // wide layer-0 fragments
   __shared__ __attribute__((aligned(16))) float sbl[8];
 
 #ifdef SIREN_FREG_DBG
@@ -199,14 +209,32 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
 
   // layer-0 weights as f32 MFMA A operands (lane (i, k): W_0[32 fb + phi(i)][2 kk + k] w0/2pi)
   const int phij = freg_phi(j);
+  const int cin = WIDE ? a.cin : C;
   float w0r[NB][NKK];
+  if constexpr (!WIDE) {
 #pragma unroll
-  for (int fb = 0; fb < NB; ++fb)
+    for (int fb = 0; fb < NB; ++fb)
 #pragma unroll
-    for (int kk = 0; kk < NKK; ++kk) {
-      const int col = 2 * kk + hh;
-      w0r[fb][kk] = col < C ? a.W0[(wb * F + 32 * fb + phij) * C + col] * k1 : 0.f;
+      for (int kk = 0; kk < NKK; ++kk) {
+        const int col = 2 * kk + hh;
+        w0r[fb][kk] = col < C ? a.W0[(wb * F + 32 * fb + phij) * C + col] * k1 : 0.f;
+      }
+  } else {
+    // wide: thread (fb, lane (i, kh)) stages the f16 hi and lo A fragments of block fb,
+    // W_0[32 fb + phi(i)][8 kh + m] w0/2pi (zero past the inputs)
+    const int fbs = tid >> 6, i = lane & 31, kh = lane >> 5;
+    const float* wr = a.W0 + (wb * F + 32 * fbs + freg_phi(i)) * (int64_t)cin;
+    h16x8 hi, lo;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int col = 8 * kh + m;
+      const float v = col < cin ? wr[col] * k1 : 0.f;
+      hi[m] = (_Float16)v;
+      lo[m] = (_Float16)(v - (float)hi[m]);
     }
+    *(h16x8*)(w0f + ((2 * fbs) * 64 + lane) * 16) = hi;
+    *(h16x8*)(w0f + ((2 * fbs + 1) * 64 + lane) * 16) = lo;
+  }
 
   // ---- LDS-DMA: ring blocks and x tiles ----
   // block (layer, fb) of hidden layer `layer` into ring slot fb (the slot of every layer's block fb)
@@ -216,8 +244,24 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst, 16, 0, 0);
     __builtin_amdgcn_global_load_lds((const void*)(src + 1024), (lds_void*)(dst + 1024), 16, 0, 0);
   };
+  // wide: the lane's 8 inputs 8 hh .. 8 hh + 7 of its row of tile t, straight from global memory
+  // into registers (rows past the end and inputs past cin read as 0); issued a layer ahead
+  float xw[8];
+  auto load_xw = [&](int64_t t) {
+    const int64_t r0 = t * FREG_WG_ROWS;
+    const int64_t nv = rows - r0 < 0 ? 0 : (rows - r0 < FREG_WG_ROWS ? rows - r0 : FREG_WG_ROWS);
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x + (batch * rows + r0) * cin, nv * cin * 4);
+    const int rbase = (wave * FREG_WROWS + j) * cin;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int col = 8 * hh + m;
+      const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rx, (rbase + (col < cin ? col : 0)) * 4, 0, 0);
+      xw[m] = col < cin ? __builtin_bit_cast(float, v) : 0.f;
+    }
+  };
   // x rows of workgroup tile t (C KB; rows past the end arrive as zeros): waves 0..C-1, 1 KB each
   auto dma_x = [&](int64_t t, int xb) {
+    if constexpr (WIDE) return;
     if (wave < C) {
       const int64_t r0 = t * FREG_WG_ROWS;
       const int64_t nv = rows - r0 < 0 ? 0 : (rows - r0 < FREG_WG_ROWS ? rows - r0 : FREG_WG_ROWS);
@@ -228,7 +272,8 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   };
 #pragma unroll
   for (int fb = 0; fb < NB; ++fb) dma_block(0, fb);
-  dma_x(t0, 0);
+  if constexpr (WIDE) load_xw(t0);
+  else dma_x(t0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   freg_barrier();
 
@@ -406,6 +451,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
 
   // output layer: y = H W_L^T + b_L (MFMA rows = outputs), beside the last hidden block's epilogue
   auto output_layer = [&](h16x8 (&Hin)[NKS]) {
+    if constexpr (WIDE) load_xw(tcur + G);  // the next round's inputs
     f32x16 accO = accNx;
     Epi ep;
     const uint32_t va_nxt = slot_va(0);  // the next round's first block
@@ -456,7 +502,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     // younger at the next layer's first ring sync, whose vmcnt(14) + barrier cover it. With one
     // hidden layer the ring is never refilled and only the phase stores follow it, so wait for
     // it here explicitly.
-    if (nh == 1 && t != t0) {
+    if (!WIDE && nh == 1 && t != t0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       freg_barrier();
     }
@@ -464,14 +510,32 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     auto layer0 = [&](auto codes_tag) {
       const float* xt = xs[xb] + (wave * FREG_WROWS + j) * C;
       float xr[NKK];
+      h16x8 xh, xl;  // wide: the f16 hi / lo B fragments of the inputs
+      if constexpr (!WIDE) {
 #pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) xr[kk] = (2 * kk + hh) < C ? xt[2 * kk + hh] : 0.f;
+        for (int kk = 0; kk < NKK; ++kk) xr[kk] = (2 * kk + hh) < C ? xt[2 * kk + hh] : 0.f;
+      } else {
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          xh[m] = (_Float16)xw[m];
+          xl[m] = (_Float16)(xw[m] - (float)xh[m]);
+        }
+      }
       // block fb + 1's MFMAs are issued before block fb's epilogue (its result latency and the
       // bias reads overlap the conversion)
       auto l0_mfma = [&](int fb) {
         f32x16 acc = bias_acc(0, fb);
+        if constexpr (!WIDE) {
 #pragma unroll
-        for (int kk = 0; kk < NKK; ++kk) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w0r[fb][kk], xr[kk], acc, 0, 0, 0);
+          for (int kk = 0; kk < NKK; ++kk)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w0r[fb][kk], xr[kk], acc, 0, 0, 0);
+        } else {
+          const h16x8 ah = *(const h16x8*)(w0f + ((2 * fb) * 64 + lane) * 16);
+          const h16x8 al = *(const h16x8*)(w0f + ((2 * fb + 1) * 64 + lane) * 16);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xh, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xl, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, xh, acc, 0, 0, 0);
+        }
         return acc;
       };
       f32x16 acc = l0_mfma(0);

@@ -155,4 +155,32 @@ __global__ __launch_bounds__(KS_THREADS) void ksse_bwd_kernel(KsseBwdArgs a) {
   }
 }
 
+// Gaussian Fourier features (features.py:31-41): out[r] = [sin(2 pi x_r B), cos(2 pi x_r B)],
+// x [rows, cin], B [cin, m], out [rows, 2 m]; one launch for the reference's matmul, scale, sin,
+// cos and cat. The argument is formed as the reference does (x B, then times 2 pi, fp32) and the
+// accurate sinf / cosf take it (|2 pi x B| reaches hundreds of radians at scale 21).
+struct FourierArgs {
+  const float* x;
+  const float* B;
+  float* out;
+  int64_t rows;
+  int cin, m;
+};
+
+__global__ __launch_bounds__(KS_THREADS) void fourier_kernel(FourierArgs a) {
+  const int64_t n = a.rows * a.m;
+  const int64_t stride = (int64_t)gridDim.x * KS_THREADS;
+  for (int64_t q = (int64_t)blockIdx.x * KS_THREADS + threadIdx.x; q < n; q += stride) {
+    const int64_t r = q / a.m;
+    const int k = (int)(q - r * a.m);
+    float z = 0.f;
+    for (int c = 0; c < a.cin; ++c) z = fmaf(a.x[r * a.cin + c], a.B[c * a.m + k], z);
+    const float arg = __fmul_rn(6.2831854820251465f, z);  // (float)(2 pi), as 2 * np.pi * z in fp32
+    float sv, cv;
+    sincosf(arg, &sv, &cv);
+    a.out[r * 2 * a.m + k] = sv;
+    a.out[r * 2 * a.m + a.m + k] = cv;
+  }
+}
+
 }  // namespace siren

@@ -95,9 +95,17 @@ long long* g_ring_prof = nullptr;   // debug: pair_ring segment cycle counters, 
 int g_ring_prof_n = 0;
 long long* g_fused_prof = nullptr;
 int g_fwd_dbg = 0;  // debug timing: fused_fwd_pipe_kernel skip bits (results wrong unless 0)  // debug: per-workgroup phase cycle counters of the fused forward
+// Wide first layer (5..16 inputs: Fourier features): the register-resident forward only, with at
+// most FREG_WIDE_MAXH hidden layers; P_0 is kept (the layer-1 backward reads it).
+bool fused_wide(const siren_mlp_desc* d) { return d->dims[0] > FUSED_MAXC && d->dims[0] <= 16; }
 bool fused_shape(const siren_mlp_desc* d) {
   if (d->prec != SIREN_PREC_BF16) return false;
-  if (d->dims[0] > FUSED_MAXC || d->dims[d->num_layers] > FUSED_MAXO) return false;
+  if (d->dims[d->num_layers] > FUSED_MAXO) return false;
+  if (fused_wide(d)) {
+    if (!g_fwd_reg || d->num_layers - 2 < 1 || d->num_layers - 2 > FREG_WIDE_MAXH) return false;
+  } else if (d->dims[0] > FUSED_MAXC) {
+    return false;
+  }
   const int F = d->dims[1];
   if (F != 256) return false;
   for (int l = 1; l < d->num_layers; ++l)
@@ -117,7 +125,7 @@ bool fused_shape(const siren_mlp_desc* d) {
 // path is no longer taken by fused shapes.
 bool g_keep_p0 = false;  // debug: fused shapes keep P_0 (the stored-P_0 path) instead of rebuilding it
 bool p0_recompute(const siren_mlp_desc* d) {
-  if (g_keep_p0 || !fused_shape(d) || d->num_layers < 3) return false;
+  if (g_keep_p0 || !fused_shape(d) || fused_wide(d) || d->num_layers < 3) return false;
   const int64_t C = d->dims[0], total = d->batch * d->rows_per_batch;
   return total * C >= 1;
 }
@@ -534,6 +542,7 @@ int fused_forward_reg(const siren_mlp_desc* d, const Geo& g, const Layout& lo, c
   a.O = d->dims[g.L];
   a.nh = nh;
   a.sine_out = d->outermost_linear ? 0 : 1;
+  a.cin = d->dims[0];
   a.w0 = d->w0;
   const int64_t tiles = cdiv(g.rows, FREG_WG_ROWS);
   const int64_t per = std::max<int64_t>(1, 256 / g.nb);
@@ -542,8 +551,10 @@ int fused_forward_reg(const siren_mlp_desc* d, const Geo& g, const Layout& lo, c
   static const KernelFn table[2][FUSED_MAXC] = {
       {fused_fwd_reg_kernel<1, 0>, fused_fwd_reg_kernel<2, 0>, fused_fwd_reg_kernel<3, 0>, fused_fwd_reg_kernel<4, 0>},
       {fused_fwd_reg_kernel<1, 1>, fused_fwd_reg_kernel<2, 1>, fused_fwd_reg_kernel<3, 1>, fused_fwd_reg_kernel<4, 1>}};
+  static const KernelFn wide[2] = {fused_fwd_reg_kernel<16, 0>, fused_fwd_reg_kernel<16, 1>};
+  const KernelFn k = fused_wide(d) ? wide[a.O == 1 ? 1 : 0] : table[a.O == 1 ? 1 : 0][d->dims[0] - 1];
   tmark_begin(SIREN_KCLASS_FWD_FUSED, st);
-  hipLaunchKernelGGL(table[a.O == 1 ? 1 : 0][d->dims[0] - 1], grid, dim3(512), 0, st, a);
+  hipLaunchKernelGGL(k, grid, dim3(512), 0, st, a);
   tmark_end(SIREN_KCLASS_FWD_FUSED, st);
   return check_launch("fused_fwd_reg");
 }
@@ -1656,6 +1667,16 @@ int siren_kspace_sse_backward(const float* d, const float* mask, const float* hf
   const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(4096, cdiv(batch * npix, KS_THREADS)));
   hipLaunchKernelGGL(ksse_bwd_kernel, dim3(blocks), dim3(KS_THREADS), 0, (hipStream_t)stream, a);
   return check_launch("kspace_sse_backward");
+}
+
+int siren_fourier_features(const float* x, const float* B, int64_t rows, int cin, int m, float* out, void* stream) {
+  if (rows < 0 || cin < 1 || m < 1 || (rows > 0 && (!x || !B || !out)))
+    return fail(SIREN_EINVAL, "fourier_features: bad arguments (rows=%lld, cin=%d, m=%d)", (long long)rows, cin, m);
+  if (rows == 0) return SIREN_OK;
+  FourierArgs a{x, B, out, rows, cin, m};
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(4096, cdiv(rows * m, KS_THREADS)));
+  hipLaunchKernelGGL(fourier_kernel, dim3(blocks), dim3(KS_THREADS), 0, (hipStream_t)stream, a);
+  return check_launch("fourier_features");
 }
 
 int siren_adam_step(const siren_adam_desc* d, void* stream) {

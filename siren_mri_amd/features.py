@@ -1,6 +1,7 @@
 """Gaussian Fourier features (features.py:6-53 of jonbmartin/siren_mri).
 
 forward: cat(sin(2 pi x B), cos(2 pi x B)) with B = randn(in, m) * scale (features.py:21-41).
+On the GPU the transform is the native op siren_mri_amd::fourier_features (one launch).
 B lives as a buffer on the module's device (the reference keeps it on the CPU and copies it to
 the input's device on every call, features.py:28,36); save_B/load_B/get_B/set_B keep the
 reference's file format (a bare tensor saved with torch.save).
@@ -9,6 +10,48 @@ from __future__ import annotations
 
 import numpy as np
 import torch
+
+from . import _native
+from .ops import _LIB
+
+# siren_mri_amd::fourier_features(x, B) -> cat(sin(2 pi x B), cos(2 pi x B)) (one native launch);
+# its gradient w.r.t. x (the reference differentiates through it when x requires grad) is the
+# PyTorch expression's, recomputed on the backward (B is a constant buffer)
+_LIB.define("fourier_features(Tensor x, Tensor B) -> Tensor")
+
+
+def _ff_cuda(x, B):
+    xc, Bc = x.contiguous(), B.contiguous()
+    cin, m = Bc.shape
+    out = torch.empty(xc.shape[:-1] + (2 * m,), dtype=torch.float32, device=x.device)
+    rows = xc.numel() // cin
+    _native.check(_native.lib().siren_fourier_features(xc.data_ptr(), Bc.data_ptr(), rows, cin, m, out.data_ptr(),
+                                                       _native.stream_handle(x.device)), "siren_fourier_features")
+    return out
+
+
+class _FFAutograd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, B):
+        with torch._C._AutoDispatchBelowAutograd():
+            out = torch.ops.siren_mri_amd.fourier_features(x, B)
+        ctx.save_for_backward(x, B)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, B = ctx.saved_tensors
+        m = B.shape[1]
+        z = 2 * np.pi * (x @ B)
+        gs, gc = g[..., :m], g[..., m:]
+        dz = gs * torch.cos(z) - gc * torch.sin(z)
+        return (2 * np.pi) * (dz @ B.t()), None
+
+
+_LIB.impl("fourier_features", _ff_cuda, "CUDA")
+_LIB.impl("fourier_features", lambda x, B: _FFAutograd.apply(x, B), "Autograd")
+torch.library.register_fake("siren_mri_amd::fourier_features",
+                            lambda x, B: x.new_empty(x.shape[:-1] + (2 * B.shape[1],)), lib=_LIB)
 
 
 class GaussianFourierFeatureTransform(torch.nn.Module):
@@ -22,6 +65,8 @@ class GaussianFourierFeatureTransform(torch.nn.Module):
             self.to(device)
 
     def forward(self, x):
+        if x.is_cuda and x.dtype == torch.float32:
+            return torch.ops.siren_mri_amd.fourier_features(x, self._B_spatial.to(x.device, x.dtype))
         z = x @ self._B_spatial.to(x.device, x.dtype)
         z = 2 * np.pi * z
         return torch.cat([torch.sin(z), torch.cos(z)], dim=-1)

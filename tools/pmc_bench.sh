@@ -6,7 +6,7 @@ TAG=$1; shift
 R=$(pwd)
 mkdir -p "$R/gpurun_out"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/${TAG}_pmc1" -o run --output-format csv -- \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE -d "$R/gpurun_out/${TAG}_pmc1" -o run --output-format csv -- \
     python "$R/bench.py" "$@" > "$R/gpurun_out/${TAG}_pmc1.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/${TAG}_pmc2" -o run --output-format csv -- \
     python "$R/bench.py" "$@" > "$R/gpurun_out/${TAG}_pmc2.log" 2>&1

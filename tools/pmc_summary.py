@@ -35,8 +35,12 @@ def main(prefix, json_out=None):
                 for disp, v in vals:
                     per[disp] += v
                 merged[name][c] = sum(per.values()) / max(1, len(per))
-    print("| kernel | HBM read MB (2xFETCH) | HBM write MB | MFMA busy % | VALU active % | wait % |")
-    print("|---|---:|---:|---:|---:|---:|")
+    # SQ_VALU_MFMA_BUSY_CYCLES is a cycle count summed over the SIMDs (32 per 32x32x16 MFMA);
+    # GRBM_GUI_ACTIVE is the kernel's active cycles summed over the 8 XCDs (MI355X_MICROARCH.md):
+    # MFMA busy % = busy / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
+    print("| kernel | HBM read MB (2xFETCH) | HBM write MB | MFMA busy cycles (sum over SIMDs) | MFMA busy % | "
+          "VALU active % | wait % |")
+    print("|---|---:|---:|---:|---:|---:|---:|")
     rows = []
     for name, c in merged.items():
         short = name.split("(")[0].replace("void ", "")[-60:]
@@ -46,11 +50,13 @@ def main(prefix, json_out=None):
         mfma = c.get("SQ_VALU_MFMA_BUSY_CYCLES", float("nan"))
         valu = c.get("SQ_ACTIVE_INST_VALU", float("nan"))
         wait = c.get("SQ_WAIT_ANY", float("nan"))
-        rows.append((rd + (wr if wr == wr else 0), name, short, rd, wr, mfma, valu, wait, wc, c))
+        gui = c.get("GRBM_GUI_ACTIVE", float("nan"))
+        mpct = 100 * mfma / (1024 * gui / 8) if gui == gui and gui > 0 else float("nan")
+        rows.append((rd + (wr if wr == wr else 0), name, short, rd, wr, (mfma, mpct), valu, wait, wc, c))
     rows.sort(key=lambda r: -r[0] if r[0] == r[0] else 0)
     for _, name, short, rd, wr, mfma, valu, wait, wc, c in rows:
-        print(f"| `{short}` | {rd:.1f} | {wr:.1f} | {mfma:.3g} | {100 * valu / wc if wc else float('nan'):.1f} | "
-              f"{100 * wait / wc if wc else float('nan'):.1f} |")
+        print(f"| `{short}` | {rd:.1f} | {wr:.1f} | {mfma[0]:.3g} | {mfma[1]:.1f} | "
+              f"{100 * valu / wc if wc else float('nan'):.1f} | {100 * wait / wc if wc else float('nan'):.1f} |")
     if json_out:
         # per-kernel HBM bytes per launch, keyed by the kernel symbol without `void ` and arguments
         d = {}
