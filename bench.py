@@ -256,6 +256,9 @@ def c4_batch(dev, n_slices, seed=0):
 
 
 def build_c4(args, dev, rank, world, precision, encoder_precision="bf16"):
+    # MIOpen's find (autotuned) convolution algorithms for the encoder: its few conv shapes are
+    # searched once during the warm-up steps
+    torch.backends.cudnn.benchmark = True
     from functools import partial
     from siren_mri_amd import loss_functions, meta_modules, training
     from siren_mri_amd.features import GaussianFourierFeatureTransform
@@ -304,7 +307,7 @@ def build_c4(args, dev, rank, world, precision, encoder_precision="bf16"):
                     "synthetic k-space (IRData slices x flips/rotations + seeded ellipses, fftshift(fft2)), "
                     "seeded CS-Cartesian masks, FF B = randn(2, 8) * 21 (seed 0)",
                     {"optimizer": opt, "encoder_flops_per_step": enc, "encoder_precision": encoder_precision,
-                     "model": model, "inp": inp})
+                     "model": model, "inp": inp, "conv_algorithms": "MIOpen find (torch.backends.cudnn.benchmark)"})
 
 
 def build(cfg, args, dev, rank, world, precision=None):
@@ -381,6 +384,12 @@ def run_timed(wl, args, dev, world, kclass=None, max_launches=4096):
             del gk, g1
         except Exception as e:  # noqa: BLE001 - reported, then timed eagerly
             print(f"bench: hipGraph capture failed ({type(e).__name__}: {e}); timing eager steps", file=sys.stderr)
+            opt = wl.extra.get("optimizer")
+            if opt is not None and hasattr(opt, "_native_reject"):
+                for g in opt.param_groups:
+                    r = opt._native_reject(g)
+                    if r:
+                        print(f"bench:   optimizer group not native: {r}", file=sys.stderr)
             torch.cuda.synchronize()
     kt = None
     if kclass is not None:

@@ -121,11 +121,14 @@ class _SineMLPJVPAutograd(torch.autograd.Function):
         ctx.meta = meta
         ctx.save_for_backward(x, saved, *params)
         ctx.mark_non_differentiable(saved)
+        ctx.set_materialize_grads(False)
         return out, saved
 
     @staticmethod
     def backward(ctx, dout, _dsaved):
         w0, prec, batched, order, n, keep = ctx.meta
+        if dout is None:
+            return (None,) * (2 + 2 * n)
         if not keep:
             raise RuntimeError("siren_mri_amd: the tangent-stream forward ran without keeping its streams "
                                "(grad mode was off); it cannot be differentiated")

@@ -138,10 +138,13 @@ class _KspaceSSEAutograd(torch.autograd.Function):
         ctx.save_for_backward(d, mask, hf)
         ctx.noise, ctx.weight = noise, weight
         ctx.mark_non_differentiable(d)
+        ctx.set_materialize_grads(False)
         return loss, d
 
     @staticmethod
     def backward(ctx, g, _gd):
+        if g is None:
+            return (None,) * 7
         d, mask, hf = ctx.saved_tensors
         dpred = torch.ops.siren_mri_amd.kspace_sse_bwd(d, mask, hf, g, ctx.noise, 2.0 * ctx.weight)
         return dpred, None, None, None, None, None, None

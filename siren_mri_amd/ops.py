@@ -221,11 +221,15 @@ class _SineMLPAutograd(torch.autograd.Function):
         ctx.meta = meta
         ctx.save_for_backward(x, saved, *params)
         ctx.mark_non_differentiable(saved)
+        # no zero-filled gradient for the uint8 saved buffer (a full-size fill kernel per step)
+        ctx.set_materialize_grads(False)
         return y, saved
 
     @staticmethod
     def backward(ctx, dy, _dsaved):
         w0, prec, outermost_linear, batched, n, keep = ctx.meta
+        if dy is None:
+            return (None,) * (2 + 2 * n)
         if not keep:
             raise RuntimeError("siren_mri_amd: the SIREN forward ran without keeping activations "
                                "(grad mode was off); it cannot be differentiated")

@@ -41,29 +41,33 @@ class Adam(torch.optim.Adam):
                 if p in self.state and "step" in self.state[p]:
                     self.state[p]["step"].fill_(t)
 
-    def _native_ok(self, group) -> bool:
+    def _native_reject(self, group):
+        """Why a group cannot take the native step (None when it can)."""
         if group["amsgrad"] or group.get("capturable") or group.get("differentiable") or group.get("fused"):
-            return False
+            return "amsgrad/capturable/differentiable/fused flag"
         if group.get("decoupled_weight_decay", False):
-            return False
+            return "decoupled_weight_decay"
         if any(isinstance(group[k], torch.Tensor) for k in ("lr",)) or any(
                 isinstance(b, torch.Tensor) for b in group["betas"]):
-            return False
+            return "tensor-valued lr/betas"
         for p in group["params"]:
             if p.grad is None:
                 continue
             if not p.is_cuda or p.dtype != torch.float32 or p.grad.is_sparse or p.grad.dtype != torch.float32:
-                return False
+                return f"param {tuple(p.shape)}: device/dtype ({p.device}, {p.dtype}, grad {p.grad.dtype})"
             # the update is elementwise over the storage: any dense layout (row-major, or the conv
             # encoder's channels-last weights) works when the gradient and the moments share it
             if not (p.is_contiguous() or p.is_contiguous(memory_format=torch.channels_last)):
-                return False
+                return f"param {tuple(p.shape)}: not dense (strides {p.stride()})"
             if p.grad.stride() != p.stride():
-                return False
+                return f"param {tuple(p.shape)}: grad strides {p.grad.stride()} != param strides {p.stride()}"
             st = self.state.get(p)
             if st and "exp_avg" in st and (st["exp_avg"].stride() != p.stride() or st["exp_avg_sq"].stride() != p.stride()):
-                return False
-        return True
+                return f"param {tuple(p.shape)}: moment strides differ from the parameter's"
+        return None
+
+    def _native_ok(self, group) -> bool:
+        return self._native_reject(group) is None
 
     @torch.no_grad()
     def step(self, closure=None):

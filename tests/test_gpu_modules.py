@@ -104,3 +104,31 @@ def test_hypernetwork_backward_reaches_hypernet_params():
             assert p.grad.norm().item() == pytest.approx(float(d[key]), rel=1e-3), n
             checked += 1
     assert checked > 0
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", (1e-5, 1e-4)), ("bf16", (2e-3, 2e-2))])
+def test_hypo256_batched_against_reference_fixture(precision, tol):
+    """The configs-4/5 hypo-network at its real width (16-256-256-256-256-2, per-slice weights, the
+    path HyperNetwork feeds) on the native stack against the REFERENCE's own outputs and gradients
+    (hypo256.npz, tests/golden/make_golden_r3.py); bf16 runs the wide-first-layer register forward."""
+    from test_oracle_golden import hypo256_params
+    from siren_mri_amd import dataio, features, modules
+    d = np.load(os.path.join(G, "hypo256.npz"), allow_pickle=False)
+    torch.manual_seed(4)
+    net = modules.SingleBVPNet(out_features=2, type="sine", in_features=16, hidden_features=256,
+                               num_hidden_layers=3, precision=precision).to(DEV)
+    params = {}
+    for i, (W, b) in enumerate(hypo256_params()):
+        params[f"net.net.{i}.0.weight"] = W.to(DEV).requires_grad_(True)
+        params[f"net.net.{i}.0.bias"] = b.to(DEV).requires_grad_(True)
+    ff = features.GaussianFourierFeatureTransform(2, 8, loaded_B=torch.from_numpy(d["B_ff"]), device=DEV)
+    x = ff(dataio.get_mgrid(64)[None].repeat(2, 1, 1).to(DEV))
+    y = net({"coords": x}, params=params)["model_out"]
+    (y * torch.from_numpy(d["lw"]).to(DEV)).sum().backward()
+    ty, tg = tol
+    assert orc.norm_rel(y.detach().cpu(), torch.from_numpy(d["y"])) < ty
+    assert orc.norm_rel(params["net.net.0.0.weight"].grad.cpu(), torch.from_numpy(d["dW0"])) < tg
+    assert orc.norm_rel(params["net.net.4.0.weight"].grad.cpu(), torch.from_numpy(d["dW4"])) < tg
+    norms = np.array([[params[f"net.net.{i}.0.weight"].grad.norm().item(),
+                       params[f"net.net.{i}.0.bias"].grad.norm().item()] for i in range(5)])
+    np.testing.assert_allclose(norms, d["grad_norms"], rtol=tg)

@@ -64,6 +64,12 @@ def test_config4_siren_batched_32x16384():
     _check([16, 256, 256, 256, 256, 2], 32, 16384, seed=3)
 
 
+def test_config4_small_siren_in120_32x16384():
+    # hyperoptIV_homebrew_small (train_mri_neural_process_ddp.py:114-128): 60 Fourier features ->
+    # 120 inputs, past the register forward's 16; runs on the per-layer bf16 kernels (MFMA first layer)
+    _check([120, 256, 256, 256, 256, 2], 32, 16384, seed=4)
+
+
 @pytest.mark.parametrize("C", [5, 7, 12, 16])
 def test_wide_inputs_shared_ragged(C):
     _check([C, 256, 256, 256, 1], None, 70000 + C, seed=C, need_dx=True)

@@ -144,3 +144,30 @@ def test_fourier_features_and_dc():
     assert orc.norm_rel(ff, torch.from_numpy(d["ff"])) < 1e-6
     dc = orc.data_consistency(torch.from_numpy(d["pred"]), torch.from_numpy(d["k0"]), torch.from_numpy(d["mask"]))
     assert np.array_equal(dc.numpy(), d["dc"])
+
+
+def hypo256_params(B=2):
+    """The per-slice parameters of hypo256.npz (tests/golden/make_golden_r3.py `batched_params`):
+    the reference init under seed 4, weights x (1 + 0.1 g), biases + 0.01 g, generator seed 11."""
+    base = orc.siren_init([16, 256, 256, 256, 256, 2], seed=4)
+    g = torch.Generator().manual_seed(11)
+    out = []
+    for W, b in base:
+        Wb = (W.unsqueeze(0).repeat(B, 1, 1) * (1 + 0.1 * torch.randn(B, 1, 1, generator=g))).contiguous()
+        bb = (b.unsqueeze(0).repeat(B, 1) + 0.01 * torch.randn(B, b.shape[0], generator=g)).contiguous()
+        out.append((Wb, bb))
+    return out
+
+
+def test_hypo256_batched_siren_matches_reference():
+    """The 256-wide hypo-network with per-slice weights (configs 4/5) against the reference itself."""
+    d = load("hypo256.npz")
+    ps = [(W.clone().requires_grad_(True), b.clone().requires_grad_(True)) for W, b in hypo256_params()]
+    x = orc.fourier_features(orc.get_mgrid(64)[None].repeat(2, 1, 1), torch.from_numpy(d["B_ff"]))
+    y = orc.siren_forward(x, ps)
+    (y * torch.from_numpy(d["lw"])).sum().backward()
+    assert orc.norm_rel(y.detach(), torch.from_numpy(d["y"])) < 1e-6
+    assert orc.norm_rel(ps[0][0].grad, torch.from_numpy(d["dW0"])) < 1e-5
+    assert orc.norm_rel(ps[-1][0].grad, torch.from_numpy(d["dW4"])) < 1e-5
+    norms = np.array([[W.grad.norm().item(), b.grad.norm().item()] for W, b in ps])
+    np.testing.assert_allclose(norms, d["grad_norms"], rtol=1e-5)
