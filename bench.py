@@ -188,13 +188,14 @@ def build_fit(cfg, args, dev, rank, world, precision):
     opt = training.make_adam(model.parameters(), 1e-4)
     reducer = GradAllReducer(model.parameters(), op="sum") if world > 1 else None
     model_input = {"coords": coords}
+    one = torch.ones((), device=dev)  # the backward's seed, allocated once (not a fill kernel per step)
 
     def step():
         out = model(model_input)
         # image_mse's reduction (sum / 128^2) over this rank's coordinates: in a strong-scaling
         # shard the partial sums over the ranks add up to the whole image's loss
         loss = loss_functions.weighted_sse(out["model_out"], tgt)
-        loss.backward()
+        loss.backward(one)
         if reducer is not None:
             reducer()
         opt.step()

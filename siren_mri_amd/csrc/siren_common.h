@@ -140,33 +140,51 @@ DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t bytes) {
                                            (int)(bytes > 0x7fffffff ? 0x7fffffff : bytes), 0x00020000);
 }
 
-// Buffer stores whose data registers may be rewritten right after them. Measured on MI355X
-// (tools/det_p0.py, profiles/r3_store_hazard.txt): in the register-resident forward, with LDS-DMA
-// traffic in flight, a buffer_store_dwordx4 followed by a VALU write of its first data VGPR
-// (v_cvt_pknorm_u16_f32, one wait state later as hipcc 7.2 schedules it; also with 16 s_nop wait
-// states in between) stored the NEW value in lanes 12-15 of each 16-lane group, nondeterministically
-// (the corrupted dword equals the one the next epilogue part writes). An s_waitcnt vmcnt(0) after
-// the store, or an s_waitcnt expcnt(0) right after it, removes it: the store's data read from the
-// VGPRs is tracked by EXP_CNT, and the compiler does not wait for it. So these stores are issued as
-// inline asm together with that wait (which returns once the data has left the VGPRs — it does
-// not wait for the write itself). The asm stores still count in vmcnt, which the kernels' counted
-// ring waits include.
+// Buffer stores whose data VGPRs are rewritten soon after them. Measured on MI355X
+// (tools/det_p0.py, tools/det_wide.py, profiles/r3_store_hazard.txt): in the register-resident
+// forward, under the ring's LDS-DMA traffic, a buffer_store_dwordx4 whose first data VGPR is
+// rewritten by a VALU instruction shortly after the store (one to a few instructions later, as
+// hipcc schedules it) sometimes stores the NEW value in lanes 12-15 of each 16-lane group: the
+// store reads its data after issue, later than the documented one-wait-state hazard covers.
+// Neither 16 s_nop wait states nor s_waitcnt expcnt(0) between the store and the write prevent it
+// (the expcnt form only moved the failure: det_wide.py still caught it at C = 16, where the VALU
+// write after the last hidden block's store is the output layer's fragment-address add). What
+// does: the store having COMPLETED (s_waitcnt vmcnt) before its data VGPRs are written again.
+// So each such store is followed by store_complete(data): an s_waitcnt vmcnt(0) that takes the
+// store's data as an input operand, so the compiler keeps those registers unmodified (and nothing
+// else allocated into them) until the store has completed. vmcnt counts in issue order, so the
+// wait also covers older vector-memory operations (the ring DMA of the kernels is issued far
+// enough ahead to have landed by then).
+template <typename T>
+DEV void store_complete(const T& data) {
+  asm volatile("s_waitcnt vmcnt(0)" ::"v"(data));
+}
+// the same for two stores' data (the older one held until here)
+template <typename T, typename U>
+DEV void store_complete2(const T& data, const U& held) {
+  asm volatile("s_waitcnt vmcnt(0)" ::"v"(data), "v"(held));
+}
 #ifndef SIREN_STORE_EXPCNT
 #define SIREN_STORE_EXPCNT 1
 #endif
 DEV void store_b128_sync(const u32x4_t& v, __amdgpu_buffer_rsrc_t r, uint32_t voff) {
-#if SIREN_STORE_EXPCNT
-  asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_waitcnt expcnt(0)" ::"v"(v), "v"(voff), "s"(r)
-               : "memory");
-#else
   __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, 0, 0);
+#if SIREN_STORE_EXPCNT
+  store_complete(v);
 #endif
 }
-// The ring backward kernels (siren_gemm.hip) keep the compiler's buffer stores: there the asm form
-// made the gradients nondeterministic (tools/det_bwd.py, profiles/r3_store_hazard.txt: 5 of 5
-// runs differ at ~1e-3 with the expcnt wait, ~1e-1 without it; the builtin form: 0 of 5 here and in
-// every determinism test). In that code the asm store's descriptor SGPRs are rewritten a few
-// instructions later (s_and_saveexec into them), which the compiler's own stores avoid.
+DEV void store_b32_sync(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, 0, 0);
+#if SIREN_STORE_EXPCNT
+  store_complete(v);
+#endif
+}
+// The ring backward kernels (siren_gemm.hip) keep the compiler's buffer stores without the wait: a
+// vmcnt(0) per store would drain their three-tile DMA ring. Their data registers stay untouched for
+// 20-60 instructions after each store, and no run-to-run difference was ever observed there
+// (tools/det_bwd.py, test_backward_deterministic). As inline asm (the compiler then reuses the data
+// registers right after the asm) they differed in 5 of 5 runs: ~1e-1 without a wait, ~1e-3 with
+// expcnt(0) (profiles/r3_store_hazard.txt) — the same hazard.
 // Diagnostic builds: 0 builtin store (default), 1 store_b128_sync, 2 asm store without the wait,
 // 3 builtin store + a separate expcnt(0).
 #ifndef SIREN_GEMM_STORE
@@ -182,14 +200,6 @@ DEV void store_b128_gemm(const u32x4_t& v, __amdgpu_buffer_rsrc_t r, uint32_t vo
   asm volatile("s_waitcnt expcnt(0)" ::: "memory");
 #else
   __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, 0, 0);
-#endif
-}
-DEV void store_b32_sync(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff) {
-#if SIREN_STORE_EXPCNT
-  asm volatile("buffer_store_dword %0, %1, %2, 0 offen\n\ts_waitcnt expcnt(0)" ::"v"(v), "v"(voff), "s"(r)
-               : "memory");
-#else
-  __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, 0, 0);
 #endif
 }
 DEV void store_b32_gemm(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff) {

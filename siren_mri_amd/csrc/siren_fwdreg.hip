@@ -50,6 +50,10 @@ constexpr int FREG_W0F_BYTES = 16384;  // [8 fb][hi, lo][64 lanes][16 B]
 #define SIREN_FREG_SYNC 2
 #endif
 constexpr int FREG_SYNC = SIREN_FREG_SYNC;
+// 1: one vmcnt(0) per block for both phase-code stores (the first store's data held until then)
+#ifndef SIREN_FREG_STORE_PAIR
+#define SIREN_FREG_STORE_PAIR 0
+#endif
 // cache-policy bits of the phase-code stores (timing experiments: 2 = nt)
 #ifndef SIREN_FREG_STORE_AUX
 #define SIREN_FREG_STORE_AUX 0
@@ -166,6 +170,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   __shared__ __attribute__((aligned(16))) float xs[2][WIDE ? 4 : FREG_WG_ROWS * 4];
   __shared__ __attribute__((aligned(16))) char w0f[WIDE ? FREG_W0F_BYTES : 16];  // wide layer-0 fragments
   __shared__ __attribute__((aligned(16))) float sbl[8];
+  __shared__ __attribute__((aligned(16))) float w0s[WIDE ? 4 : NB * NKK * 64];  // narrow layer-0 A operands
 
 #ifdef SIREN_FREG_DBG
   // timing builds only (compile-time, so the schedule of the rest is unchanged): 1: no hidden-
@@ -208,17 +213,15 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   if (tid == FREG_WL_BYTES / 16) *(u32x4_t*)(wlf + FREG_WL_BYTES) = u32x4_t{0u, 0u, 0u, 0u};
 
   // layer-0 weights as f32 MFMA A operands (lane (i, k): W_0[32 fb + phi(i)][2 kk + k] w0/2pi)
-  const int phij = freg_phi(j);
   const int cin = WIDE ? a.cin : C;
-  float w0r[NB][NKK];
+  // (staged in LDS, [fb][kk][lane], and read per layer-0 MFMA: as registers they were 8-16 VGPRs
+  // held across the whole kernel, which spilled the C = 3, 4 forms)
   if constexpr (!WIDE) {
-#pragma unroll
-    for (int fb = 0; fb < NB; ++fb)
-#pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) {
-        const int col = 2 * kk + hh;
-        w0r[fb][kk] = col < C ? a.W0[(wb * F + 32 * fb + phij) * C + col] * k1 : 0.f;
-      }
+    for (int i = tid; i < NB * NKK * 64; i += 512) {
+      const int fb = i / (NKK * 64), kk = (i >> 6) % NKK, ln = i & 63;
+      const int col = 2 * kk + (ln >> 5);
+      w0s[i] = col < C ? a.W0[(wb * F + 32 * fb + freg_phi(ln & 31)) * C + col] * k1 : 0.f;
+    }
   } else {
     // wide: thread (fb, lane (i, kh)) stages the f16 hi and lo A fragments of block fb,
     // W_0[32 fb + phi(i)][8 kh + m] w0/2pi (zero past the inputs)
@@ -238,25 +241,34 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
 
   // ---- LDS-DMA: ring blocks and x tiles ----
   // block (layer, fb) of hidden layer `layer` into ring slot fb (the slot of every layer's block fb)
+  // (a buffer resource over the weight set's blocks: one per-lane offset VGPR, the block offset in
+  // SOFFSET — a per-lane 64-bit source address was a register pair the wide form spilled)
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(wsrc, (int64_t)nh * NB * FREG_SLOT);
+  const uint32_t wvoff = wave * 2048 + lane * 16;
   auto dma_block = [&](int layer, int fb) {
-    const char* src = (const char*)(wsrc + ((int64_t)layer * NB + fb) * (FREG_SLOT / 2)) + wave * 2048 + lane * 16;
+    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)((layer * NB + fb) * FREG_SLOT));
     char* dst = slot(fb) + wave * 2048;
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst, 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(src + 1024), (lds_void*)(dst + 1024), 16, 0, 0);
+    // (the instruction's immediate offset would move the LDS destination too: SOFFSET carries it)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)dst, 16, wvoff, soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(dst + 1024), 16, wvoff, soff + 1024, 0, 0);
   };
   // wide: the lane's 8 inputs 8 hh .. 8 hh + 7 of its row of tile t, straight from global memory
   // into registers (rows past the end and inputs past cin read as 0); issued a layer ahead
-  float xw[8];
+  float xw[WIDE ? 8 : 1];
   auto load_xw = [&](int64_t t) {
+    if constexpr (!WIDE) return;
     const int64_t r0 = t * FREG_WG_ROWS;
     const int64_t nv = rows - r0 < 0 ? 0 : (rows - r0 < FREG_WG_ROWS ? rows - r0 : FREG_WG_ROWS);
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x + (batch * rows + r0) * cin, nv * cin * 4);
-    const int rbase = (wave * FREG_WROWS + j) * cin;
+    // two 16-byte loads from the lane's first input (dword-aligned; inputs past cin belong to the
+    // next row and are zeroed, rows past the end read as 0 through the resource)
+    const uint32_t xv = (uint32_t)((wave * FREG_WROWS + j) * cin + 8 * hh) * 4;
+    const u32x4_t v0 = __builtin_amdgcn_raw_buffer_load_b128(rx, xv, 0, 0);
+    const u32x4_t v1 = __builtin_amdgcn_raw_buffer_load_b128(rx, xv, 16, 0);
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
-      const int col = 8 * hh + m;
-      const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rx, (rbase + (col < cin ? col : 0)) * 4, 0, 0);
-      xw[m] = col < cin ? __builtin_bit_cast(float, v) : 0.f;
+      const uint32_t v = m < 4 ? v0[m] : v1[m - 4];
+      xw[m] = 8 * hh + m < cin ? __builtin_bit_cast(float, v) : 0.f;
     }
   };
   // x rows of workgroup tile t (C KB; rows past the end arrive as zeros): waves 0..C-1, 1 KB each
@@ -314,15 +326,25 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     return make_rsrc((const void*)(((uint64_t)hi << 32) | lo), nb);
   };
   const int p_voff = (wave * FREG_WROWS + j) * (F * 2) + hh * 16;
-  auto p_store = [&](int pl, int pfb, int half, const u32x4_t& c) {
+  // The block's two 16-byte code stores. A store's data VGPRs must not be rewritten before the
+  // store has completed (siren_common.h, the store hazard): store_b128_sync waits vmcnt(0) after
+  // it. (Holding the first store's data until the second store's wait — one wait per block —
+  // needs 4 more VGPRs than this kernel has: 11-23 spilled.)
+  auto p_store = [&](int pl, int pfb, int half, const u32x4_t& c, const u32x4_t& held) {
     if constexpr ((dbg & 4) != 0) return;
     if constexpr ((dbg & 32) != 0) {  // timing only: the same bytes as one contiguous 1 KB per store
       __builtin_amdgcn_raw_buffer_store_b128(c, p_rsrc(pl), wave * 16384 + lane * 16, (pfb * 2 + half) * 1024, 0);
       return;
     }
-    // data-read-ordered store (siren_common.h store_b128_sync: a plain store here lost its first
-    // dword to the next epilogue part's write in a few lanes, nondeterministically)
-    store_b128_sync(c, p_rsrc(pl), p_voff + pfb * 64 + half * 32);
+    // the block offset as the store's constant SOFFSET (one address VGPR for every store: folding
+    // it into the VGPR offset costs a register per store and spilled)
+    __builtin_amdgcn_raw_buffer_store_b128(c, p_rsrc(pl), p_voff, pfb * 64 + half * 32, 0);
+#if SIREN_FREG_STORE_PAIR
+    // one wait per block: the half-0 store's data stays reserved (an input of the half-1 wait)
+    if (half == 1) store_complete2(c, held);
+#else
+    store_complete(c);
+#endif
   };
 
   // Epilogue of one accumulator, in 8 parts of 2 elements (part p: elements 2p, 2p + 1, packed
@@ -331,6 +353,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   struct Epi {
     uint32_t hp[4];
     uint32_t cp[4];
+    u32x4_t held;  // SIREN_FREG_STORE_PAIR: the half-0 store's data until the half-1 store's wait
   };
   auto epi_part = [&](Epi& ep, const f32x16& acc, int p, h16x8& t0h, h16x8& t1h, int pl, int pfb,
                       auto codes_tag) {
@@ -360,7 +383,10 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
       const u32x4_t c = codes ? u32x4_t{ep.cp[0], ep.cp[1], ep.cp[2], ep.cp[3]} : u32x4_t{0u, 0u, 0u, 0u};
       if (p == 3) t0h = __builtin_bit_cast(h16x8, hq);
       else t1h = __builtin_bit_cast(h16x8, hq);
-      if constexpr (codes) p_store(pl, pfb, p == 3 ? 0 : 1, c);
+      if constexpr (codes) {
+        p_store(pl, pfb, p == 3 ? 0 : 1, c, ep.held);
+        if (p == 3) ep.held = c;
+      }
     }
   };
 
@@ -470,13 +496,17 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     const int64_t nv = rows - r0 < FREG_WG_ROWS ? rows - r0 : FREG_WG_ROWS;
     const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.y + (batch * rows + r0) * O, nv * O * 4);
     const int yrow = wave * FREG_WROWS + j;
+    // one address VGPR for the lane's outputs 4 hh .. 4 hh + 3, the output index as the constant
+    // SOFFSET (per-output address registers were spilled across the kernel)
+    const uint32_t yv = (uint32_t)(yrow * O + 4 * hh) * 4;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int o = 4 * hh + e;
-      if (o < O) {
+      if (4 * hh + e < O) {
         float z = accO[e];
         if (a.sine_out) z = Prec<kPrecBF16>::sinr(w0 * z);
-        store_b32_sync(__builtin_bit_cast(uint32_t, z), ry, (yrow * O + o) * 4);
+        const uint32_t zb = __builtin_bit_cast(uint32_t, z);
+        __builtin_amdgcn_raw_buffer_store_b32(zb, ry, yv, 4 * e, 0);
+        store_complete(zb);
       }
     }
   };
@@ -528,7 +558,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
         if constexpr (!WIDE) {
 #pragma unroll
           for (int kk = 0; kk < NKK; ++kk)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w0r[fb][kk], xr[kk], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w0s[(fb * NKK + kk) * 64 + lane], xr[kk], acc, 0, 0, 0);
         } else {
           const h16x8 ah = *(const h16x8*)(w0f + ((2 * fb) * 64 + lane) * 16);
           const h16x8 al = *(const h16x8*)(w0f + ((2 * fb + 1) * 64 + lane) * 16);

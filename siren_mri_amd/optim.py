@@ -17,6 +17,13 @@ import torch
 from . import _native
 
 
+def _same_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Same element order in storage: equal strides on every dimension longer than 1 (a 1x1 conv
+    weight's channels-last gradient has strides (C, 1, C, C) against the parameter's (C, 1, 1, 1):
+    the size-1 dimensions' strides carry no layout)."""
+    return a.shape == b.shape and all(sa == sb for n, sa, sb in zip(a.shape, a.stride(), b.stride()) if n > 1)
+
+
 class Adam(torch.optim.Adam):
     """torch.optim.Adam whose step is one native launch (see the module docstring).
 
@@ -59,10 +66,10 @@ class Adam(torch.optim.Adam):
             # encoder's channels-last weights) works when the gradient and the moments share it
             if not (p.is_contiguous() or p.is_contiguous(memory_format=torch.channels_last)):
                 return f"param {tuple(p.shape)}: not dense (strides {p.stride()})"
-            if p.grad.stride() != p.stride():
+            if not _same_layout(p.grad, p):
                 return f"param {tuple(p.shape)}: grad strides {p.grad.stride()} != param strides {p.stride()}"
             st = self.state.get(p)
-            if st and "exp_avg" in st and (st["exp_avg"].stride() != p.stride() or st["exp_avg_sq"].stride() != p.stride()):
+            if st and "exp_avg" in st and not (_same_layout(st["exp_avg"], p) and _same_layout(st["exp_avg_sq"], p)):
                 return f"param {tuple(p.shape)}: moment strides differ from the parameter's"
         return None
 

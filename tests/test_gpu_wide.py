@@ -46,6 +46,12 @@ def _check(dims, B, N, seed, tol=(2e-3, 2e-2), need_dx=False):
     (y * lw.to(DEV)).sum().backward()
     torch.cuda.synchronize()
     errs = {"y": orc.norm_rel(y.detach().cpu(), y_ref.detach())}
+    # the last rows of every weight set: their inputs come through 16-byte loads that cross the end
+    # of x (bounded per dword by the buffer resource); a dropped input would show as an O(1) row
+    # error that the norm over ~10^5 rows hides
+    yl, rl = y.detach().cpu()[..., -3:, :], y_ref.detach()[..., -3:, :]
+    scale = float(y_ref.detach().pow(2).mean().sqrt())
+    assert float((yl - rl).abs().max()) <= 0.05 * scale, (yl, rl)
     for l, (w, b, (rW, rb)) in enumerate(zip(ws, bs, ps)):
         errs[f"dW{l}"] = orc.norm_rel(w.grad.cpu(), rW.grad)
         errs[f"db{l}"] = orc.norm_rel(b.grad.cpu(), rb.grad)
@@ -66,8 +72,9 @@ def test_config4_siren_batched_32x16384():
 
 def test_config4_small_siren_in120_32x16384():
     # hyperoptIV_homebrew_small (train_mri_neural_process_ddp.py:114-128): 60 Fourier features ->
-    # 120 inputs, past the register forward's 16; runs on the per-layer bf16 kernels (MFMA first layer)
-    _check([120, 256, 256, 256, 256, 2], 32, 16384, seed=4)
+    # 120 inputs, past the register forward's 16; runs on the per-layer bf16 kernels (MFMA first layer
+    # on bf16 x and W_0, no hi/lo split: y ~5e-3 norm-relative, the bf16-operand forward's level)
+    _check([120, 256, 256, 256, 256, 2], 32, 16384, seed=4, tol=(1e-2, 2e-2))
 
 
 @pytest.mark.parametrize("C", [5, 7, 12, 16])

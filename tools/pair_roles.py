@@ -1,7 +1,7 @@
 """Time each pair_ring_bf16_kernel role alone (debug_pair_roles 1 / 2) against both (3) at the
 bench workload: which role bounds the paired launch, and what the shared tiles save.
 
-    python tools/pair_roles.py [--side 512]
+    python tools/pair_roles.py   (the bench's metric configuration)
 """
 import argparse
 import os
@@ -18,16 +18,15 @@ from siren_mri_amd import _native  # noqa: E402
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--side", type=int, default=512)
     p.add_argument("--reps", type=int, default=10)
     p.add_argument("--roles", type=int, nargs="*", default=[3, 1, 2, 3])
     p.add_argument("--option", default=None, help="NAME=V1,V2: repeat every role set per option value")
     cli = p.parse_args()
-    sys.argv = [sys.argv[0], "--side", str(cli.side), "--no-psnr", "--no-cpu-baseline"]
+    sys.argv = [sys.argv[0], "--no-psnr", "--no-cpu-baseline", "--no-other-configs"]
     args = bench.parse()
     _native.load_library()
     dev = torch.device("cuda", 0)
-    step, _ = bench.build_step(args, dev, 0, 1)
+    step = bench.build("m", args, dev, 0, 1).step
     for _ in range(5):
         step()
     torch.cuda.synchronize()
