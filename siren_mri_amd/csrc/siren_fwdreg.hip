@@ -52,7 +52,7 @@ constexpr int FREG_W0F_BYTES = 16384;  // [8 fb][hi, lo][64 lanes][16 B]
 constexpr int FREG_SYNC = SIREN_FREG_SYNC;
 // 1: one vmcnt(0) per block for both phase-code stores (the first store's data held until then)
 #ifndef SIREN_FREG_STORE_PAIR
-#define SIREN_FREG_STORE_PAIR 0
+#define SIREN_FREG_STORE_PAIR 1
 #endif
 // cache-policy bits of the phase-code stores (timing experiments: 2 = nt)
 #ifndef SIREN_FREG_STORE_AUX

@@ -1,36 +1,48 @@
 """Static check of the store-hazard rule (siren_common.h) on a disassembled code object:
-    llvm-objdump -d lib.co > lib.dis; python tools/check_store_hazard.py lib.dis [kernel-substring] [--all-operands]
-For every buffer / scratch / global store in the matching kernels, report any instruction that writes one of the
-store's data VGPRs (--all-operands: also its address VGPR and descriptor SGPRs) before an
-s_waitcnt vmcnt(0), the only wait that guarantees the store has read them."""
+    llvm-objdump -d lib.co > lib.dis
+    python tools/check_store_hazard.py lib.dis [kernel-substring] [--all-operands]
+For every buffer / scratch / global store in the matching kernels, follow every control-flow path
+from the store (branch targets included) and report an instruction that writes one of the store's
+data VGPRs (--all-operands: also the address VGPR and descriptor SGPRs of buffer stores) before an
+s_waitcnt vmcnt(0) — the only wait that guarantees the store has read them — or the program end.
+Exit status 1 if any store violates the rule."""
 import re
 import sys
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 path = args[0]
 filt = args[1] if len(args) > 1 else "fused_fwd_reg_kernel"
-text = open(path).read().split("\n")
-kernels = {}
+ALL = "--all-operands" in sys.argv
+
+kernels = {}  # name -> (base address, [(addr, ins, target addr or None)])
 cur = None
-for line in text:
-    m = re.match(r"^[0-9a-f]+ <(\S+)>:", line)
+for line in open(path).read().split("\n"):
+    m = re.match(r"^([0-9a-f]+) <(\S+)>:", line)
     if m:
-        cur = m.group(1) if filt in m.group(1) else None
+        cur = m.group(2) if filt in m.group(2) else None
         if cur:
-            kernels[cur] = []
+            kernels[cur] = (int(m.group(1), 16), [])
         continue
-    if cur and line.strip():
-        ins = re.sub(r"^\s*[0-9a-f]+:\s+(?:[0-9a-f]{8} ?)+", "", line).split("//")[0].strip()
-        if ins:
-            kernels[cur].append(ins)
+    if not cur or not line.strip():
+        continue
+    m = re.match(r"^\s*(\S.*?)\s*//\s*([0-9A-Fa-f]+):[^<]*(?:<(\S+?)(?:\+0x([0-9a-f]+))?>)?", line)
+    if not m:
+        continue
+    ins, addr = m.group(1).strip(), int(m.group(2), 16)
+    tgt = None
+    if m.group(3) and ins.startswith(("s_branch", "s_cbranch")):
+        base = kernels[cur][0] if m.group(3) == cur else None
+        if base is not None:
+            tgt = base + int(m.group(4) or "0", 16)
+    kernels[cur][1].append((addr, ins, tgt))
 
 
-def regs(tok):
+def vregs(tok):
     m = re.match(r"v\[(\d+):(\d+)\]", tok)
     if m:
-        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+        return {("v", r) for r in range(int(m.group(1)), int(m.group(2)) + 1)}
     m = re.match(r"v(\d+)$", tok)
-    return {int(m.group(1))} if m else set()
+    return {("v", int(m.group(1)))} if m else set()
 
 
 def sregs(tok):
@@ -41,57 +53,72 @@ def sregs(tok):
     return {("s", int(m.group(1)))} if m else set()
 
 
-def operands(ins):
-    """Registers a buffer store reads: data VGPRs, the address VGPR, the descriptor SGPRs."""
-    ops = [t.strip() for t in ins.split(None, 1)[1].split(",")]
-    out = set(regs(ops[0]))
-    if len(ops) > 1:
-        out |= regs(ops[1])
-    if len(ops) > 2:
-        out |= sregs(ops[2])
-    return out
+def ops(ins):
+    t = ins.split(None, 1)
+    return [x.strip() for x in t[1].split(",")] if len(t) > 1 else []
 
 
-def swrites(ins):
-    op = ins.split()[0]
-    if not op.startswith("s_") or op.startswith(("s_waitcnt", "s_nop", "s_barrier", "s_cbranch", "s_branch",
-                                                 "s_setprio", "s_sleep", "s_endpgm")):
-        return set()
-    toks = ins.split(None, 1)
-    return sregs(toks[1].split(",")[0].strip()) if len(toks) > 1 else set()
+def store_regs(ins):
+    o = ops(ins)
+    if ins.startswith("buffer_store"):
+        r = vregs(o[0])
+        if ALL:
+            r |= vregs(o[1]) | (sregs(o[2]) if len(o) > 2 else set())
+        return r
+    return vregs(o[1]) if len(o) > 1 else set()  # scratch_store / global_store ADDR, DATA
 
 
 def writes(ins):
     op = ins.split()[0]
-    if op.startswith(("buffer_store", "global_store", "ds_write", "s_", "scratch_store", "global_load_lds",
-                      "buffer_load_dword") ) and "lds" in ins:
+    if op.startswith(("buffer_store", "global_store", "scratch_store", "ds_write")) or "_lds" in op:
         return set()
-    if op.startswith(("buffer_store", "global_store", "ds_write", "s_", "scratch_store")):
+    o = ops(ins)
+    if not o:
         return set()
-    toks = ins.split(None, 1)
-    if len(toks) < 2:
-        return set()
-    return regs(toks[1].split(",")[0].strip())
+    if op.startswith("s_"):
+        if op.startswith(("s_waitcnt", "s_nop", "s_barrier", "s_cbranch", "s_branch", "s_setprio", "s_sleep",
+                          "s_endpgm", "s_dcache", "s_sethalt", "s_trap")):
+            return set()
+        return sregs(o[0])
+    return vregs(o[0]) | sregs(o[0])
 
 
-bad = 0
-nstores = 0
-for k, body in kernels.items():
-    for i, ins in enumerate(body):
+bad = nstores = 0
+for name, (base, body) in kernels.items():
+    index = {addr: i for i, (addr, _, _) in enumerate(body)}
+
+    def succ(i):
+        addr, ins, tgt = body[i]
+        if ins.startswith("s_endpgm"):
+            return []
+        out = []
+        if tgt is not None and tgt in index:
+            out.append(index[tgt])
+        if not ins.startswith("s_branch") and i + 1 < len(body):
+            out.append(i + 1)
+        return out
+
+    for i, (_, ins, _) in enumerate(body):
         if not ins.startswith(("buffer_store", "scratch_store", "global_store")):
             continue
         nstores += 1
-        first = ins.split(None, 1)[1].split(",")
-        # buffer_store DATA, ADDR, SRD ...; scratch_store ADDR|off, DATA, ...; global_store ADDR, DATA, ...
-        dtok = first[0].strip() if ins.startswith("buffer_store") else first[1].strip()
-        data = operands(ins) if "--all-operands" in sys.argv and ins.startswith("buffer_store") else regs(dtok)
-        for j in range(i + 1, len(body)):
-            if re.match(r"s_waitcnt .*vmcnt\(0\)", body[j]) or body[j].startswith("s_endpgm"):
+        data = store_regs(ins)
+        seen, stack, hit = set(), list(succ(i)), None
+        while stack and hit is None:
+            j = stack.pop()
+            if j in seen:
+                continue
+            seen.add(j)
+            w = body[j][1]
+            if re.match(r"s_waitcnt .*vmcnt\(0\)", w):
+                continue
+            if writes(w) & data:
+                hit = j
                 break
-            w = (writes(body[j]) | swrites(body[j])) & data
-            if w:
-                bad += 1
-                print(f"{k[:60]} #{i}: {ins}  <- written {j - i} later by: {body[j]}")
-                break
-print(f"{len(kernels)} kernels, {nstores} stores, {bad} with an operand register rewritten before vmcnt(0)")
+            stack.extend(succ(j))
+        if hit is not None:
+            bad += 1
+            print(f"{name[:60]} @{body[i][0]:x}: {ins}  <- written @{body[hit][0]:x}: {body[hit][1]}")
+print(f"{len(kernels)} kernels, {nstores} stores, {bad} with a {'store operand' if ALL else 'data'} register "
+      "rewritten before vmcnt(0) on some path")
 sys.exit(1 if bad else 0)
