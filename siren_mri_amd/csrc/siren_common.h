@@ -9,6 +9,13 @@
 
 namespace siren {
 
+// shape limits of the fused kernels (siren_fused.hip, siren_fwdreg.hip)
+constexpr int FUSED_MAXC = 4;   // coordinate inputs of the narrow fused forms
+constexpr int FUSED_MAXO = 8;   // outputs
+constexpr int FUSED_MAXH = 14;  // hidden layers
+// LDS address space (LDS-DMA destinations)
+typedef __attribute__((address_space(3))) void lds_void;
+
 constexpr float kInv2Pi = 0.15915494309189535f;
 constexpr int kPrecF32 = 0;
 constexpr int kPrecBF16 = 1;

@@ -28,9 +28,6 @@
 namespace siren {
 
 constexpr int FUSED_BM = 128;
-constexpr int FUSED_MAXC = 4;
-constexpr int FUSED_MAXO = 8;
-constexpr int FUSED_MAXH = 14;
 
 struct FusedFwdArgs {
   const float* x;                 // [rows, C]

@@ -59,6 +59,17 @@ constexpr int FREG_SYNC = SIREN_FREG_SYNC;
 #define SIREN_FREG_STORE_AUX 0
 #endif
 static_assert(FREG_SYNC == 1 || FREG_SYNC == 2, "ring sync interval");
+// 1: hidden-layer accumulators start at bias + FREG_MAGIC revolutions (see epi_part)
+#ifndef SIREN_FREG_MAGIC
+#define SIREN_FREG_MAGIC 1
+#endif
+#ifndef SIREN_FREG_FORCE  // timing only: 1 fract form, 2 magic form, regardless of the weights
+#define SIREN_FREG_FORCE 0
+#endif
+constexpr float FREG_MAGIC = 192.0f;  // 1.5 x 2^7: [128, 256) has an fp32 ulp of exactly 2^-16
+// The magic form holds while |fract(b) + z - b| < 63 revolutions for every feature: the hidden
+// layers' inputs are sines, so k1 sum_k |W_fk| < FREG_MAGIC_BOUND (prep_reg_kernel's wbound) is enough.
+constexpr float FREG_MAGIC_BOUND = 62.0f;
 // Vector-memory operations a wave has issued after the ring refill it must see land (every block
 // issues two phase stores — a null tensor's are still issued and dropped by their resource — and
 // every refill of a slot two DMAs):
@@ -88,6 +99,7 @@ struct FwdRegArgs {
   const _Float16* WLreg;      // [nb_w][16 ks][2 h][8 rows][8] prepared output fragments
   const float* bias[FUSED_MAXH];
   const float* bL;            // [nb_w][O]
+  const float* wbound;        // [nb_w][nh][F] k1 sum_k |W_l[f][k]| (prep_reg_kernel); null: fract form
   void* P0;                   // phase codes of sine layer 0 (null: not kept)
   char* Pb;                   // phase codes of sine layer 1 (null: none kept); layer l at Pb + (l - 1) pstride
   int64_t pstride;
@@ -141,7 +153,32 @@ DEV void freg_lgkm(h16x8& v) {
   asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "n"(N));
 }
 
-template <int C, int OC>
+// Prepared weights of the register-resident forward (see the header comment):
+//   hidden: Wreg[b][l][fb][ks][lane][m] = f16(W_l[b][32 fb + phi(lane & 31)][in0(ks, lane >> 5) + m] w0/2pi)
+//   output: WLreg[b][ks][h][i][m] = f16(W_L[b][i][in0(ks, h) + m]) (0 for i >= O)
+// and, optionally, the backward's bf16 W_l^T copies.
+struct RegPrepArgs {
+  const float* W[FUSED_MAXH];
+  bf16* Wt[FUSED_MAXH];
+  const float* WL;
+  _Float16* out;
+  _Float16* outL;
+  float* wbound;  // [nb][nh][F] k1 sum_k |W_l[f][k]| (the forward's magic-form check), or null
+  int64_t nb;
+  int nh, O;
+  float k1;
+};
+
+// FORM (SIREN_FREG_MAGIC): 1 = the magic epilogue (epi_part), 0 = the fract epilogue. Both forms are
+// launched back to back; each reads the weight bounds and the one whose form does not apply exits
+// at once (one kernel holding both forms needs more than 256 VGPRs). Without the bounds (null
+// wbound) FORM 0 does the work.
+#ifdef SIREN_FWDREG_DECL_ONLY  // the kernels are compiled in siren_fwdreg_inst.hip
+template <int C, int OC, int FORM>
+__global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a);
+__global__ __launch_bounds__(256) void prep_reg_kernel(RegPrepArgs a);
+#else
+template <int C, int OC, int FORM>
 __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   constexpr int F = 256, NKS = 16, NB = 8;
   constexpr bool WIDE = C > 4;
@@ -203,10 +240,25 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   using F_ = std::false_type;
   const _Float16* wsrc = a.Wreg + wb * (int64_t)nh * F * F;
 
+  // ---- the epilogue form (epi_part): magic unless a hidden row's weights could leave its range ----
+  int unsafe = 1;
+  if (SIREN_FREG_MAGIC && a.wbound) {
+    unsafe = 0;
+    for (int i = tid; i < nh * F; i += 512) unsafe |= !(a.wbound[wb * nh * F + i] < FREG_MAGIC_BOUND);
+  }
+  unsafe = __syncthreads_or(unsafe);
+#if SIREN_FREG_FORCE == 0
+  if (unsafe != (FORM == 0)) return;  // the other form's launch does the work
+#endif
+
   // ---- stage the small per-weight-set operands ----
   for (int i = tid; i < F; i += 512) sbias[i] = a.b0[wb * F + i] * k1;
   for (int l = 0; l < nh; ++l)
-    for (int i = tid; i < F; i += 512) sbias[(l + 1) * F + i] = a.bias[l][wb * F + i] * k1;
+    for (int i = tid; i < F; i += 512) {
+      const float bk = a.bias[l][wb * F + i] * k1;
+      // magic form: the bias reduced mod 1 revolution (sin and the phase code are periodic in it)
+      sbias[(l + 1) * F + i] = unsafe ? bk : __builtin_amdgcn_fractf(bk) + FREG_MAGIC;
+    }
   if (tid < 8) sbl[tid] = tid < O ? a.bL[wb * O + tid] : 0.f;
   if (tid < FREG_WL_BYTES / 16)
     *(u32x4_t*)(wlf + 16 * tid) = *(const u32x4_t*)((const char*)(a.WLreg + wb * (FREG_WL_BYTES / 2)) + 16 * tid);
@@ -290,7 +342,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   freg_barrier();
 
   // ---- helpers ----
-  auto bias_acc = [&](int layer, int fb) -> f32x16 {  // layer 0 = first layer, 1 + l = hidden l
+  auto bias_acc = [&](int layer, int fb) __attribute__((always_inline)) -> f32x16 {  // layer 0 = first layer, 1 + l = hidden l
     const float* bp = sbias + layer * F + 32 * fb + 8 * hh;
     f32x16 r;
 #pragma unroll
@@ -330,7 +382,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   // store has completed (siren_common.h, the store hazard): store_b128_sync waits vmcnt(0) after
   // it. (Holding the first store's data until the second store's wait — one wait per block —
   // needs 4 more VGPRs than this kernel has: 11-23 spilled.)
-  auto p_store = [&](int pl, int pfb, int half, const u32x4_t& c, const u32x4_t& held) {
+  auto p_store = [&](int pl, int pfb, int half, const u32x4_t& c, const u32x4_t& held) __attribute__((always_inline)) {
     if constexpr ((dbg & 4) != 0) return;
     if constexpr ((dbg & 32) != 0) {  // timing only: the same bytes as one contiguous 1 KB per store
       __builtin_amdgcn_raw_buffer_store_b128(c, p_rsrc(pl), wave * 16384 + lane * 16, (pfb * 2 + half) * 1024, 0);
@@ -355,12 +407,35 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     uint32_t cp[4];
     u32x4_t held;  // SIREN_FREG_STORE_PAIR: the half-0 store's data until the half-1 store's wait
   };
+  // Hidden layers (magic_tag true, SIREN_FREG_MAGIC): the accumulator started at bias + 192, so it
+  // holds 192 + z with z the phase in revolutions; while |z| < 64 the sum lies in [128, 256), whose
+  // fp32 ulp is exactly 2^-16 revolution, so its low 16 mantissa bits ARE the phase code
+  // round(fract(z) 2^16) mod 2^16 (one v_perm_b32 packs two), and v_sin_f32 (revolutions, domain
+  // +-256, exact reduction) takes the accumulator as it is: no v_fract_f32, no v_cvt_pknorm_u16 —
+  // 24 instead of 32 issue cycles per element pair. The runtime checks |z| < 64 for every row of
+  // every hidden layer from the weights (prep_reg_kernel; the inputs are sines, |h| <= 1) and
+  // takes the fract form when it does not hold.
   auto epi_part = [&](Epi& ep, const f32x16& acc, int p, h16x8& t0h, h16x8& t1h, int pl, int pfb,
-                      auto codes_tag) {
+                      auto codes_tag, auto magic_tag) __attribute__((always_inline)) {
     constexpr bool codes = decltype(codes_tag)::value;  // false: the phases are not kept
+    constexpr bool magic = decltype(magic_tag)::value;
     typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
     h16x2 hv;
     float f0, f1;
+    if constexpr (magic && (dbg & 64) == 0) {
+      hv[0] = (_Float16)__builtin_amdgcn_sinf(acc[2 * p]);
+      hv[1] = (_Float16)__builtin_amdgcn_sinf(acc[2 * p + 1]);
+      uint32_t hpk = __builtin_bit_cast(uint32_t, hv);
+      asm volatile("" : "+v"(hpk));
+      ep.hp[p & 3] = hpk;
+      if constexpr (codes) {
+        // (elements copied to scalars first: hipcc 7.2's __builtin_bit_cast of an ext_vector element
+        // reads element 0 whatever the index)
+        const float a0 = acc[2 * p], a1 = acc[2 * p + 1];
+        ep.cp[p & 3] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, a1), __builtin_bit_cast(uint32_t, a0),
+                                             0x05040100u);  // low halves: a1 << 16 | a0
+      }
+    } else {
     if constexpr ((dbg & 64) != 0) {  // timing only: convert without fract / sin
       f0 = acc[2 * p];
       f1 = acc[2 * p + 1];
@@ -378,6 +453,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     asm volatile("" : "+v"(hpk));
     ep.hp[p & 3] = hpk;
     if constexpr (codes) ep.cp[p & 3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pknorm_u16(f0, f1));
+    }
     if ((p & 3) == 3) {
       const u32x4_t hq = {ep.hp[0], ep.hp[1], ep.hp[2], ep.hp[3]};
       const u32x4_t c = codes ? u32x4_t{ep.cp[0], ep.cp[1], ep.cp[2], ep.cp[3]} : u32x4_t{0u, 0u, 0u, 0u};
@@ -413,7 +489,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   // slot of the block before it is free: refill it with (l + 1 mod nh, fb - 1), or (l, 7) at
   // fb = 0. FREG_SYNC 2 (even fb): slots fb + 1 and fb + 2 have landed; slots fb - 2 and fb - 1
   // are free: refill them with layer l + 1 mod nh (at fb = 0: slots 6 and 7 with layer l).
-  auto block_sync = [&](int l, int fb) {
+  auto block_sync = [&](int l, int fb) __attribute__((always_inline)) {
     if constexpr ((dbg & 2) != 0) return;
     if (FREG_SYNC == 2 && (fb & 1)) {
       ++kblk;
@@ -441,9 +517,11 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
 
   // one hidden layer l: Hin -> Hout (runtime l; register arrays bound at the call site;
   // last_tag: whether the output layer follows — its fragments are prefetched at the end)
-  auto hidden_layer = [&](int l, h16x8 (&Hin)[NKS], h16x8 (&Hout)[NKS], auto last_tag) {
+  auto hidden_layer = [&](int l, h16x8 (&Hin)[NKS], h16x8 (&Hout)[NKS], auto last_tag, auto mtag) __attribute__((always_inline)) {
     constexpr bool last = decltype(last_tag)::value;
-    static_for<0, NB>([&](auto fb_c) {
+    // block fb (ptag: the form of the pending epilogue — at fb = 0 of hidden layer 0 it is layer 0's
+    // last block, always in the fract form)
+    auto blk = [&](auto fb_c, auto ptag) __attribute__((always_inline)) {
       constexpr int fb = decltype(fb_c)::value;
       block_sync(l, fb);
       if (fb == 0 && l == 0) dma_x(tcur + G, (int)(((tcur - t0) / G + 1) & 1));  // next round's x
@@ -461,8 +539,8 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
         if constexpr (!(dbg & 16)) accN = __builtin_amdgcn_mfma_f32_32x32x16_f16(wq[ks & 3], Hin[ks], accN, 0, 0, 0);
         constexpr int part = freg_part_at(ks);
         if constexpr (part >= 0 && !(dbg & 1)) {
-          if constexpr (fb == 0) epi_part(ep, accP, part, Hin[14], Hin[15], pend_pl, 7, T_{});
-          else epi_part(ep, accP, part, Hout[2 * fb - 2], Hout[2 * fb - 1], l + 1, fb - 1, T_{});
+          if constexpr (fb == 0) epi_part(ep, accP, part, Hin[14], Hin[15], pend_pl, 7, T_{}, ptag);
+          else epi_part(ep, accP, part, Hout[2 * fb - 2], Hout[2 * fb - 1], l + 1, fb - 1, T_{}, ptag);
         }
         if constexpr (ks == NKS - 2) {  // the pending epilogue is done: the next block's bias
           if constexpr (fb + 1 < NB) accNx = bias_acc(l + 1, fb + 1);
@@ -472,11 +550,19 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
       });
       accP = accN;
       pend_pl = l + 1;
+    };
+    static_for<0, NB>([&](auto fb_c) {
+      if constexpr (decltype(fb_c)::value == 0) {
+        if (l == 0) blk(fb_c, F_{});
+        else blk(fb_c, mtag);
+      } else {
+        blk(fb_c, mtag);
+      }
     });
   };
 
   // output layer: y = H W_L^T + b_L (MFMA rows = outputs), beside the last hidden block's epilogue
-  auto output_layer = [&](h16x8 (&Hin)[NKS]) {
+  auto output_layer = [&](h16x8 (&Hin)[NKS], auto mtag) __attribute__((always_inline)) {
     if constexpr (WIDE) load_xw(tcur + G);  // the next round's inputs
     f32x16 accO = accNx;
     Epi ep;
@@ -489,7 +575,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
       freg_lgkm<PFD>(wq[ks & 3]);
       accO = __builtin_amdgcn_mfma_f32_32x32x16_f16(wq[ks & 3], Hin[ks], accO, 0, 0, 0);
       constexpr int part = freg_part_at(ks);
-      if constexpr (part >= 0) epi_part(ep, accP, part, Hin[14], Hin[15], pend_pl, 7, T_{});
+      if constexpr (part >= 0) epi_part(ep, accP, part, Hin[14], Hin[15], pend_pl, 7, T_{}, mtag);
     });
     // y[row][o], o = 4 h + e (rows 0..7 of the output accumulator are lanes' elements 0..3)
     const int64_t r0 = tcur * FREG_WG_ROWS;
@@ -519,6 +605,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     freg_read<2048>(wq[2], va0);
   }
 
+  auto run = [&](auto mtag) __attribute__((always_inline)) {
   for (int64_t t = t0; t < ntiles; t += G) {
     tcur = t;
     {
@@ -537,7 +624,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
       freg_barrier();
     }
     // ---- layer 0 (f32 MFMA, K = C): blocks 0..6 converted here, block 7 beside hidden block 0 ----
-    auto layer0 = [&](auto codes_tag) {
+    auto layer0 = [&](auto codes_tag) __attribute__((always_inline)) {
       const float* xt = xs[xb] + (wave * FREG_WROWS + j) * C;
       float xr[NKK];
       h16x8 xh, xl;  // wide: the f16 hi / lo B fragments of the inputs
@@ -553,7 +640,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
       }
       // block fb + 1's MFMAs are issued before block fb's epilogue (its result latency and the
       // bias reads overlap the conversion)
-      auto l0_mfma = [&](int fb) {
+      auto l0_mfma = [&](int fb) __attribute__((always_inline)) {
         f32x16 acc = bias_acc(0, fb);
         if constexpr (!WIDE) {
 #pragma unroll
@@ -576,7 +663,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
           Epi ep;
           if constexpr (!(dbg & 8))
 #pragma unroll
-            for (int p = 0; p < 8; ++p) epi_part(ep, acc, p, Ha[2 * fb], Ha[2 * fb + 1], 0, fb, codes_tag);
+            for (int p = 0; p < 8; ++p) epi_part(ep, acc, p, Ha[2 * fb], Ha[2 * fb + 1], 0, fb, codes_tag, F_{});
           acc = accn;
         } else {
           accP = acc;
@@ -594,18 +681,27 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     }
     int l = 0;
     for (; l + 2 < nh; l += 2) {
-      hidden_layer(l, Ha, Hb, F_{});
-      hidden_layer(l + 1, Hb, Ha, F_{});
+      hidden_layer(l, Ha, Hb, F_{}, mtag);
+      hidden_layer(l + 1, Hb, Ha, F_{}, mtag);
     }
     if (nh - l == 2) {
-      hidden_layer(l, Ha, Hb, F_{});
-      hidden_layer(l + 1, Hb, Ha, T_{});
-      output_layer(Ha);
+      hidden_layer(l, Ha, Hb, F_{}, mtag);
+      hidden_layer(l + 1, Hb, Ha, T_{}, mtag);
+      output_layer(Ha, mtag);
     } else {
-      hidden_layer(l, Ha, Hb, T_{});
-      output_layer(Hb);
+      hidden_layer(l, Ha, Hb, T_{}, mtag);
+      output_layer(Hb, mtag);
     }
   }
+  };
+#if SIREN_FREG_FORCE == 1
+  run(F_{});
+#elif SIREN_FREG_FORCE == 2
+  run(T_{});
+#else
+  if constexpr (FORM == 1) run(T_{});
+  else run(F_{});
+#endif
   // no LDS-DMA may land after the workgroup has released its LDS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef SIREN_FREG_CLOCK
@@ -619,21 +715,6 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   }
 #endif
 }
-
-// Prepared weights of the register-resident forward (see the header comment):
-//   hidden: Wreg[b][l][fb][ks][lane][m] = f16(W_l[b][32 fb + phi(lane & 31)][in0(ks, lane >> 5) + m] w0/2pi)
-//   output: WLreg[b][ks][h][i][m] = f16(W_L[b][i][in0(ks, h) + m]) (0 for i >= O)
-// and, optionally, the backward's bf16 W_l^T copies.
-struct RegPrepArgs {
-  const float* W[FUSED_MAXH];
-  bf16* Wt[FUSED_MAXH];
-  const float* WL;
-  _Float16* out;
-  _Float16* outL;
-  int64_t nb;
-  int nh, O;
-  float k1;
-};
 
 __global__ __launch_bounds__(256) void prep_reg_kernel(RegPrepArgs a) {
   constexpr int F = 256;
@@ -668,6 +749,22 @@ __global__ __launch_bounds__(256) void prep_reg_kernel(RegPrepArgs a) {
       *(h16x8*)(a.outL + o * 8) = v;
     }
   }
+  if (a.wbound) {  // one wave per hidden-layer row: k1 sum_k |W_l[b][f][k]|
+    const int64_t nrow = a.nb * a.nh * F;
+    const int lane = threadIdx.x & 63;
+    for (int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6; r < nrow; r += ((int64_t)gridDim.x * 256) >> 6) {
+      const int64_t f = r % F, lb = r / F;
+      const int l = (int)(lb % a.nh);
+      const int64_t b = lb / a.nh;
+      const f32x4 v = *(const f32x4*)(a.W[l] + (b * F + f) * F + 4 * lane);
+      float s = fabsf(v[0]) + fabsf(v[1]) + fabsf(v[2]) + fabsf(v[3]);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+      if (lane == 0) a.wbound[r] = s * a.k1;
+    }
+  }
 }
+
+#endif  // SIREN_FWDREG_DECL_ONLY
 
 }  // namespace siren

@@ -111,7 +111,6 @@ DEV void lds_barrier() {
 }
 DEV void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-typedef __attribute__((address_space(3))) void lds_void;
 
 template <int MODE, int KMAX, bool TOP = false, bool BOT = false>
 __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {

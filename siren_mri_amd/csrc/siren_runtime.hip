@@ -12,6 +12,7 @@
 #include "siren_gemm.hip"
 #include "siren_jvp.hip"
 #include "siren_fused.hip"
+#define SIREN_FWDREG_DECL_ONLY  // its kernels: siren_fwdreg_inst.hip (a translation unit of its own)
 #include "siren_fwdreg.hip"
 #include "siren_adam.hip"
 #include "siren_loss.hip"
@@ -85,6 +86,7 @@ bool g_ring_top = true;    // output layer folded into the top 256x256 layer's r
 bool g_bwd_ring = false;   // middle 256x256 layers in one ring kernel: measured slower (179 vs 145 us)
 bool g_fwd_pipe = true;    // fused forward: half-tile MFMA/VALU pipelined kernel
 bool g_fwd_reg = true;     // fused forward: activations resident in registers (siren_fwdreg.hip)
+bool g_freg_magic = true;  // its hidden layers in the magic epilogue form where the weights allow it
 bool g_dx_ring = true;     // 256x256 input-gradient layers on the 4-stage ring kernel
 bool g_dw_ring = true;     // 256x256 weight-gradient layers on the 4-stage ring kernel
 bool g_pair_ring = true;   // both gradients of a ring layer in one launch (pair_ring_bf16_kernel)
@@ -226,7 +228,9 @@ Layout layout_of(const siren_mlp_desc* d) {
   if (fused_shape(d) && g.L > 2) {
     // hidden-layer fragments, then (register-resident forward) the output-layer fragments
     lo.frag_off = off;
-    off = align_up(off + g.nb * ((int64_t)(g.L - 2) * d->dims[1] * d->dims[1] + FREG_WL_BYTES / 2) * 2, 256);
+    // + the rows' weight bounds of the forward's magic-form check ([nb][L - 2][F] f32)
+    off = align_up(off + g.nb * ((int64_t)(g.L - 2) * d->dims[1] * d->dims[1] + FREG_WL_BYTES / 2) * 2 +
+                       g.nb * (int64_t)(g.L - 2) * d->dims[1] * 4, 256);
   }
   lo.weights_bytes = off;
   lo.p0_rec = p0_recompute(d);
@@ -505,6 +509,7 @@ int fused_forward_reg(const siren_mlp_desc* d, const Geo& g, const Layout& lo, c
   const int F = d->dims[1], nh = g.L - 2;
   _Float16* wreg = (_Float16*)(wbuf + lo.frag_off);
   _Float16* wlreg = wreg + g.nb * (int64_t)nh * F * F;
+  float* wbound = (float*)(wlreg + g.nb * (FREG_WL_BYTES / 2));
   {
     RegPrepArgs p;
     memset(&p, 0, sizeof(p));
@@ -515,11 +520,12 @@ int fused_forward_reg(const siren_mlp_desc* d, const Geo& g, const Layout& lo, c
     p.WL = d->weight[g.L - 1];
     p.out = wreg;
     p.outL = wlreg;
+    p.wbound = wbound;
     p.nb = g.nb;
     p.nh = nh;
     p.O = d->dims[g.L];
     p.k1 = d->w0 * kInv2Pi;
-    const int64_t work = g.nb * ((int64_t)nh * F * F / 8 + FREG_WL_BYTES / 16);
+    const int64_t work = g.nb * ((int64_t)nh * F * F / 8 + FREG_WL_BYTES / 16 + (int64_t)nh * F * 64);
     hipLaunchKernelGGL(prep_reg_kernel, dim3(grid1d(work, 1024)), dim3(256), 0, st, p);
     int rc = check_launch("prep_reg");
     if (rc) return rc;
@@ -533,6 +539,7 @@ int fused_forward_reg(const siren_mlp_desc* d, const Geo& g, const Layout& lo, c
   a.WLreg = wlreg;
   for (int l = 1; l + 1 < g.L; ++l) a.bias[l - 1] = d->bias[l];
   a.bL = d->bias[g.L - 1];
+  a.wbound = wbound;
   a.P0 = (saved && lo.saved_off[0] >= 0) ? saved + lo.saved_off[0] : nullptr;
   a.Pb = saved ? saved + lo.saved_off[1] : nullptr;
   a.pstride = (saved && nh >= 2) ? lo.saved_off[2] - lo.saved_off[1] : 0;
@@ -548,13 +555,19 @@ int fused_forward_reg(const siren_mlp_desc* d, const Geo& g, const Layout& lo, c
   const int64_t per = std::max<int64_t>(1, 256 / g.nb);
   dim3 grid((unsigned)std::min<int64_t>(tiles, per), (unsigned)g.nb);
   using KernelFn = void (*)(FwdRegArgs);
-  static const KernelFn table[2][FUSED_MAXC] = {
-      {fused_fwd_reg_kernel<1, 0>, fused_fwd_reg_kernel<2, 0>, fused_fwd_reg_kernel<3, 0>, fused_fwd_reg_kernel<4, 0>},
-      {fused_fwd_reg_kernel<1, 1>, fused_fwd_reg_kernel<2, 1>, fused_fwd_reg_kernel<3, 1>, fused_fwd_reg_kernel<4, 1>}};
-  static const KernelFn wide[2] = {fused_fwd_reg_kernel<16, 0>, fused_fwd_reg_kernel<16, 1>};
-  const KernelFn k = fused_wide(d) ? wide[a.O == 1 ? 1 : 0] : table[a.O == 1 ? 1 : 0][d->dims[0] - 1];
+#define SIREN_FREG_FORMS(CC, OC) {fused_fwd_reg_kernel<CC, OC, 0>, fused_fwd_reg_kernel<CC, OC, 1>}
+  static const KernelFn table[2][FUSED_MAXC][2] = {
+      {SIREN_FREG_FORMS(1, 0), SIREN_FREG_FORMS(2, 0), SIREN_FREG_FORMS(3, 0), SIREN_FREG_FORMS(4, 0)},
+      {SIREN_FREG_FORMS(1, 1), SIREN_FREG_FORMS(2, 1), SIREN_FREG_FORMS(3, 1), SIREN_FREG_FORMS(4, 1)}};
+  static const KernelFn wide[2][2] = {SIREN_FREG_FORMS(16, 0), SIREN_FREG_FORMS(16, 1)};
+#undef SIREN_FREG_FORMS
+  const KernelFn* k = fused_wide(d) ? wide[a.O == 1 ? 1 : 0] : table[a.O == 1 ? 1 : 0][d->dims[0] - 1];
   tmark_begin(SIREN_KCLASS_FWD_FUSED, st);
-  hipLaunchKernelGGL(k, grid, dim3(512), 0, st, a);
+  // magic form (option freg_magic): both forms are launched, the one whose form does not apply to
+  // these weights exits at its start (siren_fwdreg.hip); otherwise the fract form alone
+  if (g_freg_magic) hipLaunchKernelGGL(k[1], grid, dim3(512), 0, st, a);
+  else a.wbound = nullptr;
+  hipLaunchKernelGGL(k[0], grid, dim3(512), 0, st, a);
   tmark_end(SIREN_KCLASS_FWD_FUSED, st);
   return check_launch("fused_fwd_reg");
 }
@@ -1732,6 +1745,10 @@ int siren_config_set(const char* key, int64_t value) {
     g_fwd_pipe = value != 0;
     return SIREN_OK;
   }
+  if (key && strcmp(key, "freg_magic") == 0 && (value == 0 || value == 1)) {
+    g_freg_magic = value != 0;
+    return 0;
+  }
   if (key && strcmp(key, "fused_forward_reg") == 0 && (value == 0 || value == 1)) {
     g_fwd_reg = value != 0;
     return SIREN_OK;
@@ -1798,6 +1815,7 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "debug_keep_p0") == 0) return g_keep_p0 ? 1 : 0;
   if (key && strcmp(key, "fused_forward_pipe") == 0) return g_fwd_pipe ? 1 : 0;
   if (key && strcmp(key, "fused_forward_reg") == 0) return g_fwd_reg ? 1 : 0;
+  if (key && strcmp(key, "freg_magic") == 0) return g_freg_magic ? 1 : 0;
   return -1;
 }
 

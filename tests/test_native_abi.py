@@ -69,13 +69,14 @@ def test_check_rejects_unsupported(dims, msg):
 
 def test_saved_bytes_formula_bf16():
     """saved = prepared bf16 weights (W, W^T and the fused forward's fragment-order copy of each
-    MFMA layer, plus the register-resident forward's 4 KiB output-layer fragments) + one 16-bit phase tensor per sine layer except the first (recomputed from x by
-    the backward) — 2 bytes per activation element."""
+    MFMA layer, plus the register-resident forward's 4 KiB output-layer fragments and its 4-byte
+    weight bound per hidden row) + one 16-bit phase tensor per sine layer except the first
+    (recomputed from x by the backward) — 2 bytes per activation element."""
     lib = _native.load_library()
     rows = 512 * 512
     d = _desc([2, 256, 256, 256, 256, 1], rows_per_batch=rows)
     got = lib.siren_mlp_saved_bytes(ctypes.byref(d))
-    weights = 3 * 3 * 256 * 256 * 2 + 4096
+    weights = 3 * 3 * 256 * 256 * 2 + 4096 + 3 * 256 * 4
     phases = 3 * rows * 256 * 2
     assert got == weights + phases
 
@@ -87,7 +88,7 @@ def test_saved_bytes_ragged_rows_recompute_p0():
     for rows, batch, batched in ((16385, 1, False), (16415, 5, True)):
         d = _desc([2, 256, 256, 256, 256, 1], rows_per_batch=rows, batch=batch, weights_batched=batched)
         got = lib.siren_mlp_saved_bytes(ctypes.byref(d))
-        weights = batch * (3 * 3 * 256 * 256 * 2 + 4096)
+        weights = batch * (3 * 3 * 256 * 256 * 2 + 4096 + 3 * 256 * 4)
         assert got == weights + 3 * batch * rows * 256 * 2, (rows, batch)
 
 
@@ -95,6 +96,7 @@ def test_config_options():
     lib = _native.load_library()
     assert lib.siren_config_get(b"fused_forward") in (0, 1)
     assert lib.siren_config_get(b"nope") == -1
+    assert lib.siren_config_get(b"freg_magic") == 1
     assert lib.siren_config_set(b"nope", 1) != 0
     assert "unknown option" in _native.last_error()
 

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <cmath>
 #include <algorithm>
 #include <vector>
 
@@ -20,7 +21,10 @@
 #define FWD_THREADS 256
 #else
 #include "siren_fwdreg.hip"
-#define FWD_KERNEL fused_fwd_reg_kernel<2, 1>
+#ifndef FWD_FORM  // 1: the magic epilogue form, 0: the fract form
+#define FWD_FORM 1
+#endif
+#define FWD_KERNEL fused_fwd_reg_kernel<2, 1, FWD_FORM>
 #define FWD_THREADS 512
 #endif
 
@@ -72,6 +76,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&y, rows * O * 4));
   CK(hipMalloc(&wreg, (size_t)nh * F * F * 2));
   CK(hipMalloc(&wlreg, FREG_WL_BYTES));
+  float* wbound;
+  CK(hipMalloc(&wbound, nh * F * 4));
   const int64_t pstride = rows * F * 2;
   CK(hipMalloc(&P, nh * pstride));
   CK(hipMemcpy(x, hx.data(), hx.size() * 4, hipMemcpyHostToDevice));
@@ -89,6 +95,7 @@ int main(int argc, char** argv) {
   p.WL = WL;
   p.out = wreg;
   p.outL = wlreg;
+  p.wbound = wbound;
   p.nb = 1;
   p.nh = nh;
   p.O = O;
@@ -105,6 +112,7 @@ int main(int argc, char** argv) {
   a.WLreg = wlreg;
   for (int l = 0; l < nh; ++l) a.bias[l] = b + l * F;
   a.bL = bL;
+  a.wbound = FWD_FORM ? wbound : nullptr;  // (the fract form exits when the magic form applies)
   a.P0 = nullptr;
   a.Pb = P;
   a.pstride = pstride;
@@ -137,6 +145,25 @@ int main(int argc, char** argv) {
   std::vector<uint16_t> hp(nh * rows * F);
   CK(hipMemcpy(hy.data(), y, rows * 4, hipMemcpyDeviceToHost));
   CK(hipMemcpy(hp.data(), P, nh * pstride, hipMemcpyDeviceToHost));
+  {  // run-to-run: one more launch, bitwise comparison of y and the codes
+    std::vector<float> hy2(rows);
+    std::vector<uint16_t> hp2(nh * rows * F);
+    hipLaunchKernelGGL((FWD_KERNEL), grid, block, 0, 0, a);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(hy2.data(), y, rows * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hp2.data(), P, nh * pstride, hipMemcpyDeviceToHost));
+    int64_t ny = 0, np = 0, fy = -1, fp = -1;
+    for (int64_t i = 0; i < rows; ++i)
+      if (memcmp(&hy[i], &hy2[i], 4)) { ++ny; if (fy < 0) fy = i; }
+    for (int64_t i = 0; i < (int64_t)hp.size(); ++i)
+      if (hp[i] != hp2[i]) { ++np; if (fp < 0) fp = i; }
+    std::vector<float> hb(nh * F);
+    CK(hipMemcpy(hb.data(), wbound, nh * F * 4, hipMemcpyDeviceToHost));
+    float bmax = 0.f;
+    for (float v : hb) bmax = std::max(bmax, v);
+    printf("rerun: y differs in %lld rows (first %lld), codes in %lld (first %lld); wbound max %.3f\n",
+           (long long)ny, (long long)fy, (long long)np, (long long)fp, bmax);
+  }
   double sy = 0.0;
   for (float v : hy) sy += v;
   uint64_t sp = 1469598103934665603ull;
@@ -158,6 +185,46 @@ int main(int argc, char** argv) {
            ghz[ghz.size() / 2], ghz.front(), ghz.back(), cyc[cyc.size() / 2], cyc.back());
   }
 #endif
+  {  // accuracy on the first 1024 rows against a double-precision forward of the fp32 weights:
+     // y, and each stored phase code against round(fract(p / 2 pi) 2^16) (circular code steps)
+    const int nchk = 1024;
+    double ymax = 0.0, yref2 = 0.0, yerr2 = 0.0;
+    long long cmax[8] = {0};
+    double csum[8] = {0};
+    std::vector<double> h(F), z(F);
+    for (int r = 0; r < nchk; ++r) {
+      for (int f = 0; f < F; ++f) {
+        double s = hb0[f];
+        for (int c = 0; c < C; ++c) s += (double)hW0[f * C + c] * hx[r * C + c];
+        h[f] = std::sin(w0 * s);
+      }
+      for (int l = 0; l < nh; ++l) {
+        for (int f = 0; f < F; ++f) {
+          double s = hb[l * F + f];
+          for (int k = 0; k < F; ++k) s += (double)hW[(int64_t)l * F * F + f * F + k] * h[k];
+          z[f] = w0 * s;
+        }
+        for (int f = 0; f < F; ++f) {
+          const double rev = z[f] / (2.0 * M_PI);
+          const long long cref = (long long)std::llround((rev - std::floor(rev)) * 65536.0) & 0xffff;
+          const long long cg = hp[(int64_t)l * rows * F + (int64_t)r * F + f];
+          long long d = std::llabs(cg - cref);
+          d = std::min(d, 65536 - d);
+          cmax[l] = std::max(cmax[l], d);
+          csum[l] += (double)d;
+          h[f] = std::sin(z[f]);
+        }
+      }
+      double yo = hbL[0];
+      for (int k = 0; k < F; ++k) yo += (double)hWL[k] * h[k];
+      ymax = std::max(ymax, std::fabs(yo - hy[r]));
+      yref2 += yo * yo;
+      yerr2 += (yo - hy[r]) * (yo - hy[r]);
+    }
+    printf("check (%d rows): y max-abs %.3e norm-rel %.3e; code steps", nchk, ymax, std::sqrt(yerr2 / yref2));
+    for (int l = 0; l < nh; ++l) printf("  P%d max %lld mean %.2f", l + 1, cmax[l], csum[l] / ((double)nchk * F));
+    printf("\n");
+  }
   printf("forward %.2f us  (%.1f TF/s of %.1f GFLOP)  y-sum %.9e  P-hash %016llx\n", us,
          2.0 * rows * (C * F + nh * F * F + F * O) / (us * 1e-6) / 1e12, 2.0 * rows * (C * F + nh * F * F + F * O) / 1e9,
          sy, (unsigned long long)sp);

@@ -6,10 +6,12 @@ import re
 import subprocess
 import sys
 
-SRC = "siren_mri_amd/csrc/siren_runtime.hip"
-cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-o", "/tmp/_ru.so", SRC,
-       "-Rpass-analysis=kernel-resource-usage"]
-out = subprocess.run(cmd, capture_output=True, text=True).stderr
+SRCS = ("siren_mri_amd/csrc/siren_runtime.hip", "siren_mri_amd/csrc/siren_fwdreg_inst.hip")
+out = ""
+for src in SRCS:
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c", "-o", "/tmp/_ru.o", src,
+           "-Rpass-analysis=kernel-resource-usage"]
+    out += subprocess.run(cmd, capture_output=True, text=True).stderr
 rows, cur = [], None
 for line in out.splitlines():
     m = re.search(r"remark: (.*?) \[-Rpass", line)
