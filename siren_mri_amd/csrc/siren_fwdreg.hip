@@ -51,6 +51,13 @@ constexpr int FREG_W0F_BYTES = 16384;  // [8 fb][hi, lo][64 lanes][16 B]
 #endif
 constexpr int FREG_SYNC = SIREN_FREG_SYNC;
 // 1: one vmcnt(0) per block for both phase-code stores (the first store's data held until then)
+// SIREN_FREG_DEFER 1 (magic form, off): each code store waits vmcnt(1) — for the store before it —
+// instead of its own completion, the older data held in a variable until then. Off: the compiler
+// copied that data to other registers and reused the store's own at once (check_store_hazard.py:
+// 32 stores), so a held value does not pin the registers a store reads.
+#ifndef SIREN_FREG_DEFER
+#define SIREN_FREG_DEFER 0
+#endif
 #ifndef SIREN_FREG_STORE_PAIR
 #define SIREN_FREG_STORE_PAIR 1
 #endif
@@ -113,6 +120,14 @@ struct FwdRegArgs {
   long long* clk;             // diagnostic builds only: [grid][4] s_memtime / s_memrealtime stamps
 #endif
 };
+
+// Every prefetched fragment read has landed (lgkmcnt(0)). The compiler takes an inline-asm read's
+// output as defined at the asm, so register allocation may copy it (v_mov at a control-flow edge:
+// a loop back-edge, a branch) before its counted wait — a copy of bytes not yet landed, seen in
+// round 3 as one wave's block differing in a few runs out of 100. So no fragment read is in flight
+// at a control-flow edge: a drain at the end of every layer and before the round loop
+// (tools/check_lds_hazard.py checks every path of the code object).
+DEV void freg_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 DEV void freg_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -382,6 +397,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   // store has completed (siren_common.h, the store hazard): store_b128_sync waits vmcnt(0) after
   // it. (Holding the first store's data until the second store's wait — one wait per block —
   // needs 4 more VGPRs than this kernel has: 11-23 spilled.)
+  u32x4_t prevst = {0u, 0u, 0u, 0u};  // SIREN_FREG_DEFER: the data of the last code store
   auto p_store = [&](int pl, int pfb, int half, const u32x4_t& c, const u32x4_t& held) __attribute__((always_inline)) {
     if constexpr ((dbg & 4) != 0) return;
     if constexpr ((dbg & 32) != 0) {  // timing only: the same bytes as one contiguous 1 KB per store
@@ -392,8 +408,15 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     // it into the VGPR offset costs a register per store and spilled)
     __builtin_amdgcn_raw_buffer_store_b128(c, p_rsrc(pl), p_voff, pfb * 64 + half * 32, 0);
 #if SIREN_FREG_STORE_PAIR
-    // one wait per block: the half-0 store's data stays reserved (an input of the half-1 wait)
-    if (half == 1) store_complete2(c, held);
+    if constexpr (FORM == 1 && SIREN_FREG_DEFER && !WIDE) {  // (the wide form: 24 VGPRs short)
+      // deferred: vmcnt(1) = every vector-memory operation but this store has completed, so the
+      // previous store (its data held in prevst until this wait) has read its registers
+      asm volatile("s_waitcnt vmcnt(1)" ::"v"(prevst));
+      prevst = c;
+    } else {
+      // one wait per block: the half-0 store's data stays reserved (an input of the half-1 wait)
+      if (half == 1) store_complete2(c, held);
+    }
 #else
     store_complete(c);
 #endif
@@ -423,6 +446,9 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     h16x2 hv;
     float f0, f1;
     if constexpr (magic && (dbg & 64) == 0) {
+#ifdef SIREN_FREG_SINNOP  // diagnostic: extra wait states before the first reads of a finished MFMA chain
+      if (p < 2) asm volatile("s_nop 7\n s_nop 7" ::: "memory");
+#endif
       hv[0] = (_Float16)__builtin_amdgcn_sinf(acc[2 * p]);
       hv[1] = (_Float16)__builtin_amdgcn_sinf(acc[2 * p + 1]);
       uint32_t hpk = __builtin_bit_cast(uint32_t, hv);
@@ -552,13 +578,17 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
       pend_pl = l + 1;
     };
     static_for<0, NB>([&](auto fb_c) {
-      if constexpr (decltype(fb_c)::value == 0) {
+      if constexpr (decltype(fb_c)::value == 0 && decltype(mtag)::value) {
+        // (a runtime branch: no fragment read may be in flight across it — freg_drain before, at
+        // the end of the previous layer, and after, at the end of block 0)
         if (l == 0) blk(fb_c, F_{});
         else blk(fb_c, mtag);
+        freg_drain();
       } else {
         blk(fb_c, mtag);
       }
     });
+    freg_drain();  // the next layer's first fragments (prefetched) land before any control flow
   };
 
   // output layer: y = H W_L^T + b_L (MFMA rows = outputs), beside the last hidden block's epilogue
@@ -595,6 +625,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
         store_complete(zb);
       }
     }
+    freg_drain();  // the next round's first fragments
   };
 
   // first fragments of the stream (later rounds: prefetched by the output layer)
@@ -603,6 +634,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     freg_read<0>(wq[0], va0);
     freg_read<1024>(wq[1], va0);
     freg_read<2048>(wq[2], va0);
+    freg_drain();
   }
 
   auto run = [&](auto mtag) __attribute__((always_inline)) {

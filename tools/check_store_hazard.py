@@ -4,7 +4,9 @@
 For every buffer / scratch / global store in the matching kernels, follow every control-flow path
 from the store (branch targets included) and report an instruction that writes one of the store's
 data VGPRs (--all-operands: also the address VGPR and descriptor SGPRs of buffer stores) before an
-s_waitcnt vmcnt(0) — the only wait that guarantees the store has read them — or the program end.
+s_waitcnt vmcnt(N) with at least N vector-memory operations issued after the store on that path
+(vmcnt counts in issue order: then the store has completed, the only thing that guarantees it has
+read them) — or the program end.
 Exit status 1 if any store violates the rule."""
 import re
 import sys
@@ -103,22 +105,28 @@ for name, (base, body) in kernels.items():
             continue
         nstores += 1
         data = store_regs(ins)
-        seen, stack, hit = set(), list(succ(i)), None
+        # DFS over (instruction, vector-memory operations issued after the store on this path): a
+        # wait vmcnt(N) with at least N of them younger means the store has completed (vmcnt counts
+        # in issue order)
+        seen, stack, hit = set(), [(k, 0) for k in succ(i)], None
         while stack and hit is None:
-            j = stack.pop()
-            if j in seen:
+            j, young = stack.pop()
+            if (j, young) in seen:
                 continue
-            seen.add(j)
+            seen.add((j, young))
             w = body[j][1]
-            if re.match(r"s_waitcnt .*vmcnt\(0\)", w):
+            m = re.match(r"s_waitcnt .*vmcnt\((\d+)\)", w)
+            if m and young >= int(m.group(1)):
                 continue
             if writes(w) & data:
                 hit = j
                 break
-            stack.extend(succ(j))
+            if w.startswith(("buffer_", "global_", "scratch_")):
+                young = min(young + 1, 64)
+            stack.extend((k, young) for k in succ(j))
         if hit is not None:
             bad += 1
             print(f"{name[:60]} @{body[i][0]:x}: {ins}  <- written @{body[hit][0]:x}: {body[hit][1]}")
 print(f"{len(kernels)} kernels, {nstores} stores, {bad} with a {'store operand' if ALL else 'data'} register "
-      "rewritten before vmcnt(0) on some path")
+      "rewritten before the store completed (vmcnt) on some path")
 sys.exit(1 if bad else 0)

@@ -45,6 +45,18 @@ static float urand(float a) {  // uniform in [-a, a]
   return a * (2.f * ((lcg >> 8) * (1.f / 16777216.f)) - 1.f);
 }
 
+// order-dependent hash of a buffer's 32-bit words, one value per workgroup (determinism checks)
+__global__ void hash_kernel(const uint32_t* p, int64_t n, uint32_t* out) {
+  uint32_t h = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    h ^= (p[i] + 0x9e3779b9u * (uint32_t)(i & 0xffff)) * (uint32_t)(2 * i + 1);
+  for (int o = 32; o > 0; o >>= 1) h ^= __shfl_xor(h, o);
+  __shared__ uint32_t sh[4];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = h;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = sh[0] ^ sh[1] ^ sh[2] ^ sh[3];
+}
+
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 50;
   const int64_t side = 512, rows = side * side;
@@ -145,6 +157,52 @@ int main(int argc, char** argv) {
   std::vector<uint16_t> hp(nh * rows * F);
   CK(hipMemcpy(hy.data(), y, rows * 4, hipMemcpyDeviceToHost));
   CK(hipMemcpy(hp.data(), P, nh * pstride, hipMemcpyDeviceToHost));
+  if (argc > 2) {  // determinism: K more launches, each output's hash against the first's
+    const int K = atoi(argv[2]);
+    uint32_t* dh;
+    CK(hipMalloc(&dh, 2 * 1024 * 4));
+    std::vector<uint32_t> h0(2048), h1(2048);
+    int bad = 0;
+    for (int k = 0; k <= K; ++k) {
+      if (k) hipLaunchKernelGGL((FWD_KERNEL), grid, block, 0, 0, a);
+      hipLaunchKernelGGL(hash_kernel, dim3(1024), dim3(256), 0, 0, (const uint32_t*)y, (int64_t)rows * O, dh);
+      hipLaunchKernelGGL(hash_kernel, dim3(1024), dim3(256), 0, 0, (const uint32_t*)P, (int64_t)nh * pstride / 4, dh + 1024);
+      CK(hipMemcpy((k ? h1 : h0).data(), dh, 2048 * 4, hipMemcpyDeviceToHost));
+      if (!k) {
+        CK(hipMemcpy(hy.data(), y, rows * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hp.data(), P, nh * pstride, hipMemcpyDeviceToHost));
+      }
+      if (k && h1 != h0) {
+        int by = 0, bp = 0;
+        for (int i = 0; i < 1024; ++i) { by += h1[i] != h0[i]; bp += h1[i + 1024] != h0[i + 1024]; }
+        if (bad < 5) printf("  launch %d differs: y hash blocks %d, code hash blocks %d\n", k, by, bp);
+        if (bad < 3) {  // where: rows of y, and per phase layer the rows / features / blocks of the codes
+          std::vector<float> yb(rows);
+          std::vector<uint16_t> pb(nh * rows * F);
+          CK(hipMemcpy(yb.data(), y, rows * 4, hipMemcpyDeviceToHost));
+          CK(hipMemcpy(pb.data(), P, nh * pstride, hipMemcpyDeviceToHost));
+          int64_t n = 0, r0 = -1, r1 = -1;
+          for (int64_t i = 0; i < rows; ++i)
+            if (memcmp(&yb[i], &hy[i], 4)) { ++n; if (r0 < 0) r0 = i; r1 = i; }
+          printf("    y: %lld rows differ, rows %lld..%lld (tile %lld, round %lld, waves %lld..%lld)\n", (long long)n,
+                 (long long)r0, (long long)r1, (long long)(r0 / 256), (long long)(r0 / 256 / grid.x),
+                 (long long)(r0 % 256 / 32), (long long)(r1 % 256 / 32));
+          for (int l = 0; l < nh; ++l) {
+            int64_t m = 0, q0 = -1, q1 = -1;
+            unsigned fmask = 0;
+            for (int64_t i = 0; i < rows * F; ++i)
+              if (pb[l * rows * F + i] != hp[l * rows * F + i]) {
+                ++m; if (q0 < 0) q0 = i / F; q1 = i / F; fmask |= 1u << ((i % F) / 32);
+              }
+            if (m) printf("    P%d: %lld codes differ, rows %lld..%lld, blocks mask %02x\n", l + 1, (long long)m,
+                          (long long)q0, (long long)q1, fmask);
+          }
+        }
+        ++bad;
+      }
+    }
+    printf("determinism: %d of %d launches differ from the first\n", bad, K);
+  }
   {  // run-to-run: one more launch, bitwise comparison of y and the codes
     std::vector<float> hy2(rows);
     std::vector<uint16_t> hp2(nh * rows * F);

@@ -40,6 +40,14 @@ def run(prec="bf16", torch_loss=False, steps=(0, 50, 100, 200, 300, 400, 500)):
 
 
 _native.load_library()
+if len(sys.argv) > 1 and sys.argv[1] == "magic":  # the register forward's epilogue forms
+    fine = tuple(sorted(set(tuple(range(0, 801, 50)) + (480, 520, 540, 560, 580))))
+    print("steps           ", list(fine), flush=True)
+    for v in (1, 0):
+        _native.set_option("freg_magic", v)
+        print(f"bf16 freg_magic={v}", run(steps=fine), flush=True)
+    _native.set_option("freg_magic", 1)
+    sys.exit(0)
 print("fp32            ", run("fp32"), flush=True)
 print("bf16 default    ", run(), flush=True)
 print("bf16 torch loss ", run(torch_loss=True), flush=True)
