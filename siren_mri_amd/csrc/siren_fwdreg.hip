@@ -149,9 +149,20 @@ DEV constexpr int freg_in0(int ks, int h) { return 32 * (ks >> 1) + 16 * (ks & 1
 // The 8 two-element parts of a pending epilogue are spread over K steps 0..13 (part p at step
 // 13 p / 7): one part per one or two MFMAs, and both converted halves are ready before K steps
 // 14 and 15, which read them when the pending block is the previous layer's last.
+// SIREN_FREG_SPAN: the last part's K step (parts at SPAN p / 7); SIREN_FREG_WAITAT >= 0: the block's
+// store-completion wait at that K step instead of right after its second store (the two stores'
+// data held until then), so the store's latency overlaps the MFMAs in between.
+#ifndef SIREN_FREG_SPAN
+#define SIREN_FREG_SPAN 9
+#endif
+#ifndef SIREN_FREG_WAITAT
+#define SIREN_FREG_WAITAT 15
+#endif
+static_assert(SIREN_FREG_SPAN >= 7 && SIREN_FREG_SPAN <= 13, "epilogue span");
+static_assert(SIREN_FREG_WAITAT < 0 || (SIREN_FREG_WAITAT > SIREN_FREG_SPAN && SIREN_FREG_WAITAT < 16), "wait step");
 DEV constexpr int freg_part_at(int ks) {
   for (int p = 0; p < 8; ++p)
-    if (13 * p / 7 == ks) return p;
+    if (SIREN_FREG_SPAN * p / 7 == ks) return p;
   return -1;
 }
 
@@ -415,7 +426,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
       prevst = c;
     } else {
       // one wait per block: the half-0 store's data stays reserved (an input of the half-1 wait)
-      if (half == 1) store_complete2(c, held);
+      if (half == 1 && SIREN_FREG_WAITAT < 0) store_complete2(c, held);
     }
 #else
     store_complete(c);
@@ -429,6 +440,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     uint32_t hp[4];
     uint32_t cp[4];
     u32x4_t held;  // SIREN_FREG_STORE_PAIR: the half-0 store's data until the half-1 store's wait
+    u32x4_t last;  // SIREN_FREG_WAITAT: the half-1 store's data until the block's wait
   };
   // Hidden layers (magic_tag true, SIREN_FREG_MAGIC): the accumulator started at bias + 192, so it
   // holds 192 + z with z the phase in revolutions; while |z| < 64 the sum lies in [128, 256), whose
@@ -488,6 +500,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
       if constexpr (codes) {
         p_store(pl, pfb, p == 3 ? 0 : 1, c, ep.held);
         if (p == 3) ep.held = c;
+        else ep.last = c;
       }
     }
   };
@@ -568,6 +581,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
           if constexpr (fb == 0) epi_part(ep, accP, part, Hin[14], Hin[15], pend_pl, 7, T_{}, ptag);
           else epi_part(ep, accP, part, Hout[2 * fb - 2], Hout[2 * fb - 1], l + 1, fb - 1, T_{}, ptag);
         }
+        if constexpr (ks == SIREN_FREG_WAITAT && !(dbg & 1)) store_complete2(ep.last, ep.held);
         if constexpr (ks == NKS - 2) {  // the pending epilogue is done: the next block's bias
           if constexpr (fb + 1 < NB) accNx = bias_acc(l + 1, fb + 1);
           else if constexpr (!last) accNx = bias_acc(l + 2, 0);
@@ -606,6 +620,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
       accO = __builtin_amdgcn_mfma_f32_32x32x16_f16(wq[ks & 3], Hin[ks], accO, 0, 0, 0);
       constexpr int part = freg_part_at(ks);
       if constexpr (part >= 0) epi_part(ep, accP, part, Hin[14], Hin[15], pend_pl, 7, T_{}, mtag);
+      if constexpr (ks == SIREN_FREG_WAITAT) store_complete2(ep.last, ep.held);
     });
     // y[row][o], o = 4 h + e (rows 0..7 of the output accumulator are lanes' elements 0..3)
     const int64_t r0 = tcur * FREG_WG_ROWS;
@@ -696,6 +711,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
           if constexpr (!(dbg & 8))
 #pragma unroll
             for (int p = 0; p < 8; ++p) epi_part(ep, acc, p, Ha[2 * fb], Ha[2 * fb + 1], 0, fb, codes_tag, F_{});
+          if constexpr (SIREN_FREG_WAITAT >= 0 && decltype(codes_tag)::value) store_complete2(ep.last, ep.held);
           acc = accn;
         } else {
           accP = acc;

@@ -481,6 +481,54 @@ __global__ __launch_bounds__(256) void first_bwd_kernel(FirstBwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// first_bwd_wide: dW_0 = dZ_0^T x and db_0 = sum dZ_0 for the wide first layer (5..16 inputs:
+// configs 4/5's Fourier features) when no input gradient is asked for. One thread per hidden
+// feature f (F <= 256), accumulating its C + 1 sums in registers over the split's rows: a row is one
+// coalesced 2-byte dZ read per lane plus the row's x (<= 64 B, the same address in every lane),
+// eight rows in flight. first_bwd_kernel's lanes-per-row mapping kept 64 lanes on one row and one
+// row in flight, ~1.4 ms per C4 step. Each (split, f) sum runs in a fixed row order (deterministic).
+constexpr int FBW_ROWS = 8;
+template <int PREC, int CC>  // CC: the input count when known at compile time (16), else 0
+__global__ __launch_bounds__(256) void first_bwd_wide_kernel(FirstBwdArgs a) {
+  using grad_t = typename Prec<PREC>::grad_t;
+  constexpr int MAXC = 16;
+  const int f = threadIdx.x;
+  const int split = blockIdx.x;
+  const int64_t batch = blockIdx.y;
+  const int64_t r_begin = (int64_t)split * a.rows_per_split;
+  const int64_t r_end = r_begin + a.rows_per_split < a.rows_per_batch ? r_begin + a.rows_per_split : a.rows_per_batch;
+  const int C = CC ? CC : a.C;
+  const bool live = f < a.F;
+  float dw[MAXC], db = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) dw[c] = 0.f;
+  const grad_t* dz = (const grad_t*)a.dZ + batch * a.rows_per_batch * a.F + (live ? f : 0);
+  const float* xb = a.x + batch * a.rows_per_batch * C;
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += FBW_ROWS) {
+    float z[FBW_ROWS], xv[FBW_ROWS][MAXC];
+#pragma unroll
+    for (int k = 0; k < FBW_ROWS; ++k) {
+      const int64_t r = r0 + k < r_end ? r0 + k : r_end - 1;
+      z[k] = r0 + k < r_end ? to_f32(dz[r * a.F]) : 0.f;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) xv[k][c] = c < C ? xb[r * C + c] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < FBW_ROWS; ++k) {
+      db += z[k];
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) dw[c] = fmaf(z[k], xv[k][c], dw[c]);
+    }
+  }
+  if (!live) return;
+  float* part = a.part + (int64_t)split * a.split_stride + batch * (int64_t)(a.F * C + a.F);
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c)
+    if (c < C) part[f * C + c] = dw[c];
+  part[a.F * C + f] = db;
+}
+
+// ------------------------------------------------------------------------------------------
 // reduce: out[e] = sum_s part[s * split_stride + e] for e < total (= nb * slab). Element e of
 // batch slab b goes to out0[b*n_first + r] (r < n_first) or out1[b*(slab-n_first) + r-n_first].
 // Block = 32 float4 columns x 8 split lanes; split_stride % 4 == 0.

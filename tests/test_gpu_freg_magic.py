@@ -46,7 +46,7 @@ def _run(x, params, magic):
         torch.cuda.synchronize()
         return y.detach().cpu(), [(w.grad.cpu(), b.grad.cpu()) for w, b in zip(ws, bs)]
     finally:
-        _native.set_option("freg_magic", 1)
+        _native.set_option("freg_magic", 0)
 
 
 def _oracle(x, params):

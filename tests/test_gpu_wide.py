@@ -82,6 +82,12 @@ def test_wide_inputs_shared_ragged(C):
     _check([C, 256, 256, 256, 1], None, 70000 + C, seed=C, need_dx=True)
 
 
+def test_wide_weight_gradient_kernel_generic_inputs():
+    # first_bwd_wide_kernel's runtime-C form (C != 16, no input gradient), ragged rows, per-set weights
+    _check([12, 256, 256, 256, 1], None, 70001, seed=5)
+    _check([7, 256, 256, 256, 2], 3, 5003, seed=6)
+
+
 def test_wide_one_hidden_layer_and_six():
     _check([16, 256, 256, 2], None, 3001, seed=1)
     _check([9, 256, 256, 256, 256, 256, 256, 256, 1], None, 1000, seed=2)

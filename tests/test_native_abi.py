@@ -96,7 +96,7 @@ def test_config_options():
     lib = _native.load_library()
     assert lib.siren_config_get(b"fused_forward") in (0, 1)
     assert lib.siren_config_get(b"nope") == -1
-    assert lib.siren_config_get(b"freg_magic") == 1
+    assert lib.siren_config_get(b"freg_magic") == 0
     assert lib.siren_config_set(b"nope", 1) != 0
     assert "unknown option" in _native.last_error()
 

@@ -28,7 +28,7 @@ def main():
     args = bench.parse()
     _native.load_library()
     dev = torch.device("cuda", 0)
-    step, _ = bench.build_step(args, dev, 0, 1)
+    step = bench.build(args.config, args, dev, 0, 1).step
     vals = [int(v) for v in cli.values.split(",")]
     default = _native.get_option(cli.name)
     for _ in range(10):
