@@ -75,7 +75,7 @@ KCLASS_NAMES = {
 # kernel symbol of each class at the M shape (C = 2 inputs, O = 1 output), as rocprofv3 names it
 KCLASS_SYMBOL = {
     "bf16": {1: "siren::nt_bf16_kernel<0, 256, false, false>", 2: "siren::nt_bf16_kernel<1, 256, false, false>",
-             3: "siren::tn_dw_kernel<1, false, false>", 4: "siren::fused_fwd_reg_kernel<2, 1>",
+             3: "siren::tn_dw_kernel<1, false, false>", 4: "siren::fused_fwd_reg_kernel<2, 1, 0>",
              5: "siren::bwd_ring_bf16_kernel", 6: "siren::dx_ring_bf16_kernel<0, false, false, 0>",
              7: "siren::dw_ring_bf16_kernel<0, 0>", 8: "siren::dx_ring_bf16_kernel<2, true, true, 0>",
              9: "siren::dw_ring_bf16_kernel<2, 0>", 10: "siren::dx_ring_bf16_kernel<0, false, false, 1>",

@@ -526,7 +526,7 @@ int fused_forward_reg(const siren_mlp_desc* d, const Geo& g, const Layout& lo, c
     p.WL = d->weight[g.L - 1];
     p.out = wreg;
     p.outL = wlreg;
-    p.wbound = wbound;
+    p.wbound = g_freg_magic ? wbound : nullptr;  // (the magic form's check only)
     p.nb = g.nb;
     p.nh = nh;
     p.O = d->dims[g.L];
