@@ -114,21 +114,41 @@ __global__ __launch_bounds__(256) void jvp_nt_kernel(JNTArgs a) {
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   // A chunk: 128 rows x 32 k = 1024 units of 4 -> 4 per thread. B chunk: 256 x 32 -> 8 units/thread.
+  // The chunk's raw operands (phases, tangents / adjoints, weights) are fetched into registers
+  // before the previous chunk's MFMAs and turned into operands (sin / cos / products) only when
+  // staged, after those MFMAs: the loads' latency overlaps the MFMAs instead of stalling the wave
+  // in front of them. A unit's stacked row (stream s, row n) is the same in every chunk.
   float areg[4][4];
   float breg[8][4];
+  phase_t praw[4][4];
+  float uraw[4][4];
+  int sq[4];
+  int64_t nq[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t row = m0 + ((tid + 256 * q) >> 3);
+    sq[q] = row < rows ? (int)(row / a.N) : -1;
+    nq[q] = row < rows ? row - (int64_t)sq[q] * a.N : 0;
+  }
+  const int64_t plane = a.N * (int64_t)K;
   auto load = [&](int k0) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int u = tid + 256 * q;
-      const int r = u >> 3, k = k0 + (u & 7) * 4;
-      const int64_t row = m0 + r;
-      if (row < rows) {
-        const int s = (int)(row / a.N);
-        const int64_t n = row - (int64_t)s * a.N;
+      const int k = k0 + (u & 7) * 4;
+      const int s = sq[q];
+      const int64_t n = nq[q];
+      if (s >= 0) {
         if constexpr (MODE == JMODE_FWD) {
-          jvp_operand4<PREC>(a, b, s, n, k, areg[q]);
+          const phase_t* P = (const phase_t*)a.P + (b * a.N + n) * K + k;
+          const float* Ub = a.U + b * (int64_t)(a.S - 1) * plane + n * K + k;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            praw[q][e] = P[e];
+            uraw[q][e] = (s >= 1 && s <= a.C) ? Ub[(int64_t)(s - 1) * plane + e] : 0.f;
+          }
         } else {
-          const grad_t* D = (const grad_t*)a.D + (b * rows + row) * K + k;
+          const grad_t* D = (const grad_t*)a.D + (b * rows + m0 + (u >> 3)) * K + k;
 #pragma unroll
           for (int e = 0; e < 4; ++e) areg[q][e] = to_f32(D[e]);
         }
@@ -146,7 +166,21 @@ __global__ __launch_bounds__(256) void jvp_nt_kernel(JNTArgs a) {
       for (int e = 0; e < 4; ++e) breg[q][e] = col < a.Nout ? to_f32(W[(int64_t)col * K + k + e]) : 0.f;
     }
   };
-  auto store = [&]() {
+  auto store = [&](int k0) {
+    if constexpr (MODE == JMODE_FWD) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int s = sq[q];
+        if (s < 0) continue;
+        if (s <= a.C) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            areg[q][e] = s == 0 ? PT::sinp(praw[q][e]) : a.w0 * PT::cosp(praw[q][e]) * uraw[q][e];
+        } else {  // the Laplacian stream (C + 1 tangent planes): from memory
+          jvp_operand4<PREC>(a, b, s, nq[q], k0 + ((tid + 256 * q) & 7) * 4, areg[q]);
+        }
+      }
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int u = tid + 256 * q;
@@ -168,7 +202,7 @@ __global__ __launch_bounds__(256) void jvp_nt_kernel(JNTArgs a) {
   load(0);
   for (int kc = 0; kc < nk; ++kc) {
     __syncthreads();
-    store();
+    store(kc * JNT_KC);
     __syncthreads();
     if (kc + 1 < nk) load((kc + 1) * JNT_KC);
     if constexpr (BF) {
@@ -280,38 +314,76 @@ __global__ __launch_bounds__(256) void jvp_tn_kernel(JTNArgs a) {
 #pragma unroll
   for (int e = 0; e < 16; ++e) dbacc[e] = 0.f;
 
+  // Thread units: column c = tid & 127 of rows (tid >> 7) + 2 q, q < 16, of each 32-row chunk. The
+  // chunk's raw values (D, the phase, the tangent) are fetched into registers before the previous
+  // chunk's MFMAs and turned into X only when staged after them; a row's (stream, row) pair comes
+  // from one division per chunk (rows of a chunk are consecutive).
+  const int cu = tid & 127, ru = tid >> 7;
+  float draw[16], uraw[16];
+  phase_t praw[16];
+  auto row_sn = [&](int64_t rc, int r, int& s, int64_t& n) {
+    const int64_t s0 = rc / a.N;  // (wave-uniform: one scalar division per call site and chunk)
+    s = (int)s0;
+    n = rc - s0 * a.N + r;
+    while (n >= a.N) {
+      n -= a.N;
+      ++s;
+    }
+  };
+  auto fetch = [&](int64_t rc) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int r = ru + 2 * q;
+      const int64_t row = rc + r;
+      draw[q] = 0.f;
+      uraw[q] = 0.f;
+      praw[q] = phase_t(0);
+      if (row < r_end) {
+        int s;
+        int64_t n;
+        row_sn(rc, r, s, n);
+        if (i0 + cu < a.M) draw[q] = to_f32(((const grad_t*)a.D)[(b * rows + row) * a.M + i0 + cu]);
+        if (j0 + cu < a.Kin) {
+          praw[q] = ((const phase_t*)a.P)[(b * a.N + n) * a.Kin + j0 + cu];
+          if (s >= 1 && s <= a.C) uraw[q] = a.U[b * a.Su * plane + (int64_t)(s - 1) * plane + n * a.Kin + j0 + cu];
+        }
+      }
+    }
+  };
+  fetch(r_begin);
   for (int64_t rc = r_begin; rc < r_end; rc += KC) {
     __syncthreads();
     // stage 32 rows x 128 columns of D and X (16 elements per thread each)
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const int u = tid + 256 * q;
-      const int r = u >> 7, c = u & 127;
+      const int r = ru + 2 * q;
       const int64_t row = rc + r;
       float dv = 0.f, xv = 0.f;
       if (row < r_end) {
-        const int s = (int)(row / a.N);
-        const int64_t n = row - (int64_t)s * a.N;
-        if (i0 + c < a.M) dv = to_f32(((const grad_t*)a.D)[(b * rows + row) * a.M + i0 + c]);
-        if (j0 + c < a.Kin) {
-          const phase_t p = ((const phase_t*)a.P)[(b * a.N + n) * a.Kin + j0 + c];
-          const float* Ue = a.U + b * a.Su * plane + n * a.Kin + j0 + c;
+        int s;
+        int64_t n;
+        row_sn(rc, r, s, n);
+        dv = draw[q];
+        if (j0 + cu < a.Kin) {
+          const phase_t p = praw[q];
           if (s == 0) {
             xv = PT::sinp(p);
           } else if (s <= a.C) {
-            xv = a.w0 * PT::cosp(p) * Ue[(s - 1) * plane];
-          } else {  // Laplacian stream: S = w0 c V - w0^2 s Q
-            float q = 0.f;
-            for (int j = 0; j < a.C; ++j) q = fmaf(Ue[j * plane], Ue[j * plane], q);
-            xv = a.w0 * PT::cosp(p) * Ue[a.C * plane] - a.w0 * a.w0 * PT::sinp(p) * q;
+            xv = a.w0 * PT::cosp(p) * uraw[q];
+          } else {  // Laplacian stream: S = w0 c V - w0^2 s Q (its C + 1 tangent planes from memory)
+            const float* Ue = a.U + b * a.Su * plane + n * a.Kin + j0 + cu;
+            float qq = 0.f;
+            for (int j = 0; j < a.C; ++j) qq = fmaf(Ue[j * plane], Ue[j * plane], qq);
+            xv = a.w0 * PT::cosp(p) * Ue[a.C * plane] - a.w0 * a.w0 * PT::sinp(p) * qq;
           }
         }
         if (s == 0) dbacc[q] += dv;
       }
-      Ds[r][c] = to_f32(from_f32<op_t>(dv));
-      Xs[r][c] = to_f32(from_f32<op_t>(xv));
+      Ds[r][cu] = to_f32(from_f32<op_t>(dv));
+      Xs[r][cu] = to_f32(from_f32<op_t>(xv));
     }
     __syncthreads();
+    if (rc + KC < r_end) fetch(rc + KC);
     const int r32 = lane & 31, h = lane >> 5;
     if constexpr (PREC == kPrecBF16) {
 #pragma unroll
