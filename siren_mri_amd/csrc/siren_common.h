@@ -42,6 +42,47 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 //  op_t   : MFMA operand element.
 template <int PREC> struct Prec;
 
+// fp32 sin / cos for the fp32 (reference-arithmetic) mode: 3-part Cody-Waite reduction by pi/2
+// (FMA form, exact for |x| < ~1e5) and minimax polynomials on [-pi/4, pi/4], ~1-2 ulp. OCML's
+// sinf/cosf inline a Payne-Hanek reduction at every call site: the tangent-stream GEMMs grew to
+// 33 K instructions (1,300 64-bit multiplies, 400 alignbits, 700 branches) and ran 3x the time of
+// the same GEMM without the operand math. Arguments past the Cody-Waite range take OCML's
+// functions through a call (never on the SIREN path: |w0 z| stays far below 1e5 radians).
+__attribute__((noinline)) __device__ float sin_f32_far(float x) { return sinf(x); }
+__attribute__((noinline)) __device__ float cos_f32_far(float x) { return cosf(x); }
+DEV void sincos_poly(float x, float& sn, float& cs, int& q) {
+  const float k = __builtin_rintf(x * 0.636619772367581343f);  // round(x / (pi / 2))
+  float r = fmaf(k, -1.57079637050628662109375f, x);
+  r = fmaf(k, 4.371138828673793e-8f, r);
+  r = fmaf(k, 1.7151245100058819e-15f, r);
+  q = (int)k;
+  const float t = r * r;
+  float ps = fmaf(2.86567956e-6f, t, -1.98559923e-4f);
+  ps = fmaf(ps, t, 8.33338592e-3f);
+  ps = fmaf(ps, t, -1.66666672e-1f);
+  sn = fmaf(ps * t, r, r);
+  float pc = fmaf(2.44677067e-5f, t, -1.38877297e-3f);
+  pc = fmaf(pc, t, 4.16666567e-2f);
+  pc = fmaf(pc, t, -5.0e-1f);
+  cs = fmaf(pc, t, 1.0f);
+}
+DEV float sin_f32(float x) {
+  if (__builtin_expect(!(__builtin_fabsf(x) < 1.0e5f), 0)) return sin_f32_far(x);
+  float sn, cs;
+  int q;
+  sincos_poly(x, sn, cs, q);
+  const float v = (q & 1) ? cs : sn;
+  return (q & 2) ? -v : v;
+}
+DEV float cos_f32(float x) {
+  if (__builtin_expect(!(__builtin_fabsf(x) < 1.0e5f), 0)) return cos_f32_far(x);
+  float sn, cs;
+  int q;
+  sincos_poly(x, sn, cs, q);
+  const float v = (q & 1) ? sn : cs;
+  return ((q + 1) & 2) ? -v : v;
+}
+
 template <> struct Prec<kPrecF32> {
   using phase_t = float;
   using grad_t = float;
@@ -49,11 +90,11 @@ template <> struct Prec<kPrecF32> {
   static DEV phase_t enc(float p) { return p; }
   // phase of w0 * (z + b): the reference's sin(w0 * (xW^T + b)) argument (modules.py:26,38)
   static DEV phase_t encz(float z, float b, float w0) { return w0 * (z + b); }
-  static DEV float sinp(phase_t v) { return sinf(v); }
-  static DEV float cosp(phase_t v) { return cosf(v); }
+  static DEV float sinp(phase_t v) { return sin_f32(v); }
+  static DEV float cosp(phase_t v) { return cos_f32(v); }
   // sin / cos of an fp32 radian argument (the sine output layer, outermost_linear=False)
-  static DEV float sinr(float x) { return sinf(x); }
-  static DEV float cosr(float x) { return cosf(x); }
+  static DEV float sinr(float x) { return sin_f32(x); }
+  static DEV float cosr(float x) { return cos_f32(x); }
 };
 
 template <> struct Prec<kPrecBF16> {

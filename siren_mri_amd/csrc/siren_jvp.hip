@@ -241,6 +241,9 @@ __global__ __launch_bounds__(256) void jvp_nt_kernel(JNTArgs a) {
   }
 
   const float* bias = a.bias ? a.bias + b * a.b_bstride : nullptr;
+  // stacked row -> (stream, row) from one division for the block's first row (the epilogue's 128
+  // rows per thread each paid a 64-bit division: a third of the kernel's instructions)
+  const int64_t s_m0 = m0 / a.N, n_m0 = m0 - s_m0 * a.N;
 #pragma unroll
   for (int bn = 0; bn < 4; ++bn) {
     const int col = n0 + 128 * wn + 32 * bn + (lane & 31);
@@ -249,12 +252,17 @@ __global__ __launch_bounds__(256) void jvp_nt_kernel(JNTArgs a) {
     for (int bm = 0; bm < 2; ++bm)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int64_t row = m0 + 64 * wm + 32 * bm + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        const int off = 64 * wm + 32 * bm + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        const int64_t row = m0 + off;
         if (row >= rows) continue;
         const float v = acc[bm][bn][e];
         if constexpr (MODE == JMODE_FWD) {
-          const int s = (int)(row / a.N);
-          const int64_t n = row - (int64_t)s * a.N;
+          int s = (int)s_m0;
+          int64_t n = n_m0 + off;
+          while (n >= a.N) {
+            n -= a.N;
+            ++s;
+          }
           if (s == 0)
             ((phase_t*)a.Pout)[(b * a.N + n) * a.Nout + col] = PT::encz(v, bias[col], a.w0);
           else
