@@ -90,11 +90,13 @@ template <> struct Prec<kPrecF32> {
   static DEV phase_t enc(float p) { return p; }
   // phase of w0 * (z + b): the reference's sin(w0 * (xW^T + b)) argument (modules.py:26,38)
   static DEV phase_t encz(float z, float b, float w0) { return w0 * (z + b); }
-  static DEV float sinp(phase_t v) { return sin_f32(v); }
-  static DEV float cosp(phase_t v) { return cos_f32(v); }
+  // (OCML sinf / cosf; sin_f32 / cos_f32 above are measured-accurate on the CPU emulation but not
+  // yet run on the GPU, so the fp32 mode keeps the library functions until they are)
+  static DEV float sinp(phase_t v) { return sinf(v); }
+  static DEV float cosp(phase_t v) { return cosf(v); }
   // sin / cos of an fp32 radian argument (the sine output layer, outermost_linear=False)
-  static DEV float sinr(float x) { return sin_f32(x); }
-  static DEV float cosr(float x) { return cos_f32(x); }
+  static DEV float sinr(float x) { return sinf(x); }
+  static DEV float cosr(float x) { return cosf(x); }
 };
 
 template <> struct Prec<kPrecBF16> {
