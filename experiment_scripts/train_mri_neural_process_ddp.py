@@ -83,7 +83,9 @@ if opt.checkpoint_path is not None:
     B = torch.load(b_path, map_location="cpu", weights_only=True).contiguous()
 else:
     if opt.seed is not None:
+        # the transform drew its B at construction; redraw it from the seeded generator
         torch.manual_seed(opt.seed)
+        fourier_transformer.set_B(torch.randn((2, nff)) * cfg["fourier_features_scale"])
     B = fourier_transformer.get_B().contiguous()
 model.to(device)
 B = B.to(device)

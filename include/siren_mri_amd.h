@@ -104,7 +104,15 @@ int siren_mlp_backward(const siren_mlp_desc* d, const float* x, const float* dy,
  * (diff_operators.py:27-36: lap[n] = sum_c sum_k d2y_c/dx_k2). Needs outermost_linear and
  * in_features <= 4. `saved` (may be NULL for order 2 / inference) keeps the per-layer phases and
  * tangents for siren_jvp_backward.
+ * `order` selects the derivative (the same tangent streams): SIREN_JVP_GRADIENT writes
+ * grad [rows, in_features]; SIREN_JVP_LAPLACE writes lap [rows] (grad is scratch of the gradient's
+ * size); SIREN_JVP_JACOBIAN writes the per-channel Jacobian grad [rows, out_features, in_features]
+ * (diff_operators.jacobian, diff_operators.py:46-59; and gradient() with grad_outputs that vary
+ * across output channels, or any autograd double backward through the SIREN forward).
  */
+#define SIREN_JVP_GRADIENT 1
+#define SIREN_JVP_LAPLACE 2
+#define SIREN_JVP_JACOBIAN 3
 int64_t siren_jvp_saved_bytes(const siren_mlp_desc* d, int order);
 int64_t siren_jvp_workspace_bytes(const siren_mlp_desc* d, int order);
 int siren_jvp_forward(const siren_mlp_desc* d, int order, const float* x, float* grad, float* lap,
@@ -112,8 +120,9 @@ int siren_jvp_forward(const siren_mlp_desc* d, int order, const float* x, float*
                       void* stream);
 
 /*
- * Backward of a loss on the gradient (order 1) or on the Laplacian (order 2): from
- * dgrad = dL/dgrad [rows, in_features] (order 1) or dL/dlap [rows] (order 2) writes
+ * Backward of a loss on the gradient (order 1), the Laplacian (order 2) or the Jacobian (order 3):
+ * from dgrad = dL/dgrad [rows, in_features] (order 1), dL/dlap [rows] (order 2) or
+ * dL/djac [rows, out_features, in_features] (order 3) writes
  * dweight/dbias (overwrite; the output bias gets zeros: it does not reach either derivative)
  * and, if dx != NULL, dx. These are the double / triple backward passes that
  * loss_functions.gradients_mse (loss_functions.py:330-335) and laplace_mse (:350-355) run
@@ -228,6 +237,14 @@ int siren_kspace_sse_backward(const float* d, const float* mask, const float* hf
  * one launch. Feeds the SIREN's wide first layer (5..16 inputs on the register-resident forward).
  */
 int siren_fourier_features(const float* x, const float* B, int64_t rows, int cin, int m, float* out, void* stream);
+
+/*
+ * sin / cos of n fp32 radian arguments as the fp32 (SIREN_PREC_F32) kernels evaluate them
+ * (impl 0: Cody-Waite reduction + minimax polynomials, siren_common.h sin_f32 / cos_f32) or through
+ * OCML's sinf / cosf (impl 1). No reference counterpart: the accuracy probe behind the fp32 mode's
+ * torch.sin / torch.cos replacement (modules.py:35-38), used by tests/test_gpu_sincos.py.
+ */
+int siren_sincos_f32(const float* x, float* s, float* c, int64_t n, int impl, void* stream);
 
 /*
  * Process-wide execution options (no reference counterpart; used by tests and benchmarks to

@@ -49,6 +49,7 @@ EXPORTED_SYMBOLS = (
     "siren_kspace_sse_forward",
     "siren_kspace_sse_backward",
     "siren_fourier_features",
+    "siren_sincos_f32",
     "siren_last_error",
     "siren_version",
 )
@@ -178,6 +179,8 @@ def _declare(lib):
     lib.siren_kspace_sse_backward.restype = ci
     lib.siren_fourier_features.argtypes = [vp, vp, i64, ci, ci, vp, vp]
     lib.siren_fourier_features.restype = ci
+    lib.siren_sincos_f32.argtypes = [vp, vp, vp, i64, ci, vp]
+    lib.siren_sincos_f32.restype = ci
     lib.siren_last_error.argtypes = []
     lib.siren_last_error.restype = ctypes.c_char_p
     lib.siren_version.argtypes = []

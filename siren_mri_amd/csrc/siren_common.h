@@ -41,6 +41,9 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 //  grad_t : storage of dL/dz between backward kernels.
 //  op_t   : MFMA operand element.
 template <int PREC> struct Prec;
+#ifndef SIREN_F32_OCML
+#define SIREN_F32_OCML 0
+#endif
 
 // fp32 sin / cos for the fp32 (reference-arithmetic) mode: 3-part Cody-Waite reduction by pi/2
 // (FMA form, exact for |x| < ~1e5) and minimax polynomials on [-pi/4, pi/4], ~1-2 ulp. OCML's
@@ -90,13 +93,19 @@ template <> struct Prec<kPrecF32> {
   static DEV phase_t enc(float p) { return p; }
   // phase of w0 * (z + b): the reference's sin(w0 * (xW^T + b)) argument (modules.py:26,38)
   static DEV phase_t encz(float z, float b, float w0) { return w0 * (z + b); }
-  // (OCML sinf / cosf; sin_f32 / cos_f32 above are measured-accurate on the CPU emulation but not
-  // yet run on the GPU, so the fp32 mode keeps the library functions until they are)
+  // sin_f32 / cos_f32 above (SIREN_F32_OCML=1 builds the OCML sinf / cosf instead, for A/B);
+  // pinned against fp64 over |x| <= 2000 rad and past the Cody-Waite range by
+  // tests/test_gpu_sincos.py through siren_sincos_f32
+#if SIREN_F32_OCML
   static DEV float sinp(phase_t v) { return sinf(v); }
   static DEV float cosp(phase_t v) { return cosf(v); }
+#else
+  static DEV float sinp(phase_t v) { return sin_f32(v); }
+  static DEV float cosp(phase_t v) { return cos_f32(v); }
+#endif
   // sin / cos of an fp32 radian argument (the sine output layer, outermost_linear=False)
-  static DEV float sinr(float x) { return sinf(x); }
-  static DEV float cosr(float x) { return cosf(x); }
+  static DEV float sinr(float x) { return sinp(x); }
+  static DEV float cosr(float x) { return cosp(x); }
 };
 
 template <> struct Prec<kPrecBF16> {

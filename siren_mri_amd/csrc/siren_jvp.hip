@@ -487,15 +487,16 @@ __global__ __launch_bounds__(256) void jvp_first_kernel(JFirstArgs a) {
 }
 
 // Output layer: grad[n][k] = sum_o sum_f W[o][f] t^k[f]; lap[n] = sum_o sum_f W[o][f] S[f].
+// jac = 1 (the per-channel Jacobian, SIREN_JVP_JACOBIAN): grad[n][o][k] = sum_f W[o][f] t^k[f].
 // One half-wave per row.
 struct JLastArgs {
   const void* P;      // [B][N][F]
   const float* U;     // [B][Su][N][F]
   const float* W;     // [nb_w][O][F]
-  float* grad;        // [B][N][C]
+  float* grad;        // [B][N][C], or [B][N][O][C] when jac
   float* lap;         // [B][N] or null
   int64_t N;
-  int C, F, O, Su;
+  int C, F, O, Su, jac;
   int64_t w_bstride;
   float w0;
 };
@@ -508,6 +509,31 @@ __global__ __launch_bounds__(256) void jvp_last_kernel(JLastArgs a) {
   const int64_t b = blockIdx.y;
   const float* W = a.W + b * a.w_bstride;
   const int64_t plane = a.N * (int64_t)a.F;
+  if (a.jac) {
+    // per output channel (O <= 8 passes over the row's tangents; not a hot path)
+    for (int64_t n = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5); n < a.N; n += (int64_t)gridDim.x * 8) {
+      for (int o = 0; o < a.O; ++o) {
+        float g[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int f = l32; f < a.F; f += 32) {
+          const float wc = a.w0 * W[o * a.F + f] * PT::cosp(((const phase_t*)a.P)[(b * a.N + n) * a.F + f]);
+          const float* Ub = a.U + b * (int64_t)a.Su * plane + n * a.F + f;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (k < a.C) g[k] = fmaf(wc, Ub[(int64_t)k * plane], g[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (k < a.C) {
+            float v = g[k];
+#pragma unroll
+            for (int off = 16; off >= 1; off >>= 1) v += __shfl_xor(v, off, 32);
+            if (l32 == 0) a.grad[((b * a.N + n) * a.O + o) * a.C + k] = v;
+          }
+        }
+      }
+    }
+    return;
+  }
   for (int64_t n = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5); n < a.N; n += (int64_t)gridDim.x * 8) {
     float g[4] = {0.f, 0.f, 0.f, 0.f};
     float lp = 0.f;
@@ -550,12 +576,14 @@ __global__ __launch_bounds__(256) void jvp_last_kernel(JLastArgs a) {
 // top = 1: the output layer's adjoint, t_bar^k[f] = gbar[n][k] ws[f], S_bar[f] = lbar[n] ws[f]
 //          (ws = sum_o W_L[o][f]), h_bar = 0, and also the output-layer weight-gradient
 //          partials dW_L[o][f] = sum_n (sum_k gbar t^k[f] + lbar S[f]).
+// top = 1 and jac = 1 (per-channel Jacobian adjoint): gbar is [B][N][O][C],
+//          t_bar^k[f] = sum_o gbar[n][o][k] W_L[o][f], dW_L[o][f] = sum_n sum_k gbar[n][o][k] t^k[f].
 // top = 0: raw = [h_bar; t_bar^1..C (; S_bar)] (fp32, [B][S'][N][F]) from the adjoint GEMM.
 struct JCombArgs {
   const void* P;      // [B][N][F] phase_t of this layer
   const float* U;     // [B][Su][N][F] tangents of this layer
   const float* raw;   // top=0
-  const float* gbar;  // top=1: [B][N][C] or null (Laplacian loss)
+  const float* gbar;  // top=1: [B][N][C] ([B][N][O][C] when jac) or null (Laplacian loss)
   const float* lbar;  // top=1: [B][N] (lap = 1)
   const float* WL;    // top=1: [nb_w][O][F]
   void* D;            // [B][S'][N][F] grad_t
@@ -563,10 +591,62 @@ struct JCombArgs {
   int64_t N;
   int64_t rows_per_split;
   int64_t split_stride;
-  int C, F, O, Su, S, top, lap;
+  int C, F, O, Su, S, top, lap, jac;
   int64_t w_bstride;
   float w0;
 };
+
+// The output layer's adjoint for the per-channel Jacobian (top = 1, jac = 1); same outputs as the
+// top branch of jvp_combine_kernel (no Laplacian stream).
+template <int PREC>
+__global__ __launch_bounds__(256) void jvp_combine_jac_kernel(JCombArgs a) {
+  using PT = Prec<PREC>;
+  using phase_t = typename PT::phase_t;
+  using grad_t = typename PT::grad_t;
+  const int64_t b = blockIdx.y;
+  const int S = a.S;
+  const int64_t plane = a.N * (int64_t)a.F;
+  const float* WL = a.WL + b * a.w_bstride;
+  const float w0 = a.w0;
+  grad_t* D = (grad_t*)a.D;
+  const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_split;
+  const int64_t r_end = min(r_begin + a.rows_per_split, a.N);
+  for (int f = threadIdx.x; f < a.F; f += 256) {
+    float wl[FUSED_MAXO], dwl[FUSED_MAXO];
+#pragma unroll
+    for (int o = 0; o < FUSED_MAXO; ++o) {
+      wl[o] = o < a.O ? WL[o * a.F + f] : 0.f;
+      dwl[o] = 0.f;
+    }
+    for (int64_t n = r_begin; n < r_end; ++n) {
+      const phase_t p = ((const phase_t*)a.P)[(b * a.N + n) * a.F + f];
+      const float c = PT::cosp(p), s = PT::sinp(p);
+      const float* Ub = a.U + b * (int64_t)a.Su * plane + n * a.F + f;
+      const float* gb = a.gbar + (b * a.N + n) * (int64_t)a.O * a.C;
+      float cross = 0.f;
+      for (int k = 0; k < a.C; ++k) {
+        const float u = Ub[(int64_t)k * plane];
+        float tbar = 0.f;
+#pragma unroll
+        for (int o = 0; o < FUSED_MAXO; ++o) {
+          if (o < a.O) {
+            const float gk = gb[o * a.C + k];
+            tbar = fmaf(gk, wl[o], tbar);
+            dwl[o] = fmaf(gk, w0 * c * u, dwl[o]);
+          }
+        }
+        cross = fmaf(tbar, u, cross);
+        D[((b * S + 1 + k) * a.N + n) * a.F + f] = from_f32<grad_t>(w0 * c * tbar);
+      }
+      D[(b * S * a.N + n) * a.F + f] = from_f32<grad_t>(w0 * (-w0 * s * cross));
+    }
+    float* part = a.part + (int64_t)blockIdx.x * a.split_stride + b * (int64_t)(a.O * a.F + a.O);
+#pragma unroll
+    for (int o = 0; o < FUSED_MAXO; ++o)
+      if (o < a.O) part[o * a.F + f] = dwl[o];
+    if (f < a.O) part[a.O * a.F + f] = 0.f;
+  }
+}
 
 template <int PREC>
 __global__ __launch_bounds__(256) void jvp_combine_kernel(JCombArgs a) {

@@ -1147,7 +1147,7 @@ JLayout jlayout_of(const siren_mlp_desc* d, int order) {
   memset(&jl, 0, sizeof(jl));
   jl.base = layout_of(d);
   jl.C = d->dims[0];
-  jl.Su = jl.C + (order >= 2 ? 1 : 0);
+  jl.Su = jl.C + (order == SIREN_JVP_LAPLACE ? 1 : 0);
   jl.S = 1 + jl.Su;
   jl.Sb = 1 + jl.Su;  // adjoints [a_bar; u_bar^k (; V_bar)] mirror the forward streams
   int64_t off = jl.base.weights_bytes;
@@ -1190,7 +1190,8 @@ JLayout jlayout_of(const siren_mlp_desc* d, int order) {
 int jvp_check(const siren_mlp_desc* d, int order) {
   int rc = siren_mlp_check(d);
   if (rc) return rc;
-  if (order != 1 && order != 2) return fail(SIREN_EINVAL, "derivative order %d unsupported (1 or 2)", order);
+  if (order != SIREN_JVP_GRADIENT && order != SIREN_JVP_LAPLACE && order != SIREN_JVP_JACOBIAN)
+    return fail(SIREN_EINVAL, "derivative mode %d unsupported (1 gradient, 2 Laplacian, 3 Jacobian)", order);
   if (!d->outermost_linear) return fail(SIREN_EINVAL, "analytic derivatives need outermost_linear");
   if (d->dims[0] > 4) return fail(SIREN_EINVAL, "analytic derivatives support in_features <= 4");
   return SIREN_OK;
@@ -1237,7 +1238,7 @@ int jvp_forward_impl(const siren_mlp_desc* d, int order, const float* x, float* 
     a.N = g.rows;
     a.S = jl.S;
     a.C = jl.C;
-    a.lap = order >= 2;
+    a.lap = order == SIREN_JVP_LAPLACE;
     a.w_bstride = d->weights_batched ? (int64_t)d->dims[l + 1] * d->dims[l] : 0;
     a.b_bstride = d->weights_batched ? d->dims[l + 1] : 0;
     a.K = d->dims[l];
@@ -1254,7 +1255,8 @@ int jvp_forward_impl(const siren_mlp_desc* d, int order, const float* x, float* 
     a.U = (const float*)(store + jl.u_off[l - 1]);
     a.W = d->weight[l];
     a.grad = grad;
-    a.lap = order >= 2 ? lap : nullptr;
+    a.lap = order == SIREN_JVP_LAPLACE ? lap : nullptr;
+    a.jac = order == SIREN_JVP_JACOBIAN;
     a.N = g.rows;
     a.C = jl.C;
     a.F = d->dims[l];
@@ -1274,7 +1276,7 @@ int jvp_backward_impl(const siren_mlp_desc* d, int order, const float* x, const 
                       const char* saved, char* ws, float* const* dW, float* const* db, float* dx, hipStream_t st) {
   const Geo g = geo_of(d);
   const JLayout jl = jlayout_of(d, order);
-  const int lapmode = order >= 2;
+  const int lapmode = order == SIREN_JVP_LAPLACE;
   float* part = (float*)(ws + jl.part_off);
   int rc = SIREN_OK;
   int cur = 0;
@@ -1302,7 +1304,11 @@ int jvp_backward_impl(const siren_mlp_desc* d, int order, const float* x, const 
     a.split_stride = split_stride(g, (int64_t)a.O * a.F + a.O);
     a.w_bstride = d->weights_batched ? (int64_t)d->dims[l + 1] * d->dims[l] : 0;
     a.w0 = d->w0;
-    hipLaunchKernelGGL(jvp_combine_kernel<PREC>, dim3((unsigned)s.nsplit, (unsigned)g.nb), dim3(256), 0, st, a);
+    a.jac = order == SIREN_JVP_JACOBIAN;
+    if (a.jac)
+      hipLaunchKernelGGL(jvp_combine_jac_kernel<PREC>, dim3((unsigned)s.nsplit, (unsigned)g.nb), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL(jvp_combine_kernel<PREC>, dim3((unsigned)s.nsplit, (unsigned)g.nb), dim3(256), 0, st, a);
     if ((rc = check_launch("jvp_combine top"))) return rc;
     if ((rc = launch_reduce(part, s.nsplit, a.split_stride, g.nb, (int64_t)a.O * a.F + a.O,
                             (int64_t)a.O * a.F, dW[l], db[l], st)))
@@ -1513,7 +1519,7 @@ int siren_jvp_forward(const siren_mlp_desc* d, int order, const float* x, float*
   const int64_t need = saved ? jl.ws_bytes : jl.ws_bytes + jl.saved_bytes;
   if (!workspace || workspace_bytes < need)
     return fail(SIREN_ENOSPACE, "workspace %lld < %lld bytes", (long long)workspace_bytes, (long long)need);
-  if (!x || !grad || (order >= 2 && !lap)) return fail(SIREN_EINVAL, "null x/grad/lap");
+  if (!x || !grad || (order == SIREN_JVP_LAPLACE && !lap)) return fail(SIREN_EINVAL, "null x/grad/lap");
   g_err.clear();
   hipStream_t st = (hipStream_t)stream;
   if (d->prec == SIREN_PREC_BF16)
@@ -1696,6 +1702,14 @@ int siren_fourier_features(const float* x, const float* B, int64_t rows, int cin
   const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(4096, cdiv(rows * m, KS_THREADS)));
   hipLaunchKernelGGL(fourier_kernel, dim3(blocks), dim3(KS_THREADS), 0, (hipStream_t)stream, a);
   return check_launch("fourier_features");
+}
+
+int siren_sincos_f32(const float* x, float* s, float* c, int64_t n, int impl, void* stream) {
+  if (n < 0 || (impl != 0 && impl != 1) || (n > 0 && (!x || !s || !c)))
+    return fail(SIREN_EINVAL, "sincos_f32: bad arguments (n=%lld, impl=%d)", (long long)n, impl);
+  if (n == 0) return SIREN_OK;
+  hipLaunchKernelGGL(sincos_probe_kernel, dim3(grid1d(n, 4096)), dim3(256), 0, (hipStream_t)stream, x, s, c, n, impl);
+  return check_launch("sincos_f32");
 }
 
 int siren_adam_step(const siren_adam_desc* d, void* stream) {

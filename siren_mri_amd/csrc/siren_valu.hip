@@ -668,4 +668,20 @@ __global__ __launch_bounds__(256) void prep_weights_kernel(PrepArgs a) {
   }
 }
 
+// sin / cos of fp32 radian arguments through the fp32 mode's functions (impl 0: Prec<F32>::sinp /
+// cosp, i.e. the Cody-Waite + minimax sin_f32 / cos_f32) or OCML's sinf / cosf (impl 1): the
+// accuracy probe behind siren_sincos_f32.
+__global__ __launch_bounds__(256) void sincos_probe_kernel(const float* x, float* s, float* c, int64_t n, int impl) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float v = x[i];
+    if (impl == 0) {
+      s[i] = Prec<kPrecF32>::sinp(v);
+      c[i] = Prec<kPrecF32>::cosp(v);
+    } else {
+      s[i] = sinf(v);
+      c[i] = cosf(v);
+    }
+  }
+}
+
 }  // namespace siren

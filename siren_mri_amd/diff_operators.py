@@ -59,17 +59,21 @@ def set_analytic(enabled: bool) -> None:
 
 def gradient(y, x, grad_outputs=None):
     """sum_c g_c dy_c/dx (g = grad_outputs, ones by default), differentiable. For a SIREN output
-    the analytic path takes any g that is constant across the output channels (every g when there
-    is one output, as in every BASELINE config): the sum is then g times the unweighted one."""
+    the analytic path: g = ones -> the summed tangent streams; one output channel -> g times that;
+    any other g -> the per-channel Jacobian contracted with g (no host synchronisation in any
+    case). Other (y, x) pairs go through autograd, whose SIREN backward is itself differentiable
+    (ops._differentiable_backward)."""
     if _ANALYTIC:
         src = _lookup(y, x)
         if src is not None:
-            from .jvp import siren_gradient
+            from .jvp import siren_gradient, siren_jacobian
             if grad_outputs is None:
                 return siren_gradient(x, *src)
             g = grad_outputs
-            if g.shape == y.shape and (y.shape[-1] == 1 or bool((g == g[..., :1]).all())):
-                return siren_gradient(x, *src) * g[..., :1]
+            if g.shape == y.shape:
+                if y.shape[-1] == 1:
+                    return siren_gradient(x, *src) * g
+                return (siren_jacobian(x, *src) * g.unsqueeze(-1)).sum(-2)
     if grad_outputs is None:
         grad_outputs = torch.ones_like(y)
     return torch.autograd.grad(y, [x], grad_outputs=grad_outputs, create_graph=True)[0]
@@ -92,7 +96,14 @@ def laplace(y, x):
 
 
 def jacobian(y, x):
-    """Per-output-channel jacobian [B, N, C_out, C_in] and a NaN status flag."""
+    """Per-output-channel jacobian [B, N, C_out, C_in] and a NaN status flag (for a SIREN output:
+    the tangent-stream op, one native forward)."""
+    if _ANALYTIC and y.dim() == 3:
+        src = _lookup(y, x)
+        if src is not None:
+            from .jvp import siren_jacobian
+            jac = siren_jacobian(x, *src)
+            return jac, (-1 if torch.any(torch.isnan(jac)) else 0)
     b, n = y.shape[:2]
     jac = torch.zeros(b, n, y.shape[-1], x.shape[-1], device=y.device)
     for i in range(y.shape[-1]):

@@ -7,6 +7,10 @@ siren_gradient(x, fcblock, params) == diff_operators.gradient(y, x) for y = fcbl
 siren_laplace(x, fcblock, params) == diff_operators.laplace(y, x) (diff_operators.py:27-36):
     sum over outputs and input dims of d2y/dx2. Differentiable: its backward adds the Laplacian
     adjoint stream (what laplace_mse's triple backward computes through autograd).
+siren_jacobian(x, fcblock, params) == diff_operators.jacobian(y, x)[0] (diff_operators.py:46-59):
+    dy_c/dx_k per output channel. Differentiable (the same adjoint with a per-channel cotangent);
+    it also carries gradient(y, x, grad_outputs=g) for any g, and the double backward of the
+    SIREN forward through autograd (ops._SineMLPAutograd under create_graph=True).
 
 Custom ops (torch.library.Library "siren_mri_amd", with fake kernels and an Autograd-key
 formula), over the C ABI siren_jvp_forward/backward:
@@ -41,6 +45,8 @@ def _jvp_sizes(geo, prec, order):
     return saved, L.siren_jvp_workspace_bytes(ctypes.byref(d), order)
 
 
+GRADIENT, LAPLACE, JACOBIAN = 1, 2, 3  # SIREN_JVP_* of include/siren_mri_amd.h
+
 _LIB.define("sine_mlp_jvp(Tensor x, Tensor[] weights, Tensor[] biases, float w0, int prec, bool batched, int order, "
             "bool keep) -> (Tensor, Tensor)")
 _LIB.define("sine_mlp_jvp_bwd(Tensor dout, Tensor x, Tensor[] weights, Tensor[] biases, Tensor saved, float w0, "
@@ -49,7 +55,8 @@ _LIB.define("sine_mlp_jvp_bwd(Tensor dout, Tensor x, Tensor[] weights, Tensor[] 
 
 def sine_mlp_jvp(x: Tensor, weights: List[Tensor], biases: List[Tensor], w0: float, prec: int, batched: bool,
                  order: int, keep: bool) -> Tuple[Tensor, Tensor]:
-    """siren_jvp_forward: order 1 -> sum_c dy_c/dx (shape of x); order 2 -> the Laplacian [.., 1]."""
+    """siren_jvp_forward: order 1 -> sum_c dy_c/dx (shape of x); order 2 -> the Laplacian [.., 1];
+    order 3 -> the per-channel Jacobian dy_c/dx_k [.., out, in]."""
     _require_device(x)
     geo = _geo_of(x, weights, batched)
     ws = [w.contiguous() for w in weights]
@@ -60,20 +67,24 @@ def sine_mlp_jvp(x: Tensor, weights: List[Tensor], biases: List[Tensor], w0: flo
     saved_bytes, ws_bytes = _jvp_sizes(geo, prec, order)
     saved = torch.empty(saved_bytes if keep else 0, dtype=torch.uint8, device=dev)
     work = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-    grad = torch.empty(xc.shape, dtype=torch.float32, device=dev)
-    lap = torch.empty(xc.shape[:-1] + (1,), dtype=torch.float32, device=dev) if order == 2 else None
+    gshape = xc.shape[:-1] + (geo.dims[-1], xc.shape[-1]) if order == JACOBIAN else xc.shape
+    grad = torch.empty(gshape, dtype=torch.float32, device=dev)
+    lap = torch.empty(xc.shape[:-1] + (1,), dtype=torch.float32, device=dev) if order == LAPLACE else None
     rc = _native.lib().siren_jvp_forward(ctypes.byref(desc), order, xc.data_ptr(), grad.data_ptr(),
                                          lap.data_ptr() if lap is not None else None,
                                          saved.data_ptr() if keep else None, saved_bytes if keep else 0,
                                          work.data_ptr(), ws_bytes, _native.stream_handle(dev))
     _native.check(rc, "siren_jvp_forward")
-    return (grad if order == 1 else lap), saved
+    return (lap if order == LAPLACE else grad), saved
 
 
 def _sine_mlp_jvp_fake(x, weights, biases, w0, prec, batched, order, keep):
     geo = _geo_of(x, weights, batched)
     saved_bytes, _ = _jvp_sizes(geo, prec, order)
-    out = x.new_empty(x.shape) if order == 1 else x.new_empty(x.shape[:-1] + (1,))
+    if order == JACOBIAN:
+        out = x.new_empty(x.shape[:-1] + (geo.dims[-1], x.shape[-1]))
+    else:
+        out = x.new_empty(x.shape) if order == GRADIENT else x.new_empty(x.shape[:-1] + (1,))
     return out, x.new_empty((saved_bytes if keep else 0,), dtype=torch.uint8)
 
 
@@ -135,12 +146,20 @@ class _SineMLPJVPAutograd(torch.autograd.Function):
         t = ctx.saved_tensors
         x, saved, ws, bs = t[0], t[1], list(t[2:2 + n]), list(t[2 + n:])
         need_dx = ctx.needs_input_grad[1]
-        dx, dW, db = torch.ops.siren_mri_amd.sine_mlp_jvp_bwd(dout, x, ws, bs, saved, w0, prec, batched, order,
-                                                              need_dx)
+        with torch.no_grad():
+            dx, dW, db = torch.ops.siren_mri_amd.sine_mlp_jvp_bwd(dout, x, ws, bs, saved, w0, prec, batched, order,
+                                                                  need_dx)
         db = list(db)
         # the output bias does not reach dy/dx or the Laplacian: autograd leaves its .grad None in the reference
         db[-1] = None
-        return (None, dx if need_dx else None, *dW, *db)
+        outs = [dx if need_dx else None, *dW, *db]
+        if torch.is_grad_enabled():
+            # create_graph=True over a derivative op: one more order is not provided; the gradients
+            # are exact, differentiating them again raises (instead of silently giving zeros)
+            outs = guard_higher_order(outs, [x, *ws, *bs],
+                                      "siren_mri_amd: derivatives of the tangent-stream backward (a third "
+                                      "derivative of the SIREN) are not provided")
+        return (None, *outs)
 
 
 def _sine_mlp_jvp_autograd(x, weights, biases, w0, prec, batched, order, keep):
@@ -169,8 +188,48 @@ def _apply(x, fcblock, params, order):
 
 
 def siren_gradient(x, fcblock, params=None):
-    return _apply(x, fcblock, params, 1)
+    return _apply(x, fcblock, params, GRADIENT)
 
 
 def siren_laplace(x, fcblock, params=None):
-    return _apply(x, fcblock, params, 2)
+    return _apply(x, fcblock, params, LAPLACE)
+
+
+def siren_jacobian(x, fcblock, params=None):
+    """dy_c/dx_k per output channel, [..., out_features, in_features] (diff_operators.jacobian)."""
+    return _apply(x, fcblock, params, JACOBIAN)
+
+
+def jacobian_of(x, weights, biases, w0, prec, batched):
+    """The per-channel Jacobian of the SIREN stack with these (autograd-tracked) tensors, on the
+    tangent-stream op: differentiable w.r.t. the weights, the biases and x."""
+    keep = torch.is_grad_enabled() and (x.requires_grad or any(t.requires_grad for t in list(weights) + list(biases)))
+    out, _ = torch.ops.siren_mri_amd.sine_mlp_jvp(x, list(weights), list(biases), float(w0), prec, batched,
+                                                  JACOBIAN, keep)
+    return out
+
+
+class _HigherOrderGuard(torch.autograd.Function):
+    """Passes tensors through; differentiating them raises `msg`. The anchors (the op's inputs)
+    make the outputs part of the graph whenever those inputs are, so a derivative that is not
+    provided is an error, never a silent zero."""
+
+    @staticmethod
+    def forward(ctx, msg, n, *args):
+        ctx.msg = msg
+        return tuple(t.view_as(t) for t in args[:n])
+
+    @staticmethod
+    def backward(ctx, *grads):
+        raise RuntimeError(ctx.msg)
+
+
+def guard_higher_order(outs, anchors, msg):
+    idx = [i for i, t in enumerate(outs) if t is not None]
+    if not idx or not any(a.requires_grad for a in anchors):
+        return outs
+    res = _HigherOrderGuard.apply(msg, len(idx), *[outs[i] for i in idx], *anchors)
+    outs = list(outs)
+    for i, t in zip(idx, res):
+        outs[i] = t
+    return outs

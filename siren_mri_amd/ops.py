@@ -15,10 +15,10 @@ FakeTensor tracing / torch.compile see shapes without running anything:
         -> (dx, dW[], db[])                   siren_mlp_backward
 `saved` is the uint8 buffer of prepared weights and stored phases the backward reads (never
 writes), so a graph may be back-propagated more than once (retain_graph=True). The autograd
-formula of sine_mlp_fwd (its Autograd dispatch key) is sine_mlp_bwd; a second
-differentiation of that backward (double backward through an autograd graph) is not provided:
-derivatives of a SIREN's output w.r.t. its input go through the analytic tangent-stream ops
-(jvp.py, diff_operators.gradient/laplace).
+formula of sine_mlp_fwd (its Autograd dispatch key) is sine_mlp_bwd; under create_graph=True
+(double backward through an autograd graph) the input gradient is formed instead from the
+per-channel Jacobian of the tangent-stream op (jvp.py), which is itself differentiable, and the
+weight gradients are exact but raise if differentiated again.
 
 No CPU or eager-PyTorch fallback exists: a CPU tensor, a float64 tensor or an unsupported
 shape raises.
@@ -236,9 +236,41 @@ class _SineMLPAutograd(torch.autograd.Function):
         t = ctx.saved_tensors
         x, saved, ws, bs = t[0], t[1], list(t[2:2 + n]), list(t[2 + n:])
         need_dx = ctx.needs_input_grad[1]
+        if torch.is_grad_enabled():
+            return (None, *_differentiable_backward(ctx, dy, x, saved, ws, bs, need_dx))
         dx, dW, db = torch.ops.siren_mri_amd.sine_mlp_bwd(dy, x, ws, bs, saved, w0, prec, outermost_linear,
                                                           batched, need_dx)
         return (None, dx if need_dx else None, *dW, *db)
+
+
+def _differentiable_backward(ctx, dy, x, saved, ws, bs, need_dx):
+    """The SIREN backward under create_graph=True (diff_operators.gradient through autograd,
+    diff_operators.py:39-43, for any y derived from the SIREN output and any grad_outputs): the input
+    gradient as dx_k = sum_c dy_c J[c, k] with J the per-channel Jacobian of the tangent-stream op,
+    which is differentiable w.r.t. dy, the weights, the biases and x (its backward is the native
+    adjoint). The weight gradients are exact but not differentiable again (differentiating them
+    raises)."""
+    from .jvp import guard_higher_order, jacobian_of
+    w0, prec, outermost_linear, batched, n, keep = ctx.meta
+    dx = None
+    if need_dx:
+        if not outermost_linear or x.shape[-1] > 4:
+            raise RuntimeError(
+                "siren_mri_amd: a differentiable SIREN input gradient (create_graph=True) needs "
+                "outermost_linear=True and in_features <= 4 (the tangent-stream kernels)")
+        J = jacobian_of(x, ws, bs, w0, prec, batched)
+        dx = (J * dy.unsqueeze(-1)).sum(-2)
+    need_w = any(ctx.needs_input_grad[2:])
+    dW, db = [None] * n, [None] * n
+    if need_w:
+        with torch.no_grad():
+            _, dW, db = torch.ops.siren_mri_amd.sine_mlp_bwd(dy, x, ws, bs, saved, w0, prec, outermost_linear,
+                                                             batched, False)
+        wb = guard_higher_order([*dW, *db], [dy, x, *ws, *bs],
+                                "siren_mri_amd: second derivatives of the SIREN's weight gradients are not "
+                                "provided (derivatives of its input gradient are)")
+        dW, db = wb[:n], wb[n:]
+    return (dx, *dW, *db)
 
 
 def _sine_mlp_fwd_autograd(x, weights, biases, w0, prec, outermost_linear, batched, keep):

@@ -55,8 +55,12 @@ class GradAllReducer:
       gradients first). After ``begin()``, a post-accumulate-grad hook counts the gradients of each
       bucket as autograd finishes them and launches that bucket's all-reduce (async, RCCL's own
       stream) as soon as it is complete, so the exchange overlaps the rest of the backward;
-      ``__call__`` launches whatever is left (unused parameters' slots are zero-filled, their
-      ``.grad`` stays None), waits, and applies the mean.
+      ``__call__`` launches whatever is left (a locally unused parameter's slot is zero-filled),
+      waits, and applies the mean.
+    * Unused parameters (DDP's find_unused_parameters case): each bucket carries one usage flag
+      per parameter behind its gradients, reduced in the same collective, so a parameter that ANY
+      rank used gets the reduced gradient on every rank (replicas take identical optimizer steps)
+      and one that no rank used keeps ``.grad = None`` everywhere.
     * Accumulation windows with a per-micro-step exchange (clipping, training_ddp.py:96-109):
       ``begin(delta=True)`` (or ``snapshot()``) makes the next exchange carry only what the coming
       backward adds. For 'mean' nothing is needed (the window's earlier part is identical on every
@@ -85,13 +89,15 @@ class GradAllReducer:
         self._flat = []
         self._views = {}
         self._slot = {}
+        self._flags = []
         for i, bucket in enumerate(self.buckets):
             numel = sum(p.numel() for p in bucket)
-            flat = torch.zeros(numel, dtype=bucket[0].dtype, device=bucket[0].device)
+            flat = torch.zeros(numel + len(bucket), dtype=bucket[0].dtype, device=bucket[0].device)
             self._flat.append(flat)
+            self._flags.append(flat[numel:])
             off = 0
             for p in bucket:
-                self._views[p] = flat[off:off + p.numel()].view_as(p)
+                self._views[p] = _slot_view(flat, off, p)
                 self._slot[p] = i
                 off += p.numel()
         self._armed = False
@@ -130,7 +136,13 @@ class GradAllReducer:
         if len(self._seen[i]) == len(self.buckets[i]):
             self._launch(i)
 
-    def _launch(self, i):
+    def _launch(self, i, used=None):
+        """All-reduce bucket i; used[j] says whether this rank produced parameter j's gradient
+        (None: all of them, the hook path)."""
+        if used is None:
+            self._flags[i].fill_(1.0)
+        else:
+            self._flags[i].copy_(torch.tensor(used, dtype=self._flags[i].dtype), non_blocking=True)
         self._work[i] = dist.all_reduce(self._flat[i], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     @torch.no_grad()
@@ -161,38 +173,59 @@ class GradAllReducer:
         if not self._armed:
             self.begin(delta)
         self._armed = False
-        used = {}
+        partial = []
         for i, bucket in enumerate(self.buckets):
             if self._work[i] is None:
+                used = []
                 for p in bucket:
-                    if p not in self._seen[i]:
-                        used[p] = self._bind(p)
-                        if not used[p]:
-                            self._views[p].zero_()
-                self._launch(i)
+                    u = p in self._seen[i] or self._bind(p)
+                    if not u:
+                        self._views[p].zero_()
+                    used.append(1.0 if u else 0.0)
+                if all(used):
+                    self._launch(i)
+                else:
+                    self._launch(i, used)
+                    partial.append(i)
         for i, w in enumerate(self._work):
             w.wait()
             if self.op == "mean":
                 self._flat[i].mul_(1.0 / self.world)
-        for p in self.params:
-            if used.get(p, True) and p.grad is None:
-                p.grad = self._views[p]
+        # a bucket every rank filled completely needs no flag read-back (the common case: no sync)
+        for i in range(len(self.buckets)):
+            if i in partial or any(p.grad is None for p in self.buckets[i]):
+                flags = self._flags[i].tolist()
+                for p, f in zip(self.buckets[i], flags):
+                    if f > 0:
+                        p.grad = self._views[p]
+                    else:
+                        p.grad = None
         self._work = [None] * len(self.buckets)
+
+
+def _slot_view(flat, off, p):
+    """p's gradient slot inside a flat bucket, with p's own strides (a channels-last conv weight
+    keeps channels-last gradients, so its optimizer step stays on the fused path)."""
+    if p.dim() == 4 and not p.is_contiguous() and p.is_contiguous(memory_format=torch.channels_last):
+        return torch.as_strided(flat, p.shape, p.stride(), off)
+    return flat[off:off + p.numel()].view_as(p)
 
 
 def train_ddp(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_checkpoint, model_dir, loss_fn,
               summary_fn, val_dataloader=None, double_precision=False, clip_grad=False, use_lbfgs=False,
               loss_schedules=None, fourier_feat_transformer=None, device=0, ddp_run=False, accumulation_steps=1,
-              grad_op: str = "mean", model_dir_hook=None):
+              grad_op: str = "mean", model_dir_hook=None, overlap: bool = True, bucket_bytes: int = 32 << 20):
     """training_ddp.py:23-152: the train loop with a per-step gradient all-reduce, the sampler's
     epoch set for shuffling, and rank-0-only I/O. `model` may be a plain module (preferred) or a
     torch DDP wrapper (then DDP performs the exchange and no extra all-reduce is issued).
     model_dir_hook(model_dir), if given, runs on rank 0 right after the model directory is prepared
-    (files that must exist before the first step, e.g. the Fourier matrices)."""
+    (files that must exist before the first step, e.g. the Fourier matrices). overlap / bucket_bytes
+    configure GradAllReducer (hook-launched buckets overlapping the backward, or one exchange after it)."""
     is_ddp_wrapper = isinstance(model, torch.nn.parallel.DistributedDataParallel)
     module = model.module if is_ddp_wrapper else model
     rank = dist.get_rank() if dist.is_initialized() else 0
-    reducer = None if is_ddp_wrapper else GradAllReducer(module.parameters(), op=grad_op)
+    reducer = None if is_ddp_wrapper else GradAllReducer(module.parameters(), op=grad_op, overlap=overlap,
+                                                         bucket_bytes=bucket_bytes)
 
     sampler = getattr(train_dataloader, "sampler", None)
 

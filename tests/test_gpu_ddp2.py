@@ -1,0 +1,287 @@
+"""GPU: the data-parallel path (training_ddp.py:23-164, train_mri_neural_process_ddp.py:188-238) with
+TWO ranks over the HIP kernels.
+
+Two processes share cuda:0 and exchange through torch.distributed's gloo backend, which
+all-reduces CUDA tensors: the code under test — shard_rows, GradAllReducer's hook-launched
+buckets and usage flags, train_ddp's accumulation x clipping windows — is the one RCCL runs on an
+8-GPU node, only the transport differs (the 1-GPU box cannot run RCCL with two ranks). The ranks
+are spawned as fresh child processes (multiprocessing 'spawn'), never by exec from a process that
+touched the GPU.
+
+(a) config M strong scaling: one 512^2 grid split into 2 row shards, image_mse's sum / 128^2 per
+    shard, summed gradients (op='sum'), 2 Adam steps; vs the single-process full-grid fit and the
+    fp64 oracle at the metric-parity tolerances (test_gpu_metric_parity.py).
+(b) configs 4/5: the hypernetwork MRI neural process (conv encoder -> HyperNetwork -> batched
+    SIREN -> DC -> image_mse + latent + weight losses), 2 ranks x 2 slices per micro-step,
+    accumulation 2, clip_grad every micro-step, DDP averaging (op='mean'); vs a single-process
+    statement of the same semantics on the same 8 slices, and the hook-overlapped exchange equal
+    bit for bit to the serial one.
+"""
+import os
+import socket
+from functools import partial
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from oracle import siren_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+WORLD = 2
+TOL = {"fp32": (1e-5, 1e-4), "bf16": (2e-3, 2e-2)}
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_ranks(target, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=target, args=(r, WORLD, port, *args, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=240) for _ in range(WORLD))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for p in procs:
+        assert p.exitcode == 0
+    return res
+
+
+def _setup(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(2)
+    torch.backends.cudnn.deterministic = True  # MIOpen: deterministic conv algorithms (bit-equal reruns)
+    torch.cuda.set_device(0)
+    from siren_mri_amd.training_ddp import ddp_setup
+    ddp_setup(rank, world, backend="gloo")
+
+
+# ----------------------------------------------------------------------------------- (a) M strong
+SIDE = 512
+
+
+def _m_model(precision):
+    from siren_mri_amd import modules
+    torch.manual_seed(0)
+    return modules.SingleBVPNet(type="sine", hidden_features=256, num_hidden_layers=3, precision=precision).to(DEV)
+
+
+def _m_data():
+    from siren_mri_amd import dataio
+    grid = dataio.get_mgrid(SIDE)
+    img = torch.from_numpy(dataio.smooth_random_image(SIDE, seed=0)).reshape(-1, 1).float()
+    return grid, img
+
+
+def _m_fit(model, coords, tgt, steps, reducer=None):
+    """The bench's metric step (forward, image_mse's sum / 128^2, backward, exchange, Adam)."""
+    from siren_mri_amd import loss_functions, training
+    opt = training.make_adam(model.parameters(), 1e-4)
+    first, launched = None, []
+    for s in range(steps):
+        if reducer is not None:
+            reducer.begin()
+        loss = loss_functions.weighted_sse(model({"coords": coords})["model_out"], tgt)
+        loss.backward()
+        if reducer is not None:
+            launched.append(sum(w is not None for w in reducer._work))
+            reducer()
+        if s == 0:
+            first = [p.grad.detach().cpu().numpy().copy() for p in model.parameters()]
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    params = [p.detach().cpu().numpy().copy() for p in model.parameters()]
+    return first, params, launched
+
+
+def _strong_worker(rank, world, port, precision, steps, q):
+    _setup(rank, world, port)
+    import torch.distributed as dist
+    from siren_mri_amd.training_ddp import GradAllReducer, shard_rows
+    model = _m_model(precision)
+    if rank == 1:  # a different local init: the constructor's broadcast must replace it
+        with torch.no_grad():
+            for p in model.parameters():
+                p.mul_(1.5)
+    # 64 KB buckets: the 0.8 MB gradient set spans ~13 buckets, launched from the backward hooks
+    reducer = GradAllReducer(model.parameters(), op="sum", bucket_bytes=64 << 10)
+    grid, img = _m_data()
+    lo, hi = shard_rows(grid.shape[0], rank, world)
+    first, params, launched = _m_fit(model, grid[lo:hi][None].to(DEV), img[lo:hi][None].to(DEV), steps, reducer)
+    q.put((rank, (first, params, launched, len(reducer.buckets))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def m_oracle_grads():
+    """fp64 oracle gradients of the first step (image_mse's sum / 128^2 on the full grid)."""
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    model = _m_model("fp32")
+    ps = [(p.detach().cpu().double().requires_grad_(True)) for p in model.parameters()]
+    pairs = list(zip(ps[0::2], ps[1::2]))
+    grid, img = _m_data()
+    y = orc.siren_forward(grid[None].double(), pairs)
+    (((y - img[None].double()) ** 2).sum() / (128 * 128)).backward()
+    return [p.grad.numpy() for p in ps]
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_two_rank_coordinate_sharded_fit(precision, m_oracle_grads):
+    steps = 2
+    res = run_ranks(_strong_worker, precision, steps)
+    grid, img = _m_data()
+    ref_first, ref_params, _ = _m_fit(_m_model(precision), grid[None].to(DEV), img[None].to(DEV), steps)
+    (f0, p0, launched, nbuckets), (f1, p1, _, _) = res[0], res[1]
+    assert nbuckets > 4 and all(k == nbuckets for k in launched), (nbuckets, launched)
+    for a, b in zip(p0, p1):
+        assert np.array_equal(a, b), "ranks diverged"
+    for a, b in zip(f0, f1):
+        assert np.array_equal(a, b), "ranks hold different reduced gradients"
+    _, tg = TOL[precision]
+    errs = {}
+    for i, (g, r, o) in enumerate(zip(f0, ref_first, m_oracle_grads)):
+        errs[f"g{i}/single"] = orc.norm_rel(torch.from_numpy(g), torch.from_numpy(r))
+        errs[f"g{i}/oracle"] = orc.norm_rel(torch.from_numpy(g).double(), torch.from_numpy(o))
+    for i, (a, r) in enumerate(zip(p0, ref_params)):
+        errs[f"p{i}"] = orc.norm_rel(torch.from_numpy(a), torch.from_numpy(r))
+    print(f"\n[2-rank strong {precision}] max grad/single "
+          f"{max(v for k, v in errs.items() if k.endswith('single')):.2e}, grad/oracle "
+          f"{max(v for k, v in errs.items() if k.endswith('oracle')):.2e}, params "
+          f"{max(v for k, v in errs.items() if k.startswith('p')):.2e}")
+    for k, v in errs.items():
+        bound = (1e-5 if precision == "fp32" else 1e-4) if k.startswith("p") else tg
+        if precision == "fp32" and k.endswith("single"):
+            bound = 1e-5  # the same fp32 arithmetic, only the row split and one extra addition differ
+        assert v <= bound, (k, v)
+
+
+# ------------------------------------------------------------------------ (b) hypernetwork, C4/C5
+RES = 64
+NFF = 8
+KL, FW, LR = 2.78e-8, 6.4e-6, 5.57e-5
+
+
+def _hyper_model():
+    from siren_mri_amd import meta_modules
+    torch.manual_seed(0)
+    return meta_modules.ConvolutionalNeuralProcessImplicit2DHypernetFourierFeatures(
+        in_features=2 * NFF, out_features=2, image_resolution=(RES, RES), fourier_features_size=2 * NFF,
+        latent_dim=32, hidden_features=256, hyper_hidden_features=16, hyper_hidden_layers=1, num_hidden_layers=3,
+        conv_kernel_size=3, num_conv_res_blocks=1, w0=30, precision="bf16", encoder_precision="bf16").to(DEV)
+
+
+def _ff():
+    from siren_mri_amd.features import GaussianFourierFeatureTransform
+    torch.manual_seed(1)
+    return GaussianFourierFeatureTransform(2, NFF, scale=21, device=DEV)
+
+
+def _slices():
+    from siren_mri_amd import dataio
+    ds = dataio.SyntheticMRIKspace(n_slices=8, image_resolution=(RES, RES), seed=3)
+    coord = dataio.Implicit2DWrapper(ds, sidelength=(RES, RES), image=False)
+    gen = dataio.ImageGeneralizationWrapper(coord, test_sparsity="CS_cartesian", generalization_mode="conv_cnp")
+    return [gen[i] for i in range(8)]
+
+
+def _rank_batches(rank, items):
+    """DistributedSampler(shuffle=False) order: rank r owns slices r, r+2, r+4, r+6; batches of 2."""
+    own = items[rank::WORLD]
+    out = []
+    for j in range(0, len(own), 2):
+        grp = own[j:j + 2]
+        inp = {k: torch.stack([it[0][k] for it in grp]) for k in grp[0][0]}
+        gt = {k: torch.stack([it[1][k] for it in grp]) for k in grp[0][1]}
+        out.append((inp, gt))
+    return out
+
+
+def _hyper_worker(rank, world, port, overlap, root, q):
+    _setup(rank, world, port)
+    import torch.distributed as dist
+    from siren_mri_amd import loss_functions, training_ddp
+    model = _hyper_model()
+    batches = _rank_batches(rank, _slices())
+    training_ddp.train_ddp(model, batches, epochs=2, lr=LR, steps_til_summary=1000, epochs_til_checkpoint=1000,
+                           model_dir=root, loss_fn=partial(loss_functions.image_hypernetwork_loss, None, KL, FW),
+                           summary_fn=lambda *a, **k: None, clip_grad=True, fourier_feat_transformer=_ff(),
+                           device=DEV, accumulation_steps=2, grad_op="mean", overlap=overlap,
+                           bucket_bytes=4 << 20)
+    q.put((rank, [p.detach().cpu().float().numpy().copy() for p in model.parameters()]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _hyper_reference():
+    """training_ddp.py:96-109 with DDP averaging, in one process: every micro-step's gradient is
+    averaged over the ranks' batches, added to the window's gradient and clipped; Adam at the
+    window's end (the same statement as tests/test_ddp_gloo.py::_accum_reference)."""
+    from siren_mri_amd import loss_functions, training
+    torch.backends.cudnn.deterministic = True
+    model = _hyper_model()
+    ff = _ff()
+    params = [p for p in model.parameters() if p.requires_grad]
+    opt = training.make_adam(model.parameters(), LR)
+    items = _slices()
+    per_rank = [_rank_batches(r, items) for r in range(WORLD)]
+    loss_fn = partial(loss_functions.image_hypernetwork_loss, None, KL, FW)
+    acc = 2
+    for _epoch in range(2):
+        for step in range(len(per_rank[0])):
+            grads = []
+            for r in range(WORLD):
+                inp, gt = per_rank[r][step]
+                inp = {k: v.to(DEV) for k, v in inp.items()}
+                gt = {k: v.to(DEV) for k, v in gt.items()}
+                inp["coords"] = ff(inp["coords"])
+                losses = loss_fn(model(inp), gt)
+                loss = sum(v.mean() for v in losses.values()) / acc
+                grads.append(torch.autograd.grad(loss, params, allow_unused=True))
+            with torch.no_grad():
+                for i, p in enumerate(params):
+                    gs = [g[i] for g in grads if g[i] is not None]
+                    if not gs:
+                        continue
+                    red = sum(gs) / WORLD
+                    p.grad = red.clone() if p.grad is None else p.grad + red
+            torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
+            if (step + 1) % acc == 0:
+                opt.step()
+                opt.zero_grad()
+    return [p.detach().cpu().float().numpy() for p in model.parameters()]
+
+
+def test_two_rank_hypernetwork_accumulation_clip_mean(tmp_path):
+    res_overlap = run_ranks(_hyper_worker, True, str(tmp_path / "overlap"))
+    res_serial = run_ranks(_hyper_worker, False, str(tmp_path / "serial"))
+    for a, b in zip(res_overlap[0], res_overlap[1]):
+        assert np.array_equal(a, b), "ranks diverged"
+    for a, b in zip(res_overlap[0], res_serial[0]):
+        assert np.array_equal(a, b), "hook-overlapped exchange != serial exchange"
+    assert os.path.exists(tmp_path / "overlap" / "checkpoints" / "model_final.pth")
+    ref = _hyper_reference()
+    init = [p.detach().cpu().float().numpy() for p in _hyper_model().parameters()]
+    errs = []
+    for a, r, p0 in zip(res_overlap[0], ref, init):
+        moved = np.linalg.norm(r - p0)
+        if moved == 0:
+            assert np.array_equal(a, r)
+            continue
+        # the update (two Adam steps) of every tensor, relative to the reference's update
+        errs.append(float(np.linalg.norm((a - p0) - (r - p0)) / moved))
+    print(f"\n[2-rank hypernet] max relative update difference {max(errs):.2e} over {len(errs)} tensors")
+    assert max(errs) < 1e-3

@@ -200,3 +200,97 @@ def test_laplace_loss_training_matches_oracle(tmp_path):
     np.testing.assert_allclose(losses, ref_losses, rtol=1e-4)
     for i, (W, b) in enumerate(ref_ps):
         assert orc.norm_rel(m.net.net[i][0].weight.detach().cpu(), W) < 1e-4, f"layer {i} W"
+
+
+# ------------------------------------------------------------------ per-channel Jacobian, double backward
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_jacobian_and_channel_weighted_gradient(precision):
+    """diff_operators.jacobian (diff_operators.py:46-59) and gradient(y, x, grad_outputs=g) with g
+    varying across output channels, on the SIREN_JVP_JACOBIAN tangent-stream op; both
+    differentiable (the parameter gradients of a loss on them vs the oracle's double backward)."""
+    from siren_mri_amd import diff_operators
+    side, out = 20, 3
+    m = _model(64, 2, 13, precision, out=out)
+    coords = orc.get_mgrid(side)[None]
+    g = torch.randn(1, side * side, out, generator=torch.Generator().manual_seed(6))
+    o = m({"coords": coords.to(DEV)})
+    jac, status = diff_operators.jacobian(o["model_out"], o["model_in"])
+    gr = diff_operators.gradient(o["model_out"], o["model_in"], grad_outputs=g.to(DEV))
+    (gr.square().sum() + 0.5 * jac.square().sum()).backward()
+    ps = _oracle_params(m)
+    x = coords.double().clone().requires_grad_(True)
+    y = orc.siren_forward(x, ps)
+    jac_ref = torch.stack([torch.autograd.grad(y[..., c].sum(), x, create_graph=True)[0] for c in range(out)], dim=-2)
+    gr_ref = torch.autograd.grad(y, x, grad_outputs=g.double(), create_graph=True)[0]
+    (gr_ref.square().sum() + 0.5 * jac_ref.square().sum()).backward()
+    tv, tg = TOL[precision]
+    assert status == 0 and jac.shape == (1, side * side, out, 2)
+    assert orc.norm_rel(jac.detach().cpu(), jac_ref.detach()) < tv
+    assert orc.norm_rel(gr.detach().cpu(), gr_ref.detach()) < tv
+    _oracle_check_grads(m, ps, tg)
+
+
+@pytest.mark.parametrize("batched", [False, True])
+def test_autograd_double_backward_through_further_ops(batched):
+    """A derivative of a function OF the SIREN output (here a data-consistency-like mix with a
+    channel-varying mask, data_consistency.py:32-48) w.r.t. the coordinates, through
+    torch.autograd.grad(create_graph=True) — the reference's generic path (diff_operators.py:39-43)
+    — then a loss on it, backward: every parameter gradient and dL/dx vs the oracle (fp32)."""
+    from siren_mri_amd import modules
+    torch.manual_seed(21)
+    side, out = 16, 2
+    m = modules.SingleBVPNet(out_features=out, type="sine", hidden_features=64, num_hidden_layers=1,
+                             precision="fp32").to(DEV)
+    B = 2 if batched else 1
+    params = None
+    if batched:
+        params = {k: torch.stack([v * (1 + 0.04 * i) for i in range(B)]).requires_grad_(True)
+                  for k, v in m.state_dict().items()}
+    coords = orc.get_mgrid(side)[None].repeat(B, 1, 1)
+    gen = torch.Generator().manual_seed(8)
+    mask = (torch.rand(B, side * side, out, generator=gen) > 0.5).float()
+    k0 = torch.randn(B, side * side, out, generator=gen)
+    o = m({"coords": coords.to(DEV)}, params=params)
+    x = o["model_in"]
+    z = (1 - mask.to(DEV)) * o["model_out"] ** 2 + mask.to(DEV) * k0.to(DEV)
+    dz = torch.autograd.grad(z, [x], grad_outputs=torch.ones_like(z), create_graph=True)[0]
+    loss = (dz * torch.linspace(0.5, 1.5, 2, device=DEV)).square().sum()
+    loss.backward()
+    sd = m.state_dict() if params is None else None
+    for bi in range(B):
+        if batched:
+            ps = [(params[f"net.net.{i}.0.weight"][bi].detach().double().cpu().requires_grad_(True),
+                   params[f"net.net.{i}.0.bias"][bi].detach().double().cpu().requires_grad_(True)) for i in range(3)]
+        else:
+            ps = [(sd[f"net.net.{i}.0.weight"].double().cpu().clone().requires_grad_(True),
+                   sd[f"net.net.{i}.0.bias"].double().cpu().clone().requires_grad_(True)) for i in range(3)]
+        xr = coords[bi:bi + 1].double().clone().requires_grad_(True)
+        y = orc.siren_forward(xr, ps)
+        zr = (1 - mask[bi:bi + 1].double()) * y ** 2 + mask[bi:bi + 1].double() * k0[bi:bi + 1].double()
+        dzr = torch.autograd.grad(zr, [xr], grad_outputs=torch.ones_like(zr), create_graph=True)[0]
+        ref = (dzr * torch.linspace(0.5, 1.5, 2, dtype=torch.float64)).square().sum()
+        ref.backward()
+        assert orc.norm_rel(dz[bi:bi + 1].detach().cpu(), dzr.detach()) < 1e-5
+        for i, (W, b) in enumerate(ps):
+            gW = (params[f"net.net.{i}.0.weight"].grad[bi] if batched else m.net.net[i][0].weight.grad).cpu()
+            gb = (params[f"net.net.{i}.0.bias"].grad[bi] if batched else m.net.net[i][0].bias.grad).cpu()
+            assert orc.norm_rel(gW, W.grad) < 1e-4, f"sample {bi} layer {i} dW"
+            assert orc.norm_rel(gb, b.grad) < 1e-4, f"sample {bi} layer {i} db"
+        assert orc.norm_rel(x.grad[bi:bi + 1].cpu(), xr.grad) < 1e-4, f"sample {bi} dx"
+
+
+def test_unprovided_higher_orders_raise():
+    """Differentiating the SIREN's weight gradients (create_graph=True), or a derivative of the
+    tangent-stream backward, raises instead of giving silent zeros."""
+    from siren_mri_amd import diff_operators, modules
+    torch.manual_seed(2)
+    m = modules.SingleBVPNet(type="sine", hidden_features=32, num_hidden_layers=1, precision="fp32").to(DEV)
+    o = m({"coords": orc.get_mgrid(8)[None].to(DEV)})
+    gw = torch.autograd.grad(o["model_out"].square().sum(), list(m.parameters()), create_graph=True)
+    with pytest.raises(RuntimeError, match="not provided"):
+        gw[0].square().sum().backward()
+    o = m({"coords": orc.get_mgrid(8)[None].to(DEV)})
+    g = diff_operators.gradient(o["model_out"], o["model_in"])
+    gw = torch.autograd.grad(g.square().sum(), list(m.parameters())[:2], create_graph=True)
+    with pytest.raises(RuntimeError, match="not provided"):
+        gw[0].sum().backward()
