@@ -215,7 +215,7 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
   if constexpr (TOP) {
     for (int i = tid; i < TOP_MAXO * K; i += 512) {
       const int o = i / K, f = i - o * K;
-      WLs[i] = o < a.top.O ? a.top.WL[batch * a.top.wl_bstride + (int64_t)o * K + f] : 0.f;
+      WLs[i] = o < a.top.O ? a.top.WL[batch * a.top.wl_bstride + (int64_t)o * K + f] * a.w0 : 0.f;
     }
   }
   // In place over the A image, whose chunks the DMA filled with P_top phases (same swizzle).
@@ -234,10 +234,10 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
         bf16x8 v;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float dh = 0.f;
+          float dh = g[0] * WLs[8 * c + e];
 #pragma unroll
-          for (int o = 0; o < TOP_MAXO; ++o) dh = fmaf(g[o], WLs[o * K + 8 * c + e], dh);
-          v[e] = (bf16)((dh * PT::cosp(ph[e])) * a.w0);
+          for (int o = 1; o < TOP_MAXO; ++o) dh = fmaf(g[o], WLs[o * K + 8 * c + e], dh);
+          v[e] = (bf16)(dh * PT::cosp(ph[e]));
         }
         *(bf16x8*)p = v;
       }
@@ -629,7 +629,7 @@ __global__ __launch_bounds__(256) void tn_dw_kernel(TNArgs a) {
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
         const int ci = i0 + cu * VEC + e;
-        twl[o][e] = (o < a.top.O && ci < a.M) ? a.top.WL[batch * a.top.wl_bstride + (int64_t)o * a.M + ci] : 0.f;
+        twl[o][e] = (o < a.top.O && ci < a.M) ? a.top.WL[batch * a.top.wl_bstride + (int64_t)o * a.M + ci] * a.w0 : 0.f;
         tdw[o][e] = 0.f;
       }
     }
@@ -685,10 +685,10 @@ __global__ __launch_bounds__(256) void tn_dw_kernel(TNArgs a) {
         // dZ_top exactly as last_bwd_kernel forms it; dW_L / db_L sums on the side (tj == 0)
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
-          float dh = 0.f;
+          float dh = tg[q][0] * twl[0][e];
 #pragma unroll
-          for (int o = 0; o < TOP_MAXO; ++o) dh = fmaf(tg[q][o], twl[o][e], dh);
-          dv[e] = from_f32<op_t>((dh * PT::cosp(tph[q][e])) * a.w0);
+          for (int o = 1; o < TOP_MAXO; ++o) dh = fmaf(tg[q][o], twl[o][e], dh);
+          dv[e] = from_f32<op_t>(dh * PT::cosp(tph[q][e]));
         }
         if (do_db) {
 #pragma unroll
@@ -1002,7 +1002,7 @@ DEV void dx_ring_body_v1(const NTArgs& a, char* smem, const int64_t t0, const in
 #pragma unroll
     for (int o = 0; o < TOPO; ++o)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) twl[o][e] = a.top.WL[batch * a.top.wl_bstride + (int64_t)o * K + 8 * (tid & 31) + e];
+      for (int e = 0; e < 8; ++e) twl[o][e] = a.top.WL[batch * a.top.wl_bstride + (int64_t)o * K + 8 * (tid & 31) + e] * a.w0;
   }
 
   auto a_off = [&](int r, int c) -> int { return r * K * 2 + ((c ^ (r & SMASK)) << 4); };
@@ -1079,10 +1079,10 @@ DEV void dx_ring_body_v1(const NTArgs& a, char* smem, const int64_t t0, const in
         bf16x8 v;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float dh = 0.f;
+          float dh = g[0] * twl[0][e];
 #pragma unroll
-          for (int o = 0; o < TOP_MAXO; ++o) dh = fmaf(g[o], o < TOPO ? twl[o < TOPO ? o : 0][e] : 0.f, dh);
-          v[e] = (bf16)((dh * PT::cosp(ph[e])) * a.w0);
+          for (int o = 1; o < TOPO; ++o) dh = fmaf(g[o], twl[o][e], dh);
+          v[e] = (bf16)(dh * PT::cosp(ph[e]));
         }
         *(bf16x8*)p = v;
       }
@@ -1246,7 +1246,7 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
 #pragma unroll
     for (int o = 0; o < TOPO; ++o)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) twl[o][e] = a.top.WL[batch * a.top.wl_bstride + (int64_t)o * K + 8 * (tid & 31) + e];
+      for (int e = 0; e < 8; ++e) twl[o][e] = a.top.WL[batch * a.top.wl_bstride + (int64_t)o * K + 8 * (tid & 31) + e] * a.w0;
   }
 
   // both images: row r (512 B), 16-byte chunk c stored at chunk c ^ (r & 15)
@@ -1350,10 +1350,10 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
         bf16x8 v;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float dh = 0.f;
+          float dh = gg[0] * twl[0][e];
 #pragma unroll
-          for (int o = 0; o < TOP_MAXO; ++o) dh = fmaf(gg[o], o < TOPO ? twl[o < TOPO ? o : 0][e] : 0.f, dh);
-          v[e] = (bf16)((dh * PT::cosp(ph[e])) * a.w0);
+          for (int o = 1; o < TOPO; ++o) dh = fmaf(gg[o], twl[o][e], dh);
+          v[e] = (bf16)(dh * PT::cosp(ph[e]));
         }
         *(bf16x8*)pp = v;
       }
@@ -1847,7 +1847,7 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       tdw[o][e] = 0.f;
-      twl[o][e] = TOPO > 0 ? a.top.WL[batch * a.top.wl_bstride + (int64_t)o * M + 8 * cth + e] : 0.f;
+      twl[o][e] = TOPO > 0 ? a.top.WL[batch * a.top.wl_bstride + (int64_t)o * M + 8 * cth + e] * a.w0 : 0.f;
     }
   }
   if constexpr (RECC > 0) {
@@ -1897,10 +1897,10 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
       bf16x8 dz;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float dh = 0.f;
+        float dh = gg[0] * twl[0][e];
 #pragma unroll
-        for (int o = 0; o < TOP_MAXO; ++o) dh = fmaf(gg[o], o < TOPO ? twl[o < TOPO ? o : 0][e] : 0.f, dh);
-        dz[e] = (bf16)((dh * PT::cosp(pt[e])) * a.w0);
+        for (int o = 1; o < TO; ++o) dh = fmaf(gg[o], twl[o][e], dh);
+        dz[e] = (bf16)(dh * PT::cosp(pt[e]));
         const float sv = PT::sinp(pt[e]);
 #pragma unroll
         for (int o = 0; o < TO; ++o) tdw[o][e] = fmaf(gg[o], sv, tdw[o][e]);

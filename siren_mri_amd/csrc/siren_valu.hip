@@ -312,13 +312,14 @@ __global__ __launch_bounds__(256) void last_bwd_kernel(LastBwdArgs a) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float s = PT::sinp(pv[it][e]), c = PT::cosp(pv[it][e]);
-          float dh = 0.f;
+          // (sum_o g_o (W_L[o][f] w0)) cos(P): the arithmetic of every output-layer fusion
+          // (siren_gemm.hip, W_L prescaled by w0 once)
+          float dh = g[0] * (w[it][0][e] * a.w0);
 #pragma unroll
-          for (int o = 0; o < MAXO; ++o) {
-            dh = fmaf(g[o], w[it][o][e], dh);
-            dw[it][o][e] = fmaf(g[o], s, dw[it][o][e]);
-          }
-          dz[e] = (dh * c) * a.w0;
+          for (int o = 1; o < MAXO; ++o) dh = fmaf(g[o], w[it][o][e] * a.w0, dh);
+#pragma unroll
+          for (int o = 0; o < MAXO; ++o) dw[it][o][e] = fmaf(g[o], s, dw[it][o][e]);
+          dz[e] = dh * c;
         }
         store8f((grad_t*)a.dZ + row * a.F + f, dz);
       }
