@@ -85,7 +85,8 @@ KCLASS_SYMBOL = {
              14: "siren::pair_ring_bf16_kernel<2, true, true, 0, 2>"},
     "fp32": {1: "siren::nt_f32_kernel<0>", 2: "siren::nt_f32_kernel<1>", 3: "siren::tn_dw_kernel<0, false, false>"},
 }
-CONFIG_DEFAULT_STEPS = {"m": (50, 10), "c1": (50, 10), "c2": (50, 10), "c3": (20, 5), "c4": (10, 3)}
+CONFIG_DEFAULT_STEPS = {"m": (50, 10), "c1": (50, 10), "c2": (50, 10), "c3": (20, 5), "c4": (10, 3),
+                        "m_fp32": (10, 3), "m_shard8": (50, 10)}
 C4 = dict(num_fourier_features=8, kl_weight=2.78e-8, fw_weight=6.4e-6, lr=5.57e-5, fourier_features_scale=21,
           latent_dim=128, hidden_features_hyper=128, hidden_layers_hyper=2, hidden_layers=3, hidden_features=256,
           conv_kernel_size=7, num_conv_res_blocks=5, w0=30, slices=32, res=128)
@@ -96,7 +97,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=None)
     p.add_argument("--warmup", type=int, default=None)
-    p.add_argument("--config", default="m", choices=["m", "c1", "c2", "c3", "c4"])
+    p.add_argument("--config", default="m", choices=["m", "c1", "c2", "c3", "c4", "m_fp32", "m_shard8"])
     p.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     p.add_argument("--precision", default=None, choices=["bf16", "fp32"],
                    help="SIREN arithmetic (default: bf16, fp32 for c3)")
@@ -113,7 +114,7 @@ def parse():
     a.steps = st if a.steps is None else a.steps
     a.warmup = wu if a.warmup is None else a.warmup
     if a.precision is None:
-        a.precision = "fp32" if a.config == "c3" else "bf16"
+        a.precision = "fp32" if a.config in ("c3", "m_fp32") else "bf16"
     if a.no_graph:
         a.timing = "eager"
     return a
@@ -160,8 +161,10 @@ class Workload:
         self.precision, self.workload, self.data, self.extra = precision, workload, data, extra or {}
 
 
-def build_fit(cfg, args, dev, rank, world, precision):
-    """M / C1 / C2: the train_img.py fit (image_mse, Adam 1e-4) of one image."""
+def build_fit(cfg, args, dev, rank, world, precision, shard_of=None):
+    """M / C1 / C2: the train_img.py fit (image_mse, Adam 1e-4) of one image. shard_of=N: this
+    process computes rank 0's row shard of an N-way strong-scaling split, without the exchange (the
+    compute-only bound of the N-GPU speed-up)."""
     from siren_mri_amd import dataio, loss_functions, modules, training
     from siren_mri_amd.training_ddp import GradAllReducer, shard_rows
     side, nh = {"m": (512, 3), "c1": (64, 1), "c2": (256, 3)}[cfg]
@@ -179,7 +182,9 @@ def build_fit(cfg, args, dev, rank, world, precision):
         img = dataio.irdata_image(0, side)
         data = "IRData slice 0 (data/IRData.mat) / max, x2-1, bilinear 256^2; coords = get_mgrid(256)"
     img = img.reshape(-1, 1)
-    if args.scaling == "strong" and world > 1:
+    if shard_of:
+        lo, hi = shard_rows(grid.shape[0], 0, shard_of)
+    elif args.scaling == "strong" and world > 1:
         lo, hi = shard_rows(grid.shape[0], rank, world)
     else:
         lo, hi = 0, grid.shape[0]
@@ -204,7 +209,9 @@ def build_fit(cfg, args, dev, rank, world, precision):
 
     dims = [2] + [256] * (nh + 1) + [1]
     n = hi - lo
-    wl = (f"train_img.py fit step: {side}x{side} grid{' (strong: this rank ' + str(n) + ' rows)' if args.scaling == 'strong' and world > 1 else ''}, "
+    strong = shard_of or (args.scaling == "strong" and world > 1)
+    wl = (f"train_img.py fit step: {side}x{side} grid{' (strong: this rank ' + str(n) + ' rows)' if strong else ''}"
+          f"{' (1/' + str(shard_of) + ' shard, no exchange)' if shard_of else ''}, "
           f"SingleBVPNet {'-'.join(map(str, dims))} (w0=30), image_mse + Adam(1e-4), full batch")
     return Workload(cfg, step, n, 3 * siren_fwd_flops(dims) * n, dims, precision, wl, data,
                     {"optimizer": opt, "side": side})
@@ -312,9 +319,13 @@ def build_c4(args, dev, rank, world, precision, encoder_precision="bf16"):
 
 
 def build(cfg, args, dev, rank, world, precision=None):
-    precision = precision or ("fp32" if cfg == "c3" else args.precision)
+    precision = precision or ("fp32" if cfg in ("c3", "m_fp32") else args.precision)
     if cfg in ("m", "c1", "c2"):
         return build_fit(cfg, args, dev, rank, world, precision)
+    if cfg == "m_fp32":  # the metric fit in the reference's arithmetic (fp32 operands, exact-fp32 MFMA)
+        return build_fit("m", args, dev, rank, world, precision)
+    if cfg == "m_shard8":  # rank 0's 1/8 row shard of the metric grid (strong scaling at 8 GPUs)
+        return build_fit("m", args, dev, rank, world, precision, shard_of=8)
     if cfg == "c3":
         return build_c3(args, dev, rank, world, precision)
     return build_c4(args, dev, rank, world, precision)
@@ -751,7 +762,7 @@ def main():
     if world == 1 and not args.no_other_configs and args.config == "m":
         oargs = argparse.Namespace(**vars(args))
         others = {}
-        for cfg in ("c1", "c2", "c3", "c4"):
+        for cfg in ("c1", "c2", "c3", "c4", "m_fp32", "m_shard8"):
             oargs.steps, oargs.warmup = CONFIG_DEFAULT_STEPS[cfg]
             try:
                 r, owl, _, _ = measure(cfg, oargs, dev, rank, world, with_kernels=(cfg != "c4"))
@@ -760,9 +771,15 @@ def main():
             except Exception as e:  # noqa: BLE001 - a failing side config must not lose the metric line
                 others[cfg] = {"error": f"{type(e).__name__}: {e}"}
             torch.cuda.empty_cache()
+        sh = others.get("m_shard8", {})
+        if "ms_per_step" in sh:
+            # compute-only bound of the 8-GPU strong-scaling speed-up: the full step over one rank's
+            # 1/8 shard (no all-reduce; SURVEY.md §8(d) target >= 6.5x)
+            others["m_shard8"]["strong_scaling_bound_8gpu"] = round(res["ms_per_step"] / sh["ms_per_step"], 2)
         result["configs"] = others
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget_s)
+        # the metric config's CPU sample: 3 warm-up + 5 timed full steps need ~16 s
+        result["cpu_baseline"] = cpu_baseline(args.config, max(args.cpu_budget_s, 20.0 if args.config == "m" else 0.0))
         if args.config == "m" and not args.no_other_configs:
             result["cpu_baselines"] = {c: cpu_baseline(c, args.cpu_budget_s) for c in ("c1", "c2", "c3", "c4")}
     if rank == 0:

@@ -85,7 +85,8 @@ DEV void jvp_operand4(const JNTArgs& a, int64_t b, int s, int64_t n, int k, floa
   }
 }
 
-template <int PREC, int MODE>
+// LAP: the operand has a Laplacian stream (order 2); the gradient / Jacobian forms omit its code.
+template <int PREC, int MODE, bool LAP = false>
 __global__ __launch_bounds__(256) void jvp_nt_kernel(JNTArgs a) {
   using PT = Prec<PREC>;
   using phase_t = typename PT::phase_t;
@@ -140,17 +141,36 @@ __global__ __launch_bounds__(256) void jvp_nt_kernel(JNTArgs a) {
       const int64_t n = nq[q];
       if (s >= 0) {
         if constexpr (MODE == JMODE_FWD) {
+          // four consecutive columns: one 16-byte (fp32) or 8-byte (16-bit phase) load each
           const phase_t* P = (const phase_t*)a.P + (b * a.N + n) * K + k;
-          const float* Ub = a.U + b * (int64_t)(a.S - 1) * plane + n * K + k;
+          if constexpr (BF) {
+            const u16x4 pv = *(const u16x4*)P;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            praw[q][e] = P[e];
-            uraw[q][e] = (s >= 1 && s <= a.C) ? Ub[(int64_t)(s - 1) * plane + e] : 0.f;
+            for (int e = 0; e < 4; ++e) praw[q][e] = pv[e];
+          } else {
+            const f32x4 pv = *(const f32x4*)P;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) praw[q][e] = pv[e];
+          }
+          if (s >= 1 && s <= a.C) {
+            const f32x4 uv = *(const f32x4*)(a.U + b * (int64_t)(a.S - 1) * plane + (int64_t)(s - 1) * plane + n * K + k);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) uraw[q][e] = uv[e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) uraw[q][e] = 0.f;
           }
         } else {
           const grad_t* D = (const grad_t*)a.D + (b * rows + m0 + (u >> 3)) * K + k;
+          if constexpr (BF) {
+            const bf16x4 dv = *(const bf16x4*)D;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) areg[q][e] = to_f32(D[e]);
+            for (int e = 0; e < 4; ++e) areg[q][e] = (float)dv[e];
+          } else {
+            const f32x4 dv = *(const f32x4*)D;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) areg[q][e] = dv[e];
+          }
         }
       } else {
 #pragma unroll
@@ -162,8 +182,20 @@ __global__ __launch_bounds__(256) void jvp_nt_kernel(JNTArgs a) {
       const int u = tid + 256 * q;
       const int c = u >> 3, k = k0 + (u & 7) * 4;
       const int col = n0 + c;
+      if (col < a.Nout) {
+        if constexpr (BF) {
+          const bf16x4 wv = *(const bf16x4*)(W + (int64_t)col * K + k);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) breg[q][e] = col < a.Nout ? to_f32(W[(int64_t)col * K + k + e]) : 0.f;
+          for (int e = 0; e < 4; ++e) breg[q][e] = (float)wv[e];
+        } else {
+          const f32x4 wv = *(const f32x4*)((const float*)W + (int64_t)col * K + k);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) breg[q][e] = wv[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) breg[q][e] = 0.f;
+      }
     }
   };
   auto store = [&](int k0) {
@@ -172,12 +204,15 @@ __global__ __launch_bounds__(256) void jvp_nt_kernel(JNTArgs a) {
       for (int q = 0; q < 4; ++q) {
         const int s = sq[q];
         if (s < 0) continue;
-        if (s <= a.C) {
+        if (s == 0) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            areg[q][e] = s == 0 ? PT::sinp(praw[q][e]) : a.w0 * PT::cosp(praw[q][e]) * uraw[q][e];
-        } else {  // the Laplacian stream (C + 1 tangent planes): from memory
-          jvp_operand4<PREC>(a, b, s, nq[q], k0 + ((tid + 256 * q) & 7) * 4, areg[q]);
+          for (int e = 0; e < 4; ++e) areg[q][e] = PT::sinp(praw[q][e]);
+        } else if (!LAP || s <= a.C) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) areg[q][e] = a.w0 * PT::cosp(praw[q][e]) * uraw[q][e];
+        } else {
+          if constexpr (LAP)  // the Laplacian stream (C + 1 tangent planes): from memory
+            jvp_operand4<PREC>(a, b, s, nq[q], k0 + ((tid + 256 * q) & 7) * 4, areg[q]);
         }
       }
     }
@@ -244,34 +279,48 @@ __global__ __launch_bounds__(256) void jvp_nt_kernel(JNTArgs a) {
   // stacked row -> (stream, row) from one division for the block's first row (the epilogue's 128
   // rows per thread each paid a 64-bit division: a third of the kernel's instructions)
   const int64_t s_m0 = m0 / a.N, n_m0 = m0 - s_m0 * a.N;
+  // this lane's 4 output columns (one per bn) and their biases
+  const int colb = n0 + 128 * wn + (lane & 31);
+  float bcol[4];
 #pragma unroll
-  for (int bn = 0; bn < 4; ++bn) {
-    const int col = n0 + 128 * wn + 32 * bn + (lane & 31);
-    if (col >= a.Nout) continue;
+  for (int bn = 0; bn < 4; ++bn)
+    bcol[bn] = (MODE == JMODE_FWD && s_m0 == 0 && colb + 32 * bn < a.Nout) ? bias[colb + 32 * bn] : 0.f;
+  // row-major: each of the lane's 32 rows is resolved to (stream, row) and a base pointer once,
+  // then its 4 columns are stored
 #pragma unroll
-    for (int bm = 0; bm < 2; ++bm)
+  for (int bm = 0; bm < 2; ++bm)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int off = 64 * wm + 32 * bm + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-        const int64_t row = m0 + off;
-        if (row >= rows) continue;
-        const float v = acc[bm][bn][e];
-        if constexpr (MODE == JMODE_FWD) {
-          int s = (int)s_m0;
-          int64_t n = n_m0 + off;
-          while (n >= a.N) {
-            n -= a.N;
-            ++s;
-          }
-          if (s == 0)
-            ((phase_t*)a.Pout)[(b * a.N + n) * a.Nout + col] = PT::encz(v, bias[col], a.w0);
-          else
-            a.Uout[((b * (a.S - 1) + (s - 1)) * a.N + n) * a.Nout + col] = v;
-        } else {
-          a.Uout[(b * rows + row) * a.Nout + col] = v;
+    for (int e = 0; e < 16; ++e) {
+      const int off = 64 * wm + 32 * bm + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+      const int64_t row = m0 + off;
+      if (row >= rows) continue;
+      if constexpr (MODE == JMODE_FWD) {
+        int s = (int)s_m0;
+        int64_t n = n_m0 + off;
+        while (n >= a.N) {
+          n -= a.N;
+          ++s;
         }
+        if (s == 0) {
+          phase_t* dst = (phase_t*)a.Pout + (b * a.N + n) * a.Nout + colb;
+#pragma unroll
+          for (int bn = 0; bn < 4; ++bn) {
+            // (a block that starts in stream s > 0 never holds stream-0 rows: bcol only when s_m0 == 0)
+            if (colb + 32 * bn < a.Nout) dst[32 * bn] = PT::encz(acc[bm][bn][e], bcol[bn], a.w0);
+          }
+        } else {
+          float* dst = a.Uout + ((b * (a.S - 1) + (s - 1)) * a.N + n) * a.Nout + colb;
+#pragma unroll
+          for (int bn = 0; bn < 4; ++bn)
+            if (colb + 32 * bn < a.Nout) dst[32 * bn] = acc[bm][bn][e];
+        }
+      } else {
+        float* dst = a.Uout + (b * rows + row) * a.Nout + colb;
+#pragma unroll
+        for (int bn = 0; bn < 4; ++bn)
+          if (colb + 32 * bn < a.Nout) dst[32 * bn] = acc[bm][bn][e];
       }
-  }
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -290,7 +339,7 @@ struct JTNArgs {
   float w0;
 };
 
-template <int PREC>
+template <int PREC, bool LAP = false>
 __global__ __launch_bounds__(256) void jvp_tn_kernel(JTNArgs a) {
   using PT = Prec<PREC>;
   using phase_t = typename PT::phase_t;
@@ -329,16 +378,18 @@ __global__ __launch_bounds__(256) void jvp_tn_kernel(JTNArgs a) {
   const int cu = tid & 127, ru = tid >> 7;
   float draw[16], uraw[16];
   phase_t praw[16];
-  auto row_sn = [&](int64_t rc, int r, int& s, int64_t& n) {
-    const int64_t s0 = rc / a.N;  // (wave-uniform: one scalar division per call site and chunk)
+  // (stream, row) of the chunk's row r from the chunk's first row (s0, n0): one scalar division
+  // per chunk, outside the unrolled per-row loops
+  auto row_sn = [&](int64_t s0, int64_t n0, int r, int& s, int64_t& n) {
     s = (int)s0;
-    n = rc - s0 * a.N + r;
+    n = n0 + r;
     while (n >= a.N) {
       n -= a.N;
       ++s;
     }
   };
   auto fetch = [&](int64_t rc) {
+    const int64_t s0 = rc / a.N, n0 = rc - s0 * a.N;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int r = ru + 2 * q;
@@ -349,7 +400,7 @@ __global__ __launch_bounds__(256) void jvp_tn_kernel(JTNArgs a) {
       if (row < r_end) {
         int s;
         int64_t n;
-        row_sn(rc, r, s, n);
+        row_sn(s0, n0, r, s, n);
         if (i0 + cu < a.M) draw[q] = to_f32(((const grad_t*)a.D)[(b * rows + row) * a.M + i0 + cu]);
         if (j0 + cu < a.Kin) {
           praw[q] = ((const phase_t*)a.P)[(b * a.N + n) * a.Kin + j0 + cu];
@@ -361,6 +412,7 @@ __global__ __launch_bounds__(256) void jvp_tn_kernel(JTNArgs a) {
   fetch(r_begin);
   for (int64_t rc = r_begin; rc < r_end; rc += KC) {
     __syncthreads();
+    const int64_t s0 = rc / a.N, n0 = rc - s0 * a.N;
     // stage 32 rows x 128 columns of D and X (16 elements per thread each)
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -370,15 +422,15 @@ __global__ __launch_bounds__(256) void jvp_tn_kernel(JTNArgs a) {
       if (row < r_end) {
         int s;
         int64_t n;
-        row_sn(rc, r, s, n);
+        row_sn(s0, n0, r, s, n);
         dv = draw[q];
         if (j0 + cu < a.Kin) {
           const phase_t p = praw[q];
           if (s == 0) {
             xv = PT::sinp(p);
-          } else if (s <= a.C) {
+          } else if (!LAP || s <= a.C) {
             xv = a.w0 * PT::cosp(p) * uraw[q];
-          } else {  // Laplacian stream: S = w0 c V - w0^2 s Q (its C + 1 tangent planes from memory)
+          } else if constexpr (LAP) {  // Laplacian stream: S = w0 c V - w0^2 s Q (C + 1 planes from memory)
             const float* Ue = a.U + b * a.Su * plane + n * a.Kin + j0 + cu;
             float qq = 0.f;
             for (int j = 0; j < a.C; ++j) qq = fmaf(Ue[j * plane], Ue[j * plane], qq);

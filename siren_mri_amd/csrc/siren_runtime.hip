@@ -1245,7 +1245,8 @@ int jvp_forward_impl(const siren_mlp_desc* d, int order, const float* x, float* 
     a.Nout = d->dims[l + 1];
     a.w0 = d->w0;
     dim3 grid((unsigned)cdiv((int64_t)jl.S * g.rows, JNT_BM), (unsigned)cdiv(a.Nout, JNT_BN), (unsigned)g.nb);
-    hipLaunchKernelGGL((jvp_nt_kernel<PREC, JMODE_FWD>), grid, dim3(256), 0, st, a);
+    if (a.lap) hipLaunchKernelGGL((jvp_nt_kernel<PREC, JMODE_FWD, true>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((jvp_nt_kernel<PREC, JMODE_FWD>), grid, dim3(256), 0, st, a);
     if ((rc = check_launch("jvp_nt fwd"))) return rc;
   }
   {
@@ -1333,7 +1334,8 @@ int jvp_backward_impl(const siren_mlp_desc* d, int order, const float* x, const 
       a.Kin = N;
       a.w0 = d->w0;
       dim3 grid((unsigned)(cdiv(M, 128) * cdiv(N, 128)), (unsigned)s.nsplit, (unsigned)g.nb);
-      hipLaunchKernelGGL(jvp_tn_kernel<PREC>, grid, dim3(256), 0, st, a);
+      if (lapmode) hipLaunchKernelGGL((jvp_tn_kernel<PREC, true>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((jvp_tn_kernel<PREC>), grid, dim3(256), 0, st, a);
       if ((rc = check_launch("jvp_tn"))) return rc;
       if ((rc = launch_reduce(part, s.nsplit, a.split_stride, g.nb, (int64_t)M * N + M, (int64_t)M * N,
                               dW[l], db[l], st)))

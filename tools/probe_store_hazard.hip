@@ -95,6 +95,88 @@ __global__ __launch_bounds__(512) void probe(uint32_t* out, const uint32_t* src,
   }
 }
 
+// Deep store queue: 8 buffer_store_dwordx4 back to back (v[200:231]), optionally behind K LDS-DMA
+// loads, then GAP filler instructions (VALU adds, or s_nop when NOP), then every data register is
+// overwritten. The stores' data may be read out of the VGPRs late when the queue ahead is deep.
+template <int GAP, int K, int NOP>
+__global__ __launch_bounds__(512) void probe8(uint32_t* out, const uint32_t* src, int src_words) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES][K > 0 ? K * 64 : 64];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(src), (short)0,
+                                                                      src_words * 4, 0x00020000);
+  const uint32_t ldsbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t*)&lds[wave][0];
+  const int slot0 = (blockIdx.x * WAVES + wave) * (ITERS / 8);
+  for (int it = 0; it < ITERS / 8; ++it) {
+    const uint32_t tag = ((uint32_t)(slot0 + it) * 64u + lane) * 8u;  // store j of this lane: tag + j
+    const uint32_t voff = tag * 16u;                                     // + 16 * 64 * ... per store j below
+    uint32_t soff = (((blockIdx.x * 577u + it * 97u + wave * 13u) * 4096u) % (uint32_t)(src_words * 4 - 1024)) & ~255u;
+    soff += lane * 4;
+    asm volatile(
+        ".irp j, 0,1,2,3,4,5,6,7\n"
+        "v_add_u32 v[200+4*\\j], \\j, %0\n"
+        "v_or_b32 v[201+4*\\j], 0x10000000, v[200+4*\\j]\n"
+        "v_or_b32 v[202+4*\\j], 0x20000000, v[200+4*\\j]\n"
+        "v_or_b32 v[203+4*\\j], 0x30000000, v[200+4*\\j]\n"
+        ".endr\n"
+        "s_mov_b32 m0, %3\n"
+        ".rept %6\n"
+        "buffer_load_dword %2, %4, 0 offen lds\n"
+        ".endr\n"
+        ".irp j, 0,1,2,3,4,5,6,7\n"
+        "buffer_store_dwordx4 v[200+4*\\j:203+4*\\j], %1, %5, 0 offen offset:16*\\j\n"
+        ".endr\n"
+        ".if %8\n"
+        ".rept %7\n"
+        "s_nop 0\n"
+        ".endr\n"
+        ".else\n"
+        ".rept %7\n"
+        "v_add_u32 v240, 1, v240\n"
+        ".endr\n"
+        ".endif\n"
+        ".irp r, 200,201,202,203,204,205,206,207,208,209,210,211,212,213,214,215,216,217,218,219,220,221,222,223,224,225,226,227,228,229,230,231\n"
+        "v_mov_b32 v\\r, 0xdead0000\n"
+        ".endr\n"
+        "s_waitcnt vmcnt(0)\n" ::"v"(tag),
+        "v"(voff), "v"(soff), "s"(ldsbase), "s"(rs), "s"(ro), "n"(K), "n"(GAP), "n"(NOP)
+        : "memory", "m0", "v200", "v201", "v202", "v203", "v204", "v205", "v206", "v207", "v208", "v209", "v210",
+          "v211", "v212", "v213", "v214", "v215", "v216", "v217", "v218", "v219", "v220", "v221", "v222", "v223",
+          "v224", "v225", "v226", "v227", "v228", "v229", "v230", "v231", "v240");
+  }
+}
+
+template <int GAP, int K, int NOP>
+void run8(uint32_t* out, const uint32_t* src, int src_words, int blocks, const char* name) {
+  const size_t stores = (size_t)blocks * WAVES * (ITERS / 8) * 64 * 8;
+  hipMemset(out, 0, stores * 16);
+  long bad = 0, trials = 0;
+  int lanes[64] = {0};
+  std::vector<uint32_t> h(stores * 4);
+  for (int rep = 0; rep < 20; ++rep) {
+    hipLaunchKernelGGL((probe8<GAP, K, NOP>), dim3(blocks), dim3(512), 0, 0, out, src, src_words);
+    hipMemcpy(h.data(), out, stores * 16, hipMemcpyDeviceToHost);
+    for (size_t i = 0; i < stores; ++i) {
+      const uint32_t t = (uint32_t)i;  // store index = tag + j (row-major: lane-major tags x 8 stores)
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t want = q == 0 ? t : (t | ((uint32_t)q << 28));
+        if (h[4 * i + q] != want) {
+          ++bad;
+          ++lanes[(i / 8) & 63];
+        }
+      }
+    }
+    trials += (long)stores;
+  }
+  printf("%-44s gap %3d (%s): %10ld corrupted dwords of %ld stores x 4", name, GAP, NOP ? "s_nop" : "VALU", bad, trials);
+  if (bad) {
+    printf("  lanes:");
+    for (int l = 0; l < 64; ++l)
+      if (lanes[l]) printf(" %d", l);
+  }
+  printf("\n");
+}
+
 template <int GAP, int MODE, int K>
 void run(uint32_t* out, const uint32_t* src, int src_words, int blocks, const char* name) {
   const int storers = (MODE == 2 || MODE == 6) ? 4 : WAVES;
@@ -138,6 +220,9 @@ int main() {
   run<0, 0, 0>(out, src, src_words, blocks, "no other traffic");
   run<0, 3, 8>(out, src, src_words, blocks, "8 VGPR loads before the store");
   run<0, 1, 8>(out, src, src_words, blocks, "8 LDS-DMA loads before the store");
+  run<1, 0, 0>(out, src, src_words, blocks, "no other traffic");
+  run<2, 0, 0>(out, src, src_words, blocks, "no other traffic");
+  run<2, 1, 8>(out, src, src_words, blocks, "8 LDS-DMA loads before the store");
   run<4, 1, 8>(out, src, src_words, blocks, "8 LDS-DMA loads before the store");
   run<16, 1, 8>(out, src, src_words, blocks, "8 LDS-DMA loads before the store");
   run<64, 1, 8>(out, src, src_words, blocks, "8 LDS-DMA loads before the store");
@@ -146,6 +231,15 @@ int main() {
   run<0, 2, 8>(out, src, src_words, blocks, "partner waves stream LDS-DMA");
   run<16, 2, 8>(out, src, src_words, blocks, "partner waves stream LDS-DMA");
   run<0, 6, 8>(out, src, src_words, blocks, "partner LDS-DMA, expcnt(0) after the store");
+  run8<0, 0, 0>(out, src, src_words, blocks, "8 stores in flight");
+  run8<2, 0, 0>(out, src, src_words, blocks, "8 stores in flight");
+  run8<4, 0, 0>(out, src, src_words, blocks, "8 stores in flight");
+  run8<2, 8, 0>(out, src, src_words, blocks, "8 LDS-DMA + 8 stores in flight");
+  run8<4, 8, 0>(out, src, src_words, blocks, "8 LDS-DMA + 8 stores in flight");
+  run8<16, 8, 0>(out, src, src_words, blocks, "8 LDS-DMA + 8 stores in flight");
+  run8<4, 8, 1>(out, src, src_words, blocks, "8 LDS-DMA + 8 stores in flight");
+  run8<16, 8, 1>(out, src, src_words, blocks, "8 LDS-DMA + 8 stores in flight");
+  run8<64, 8, 1>(out, src, src_words, blocks, "8 LDS-DMA + 8 stores in flight");
   hipError_t e = hipDeviceSynchronize();
   printf("status %s\n", hipGetErrorString(e));
   return 0;
