@@ -223,6 +223,21 @@ template <typename T, typename U>
 DEV void store_complete2(const T& data, const U& held) {
   asm volatile("s_waitcnt vmcnt(0)" ::"v"(data), "v"(held));
 }
+// The measured rule (tools/probe_store_hazard.hip): a store of more than 8 bytes
+// reads its data VGPRs during the 2 wait states after its issue; a VALU write of them with 0 wait
+// states in between corrupts lanes 8-15 of each 16-lane group, with 1 lanes 12-15, with 2 none
+// (2.7e9 stores, with or without LDS-DMA or other stores in flight). hipcc 7.2 sometimes leaves a
+// single wait state there. These stores carry their own `s_nop 1` (2 wait states) inside the asm
+// statement that takes the data as input, so nothing can write those registers before it has
+// passed — instead of waiting for the store to complete.
+DEV void store_b128_ws2(const u32x4_t& v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(r), "s"(soff)
+               : "memory");
+}
+DEV void store_b32_ws2(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  asm volatile("buffer_store_dword %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(r), "s"(soff)
+               : "memory");
+}
 #ifndef SIREN_STORE_EXPCNT
 #define SIREN_STORE_EXPCNT 1
 #endif

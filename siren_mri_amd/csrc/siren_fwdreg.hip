@@ -155,8 +155,18 @@ DEV constexpr int freg_in0(int ks, int h) { return 32 * (ks >> 1) + 16 * (ks & 1
 #ifndef SIREN_FREG_SPAN
 #define SIREN_FREG_SPAN 9
 #endif
+// 1 (default): the phase-code and y stores are asm stores followed by s_nop 1 (siren_common.h
+// store_b128_ws2: the measured 2 wait states), no store-completion waits; 0: the round-3 form
+// (builtin stores, data held until an s_waitcnt vmcnt(0) at K step SIREN_FREG_WAITAT)
+#ifndef SIREN_FREG_STORE_WS2
+#define SIREN_FREG_STORE_WS2 1
+#endif
 #ifndef SIREN_FREG_WAITAT
+#if SIREN_FREG_STORE_WS2
+#define SIREN_FREG_WAITAT -1
+#else
 #define SIREN_FREG_WAITAT 15
+#endif
 #endif
 static_assert(SIREN_FREG_SPAN >= 7 && SIREN_FREG_SPAN <= 13, "epilogue span");
 static_assert(SIREN_FREG_WAITAT < 0 || (SIREN_FREG_WAITAT > SIREN_FREG_SPAN && SIREN_FREG_WAITAT < 16), "wait step");
@@ -417,6 +427,10 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     }
     // the block offset as the store's constant SOFFSET (one address VGPR for every store: folding
     // it into the VGPR offset costs a register per store and spilled)
+#if SIREN_FREG_STORE_WS2
+    store_b128_ws2(c, p_rsrc(pl), p_voff, pfb * 64 + half * 32);
+    return;
+#endif
     __builtin_amdgcn_raw_buffer_store_b128(c, p_rsrc(pl), p_voff, pfb * 64 + half * 32, 0);
 #if SIREN_FREG_STORE_PAIR
     if constexpr (FORM == 1 && SIREN_FREG_DEFER && !WIDE) {  // (the wide form: 24 VGPRs short)
@@ -426,7 +440,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
       prevst = c;
     } else {
       // one wait per block: the half-0 store's data stays reserved (an input of the half-1 wait)
-      if (half == 1 && SIREN_FREG_WAITAT < 0) store_complete2(c, held);
+      if (half == 1 && SIREN_FREG_WAITAT < 0 && !SIREN_FREG_STORE_WS2) store_complete2(c, held);
     }
 #else
     store_complete(c);
@@ -636,8 +650,12 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
         float z = accO[e];
         if (a.sine_out) z = Prec<kPrecBF16>::sinr(w0 * z);
         const uint32_t zb = __builtin_bit_cast(uint32_t, z);
+#if SIREN_FREG_STORE_WS2
+        store_b32_ws2(zb, ry, yv, 4 * e);
+#else
         __builtin_amdgcn_raw_buffer_store_b32(zb, ry, yv, 4 * e, 0);
         store_complete(zb);
+#endif
       }
     }
     freg_drain();  // the next round's first fragments

@@ -25,7 +25,7 @@
 constexpr int ITERS = 64;
 constexpr int WAVES = 8;
 
-template <int GAP, int MODE, int K>
+template <int GAP, int MODE, int K, int NOPK = 0>
 __global__ __launch_bounds__(512) void probe(uint32_t* out, const uint32_t* src, int src_words) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES][K > 0 ? K * 64 : 64];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -82,15 +82,21 @@ __global__ __launch_bounds__(512) void probe(uint32_t* out, const uint32_t* src,
         ".if %6 == 5\n"
         "s_waitcnt vmcnt(0)\n"
         ".endif\n"
+        ".if %9\n"
+        ".rept %8\n"
+        "s_nop %9 - 1\n"
+        ".endr\n"
+        ".else\n"
         ".rept %8\n"
         "v_add_u32 v220, 1, v220\n"
         ".endr\n"
+        ".endif\n"
         "v_mov_b32 v200, 0xdead0000\n"
         "v_mov_b32 v201, 0xdead0001\n"
         "v_mov_b32 v202, 0xdead0002\n"
         "v_mov_b32 v203, 0xdead0003\n"
         "s_waitcnt vmcnt(0)\n" ::"v"(tag),
-        "v"(voff), "v"(soff), "s"(ldsbase), "s"(rs), "s"(ro), "n"(MODE), "n"(K), "n"(GAP)
+        "v"(voff), "v"(soff), "s"(ldsbase), "s"(rs), "s"(ro), "n"(MODE), "n"(K), "n"(GAP), "n"(NOPK)
         : "memory", "m0", "v200", "v201", "v202", "v203", "v210", "v211", "v212", "v213", "v220");
   }
 }
@@ -177,7 +183,7 @@ void run8(uint32_t* out, const uint32_t* src, int src_words, int blocks, const c
   printf("\n");
 }
 
-template <int GAP, int MODE, int K>
+template <int GAP, int MODE, int K, int NOPK = 0>
 void run(uint32_t* out, const uint32_t* src, int src_words, int blocks, const char* name) {
   const int storers = (MODE == 2 || MODE == 6) ? 4 : WAVES;
   const size_t words = (size_t)blocks * storers * ITERS * 64 * 4;
@@ -186,7 +192,7 @@ void run(uint32_t* out, const uint32_t* src, int src_words, int blocks, const ch
   std::vector<uint32_t> h(words);
   int lanes[64] = {0};
   for (int rep = 0; rep < 20; ++rep) {
-    hipLaunchKernelGGL((probe<GAP, MODE, K>), dim3(blocks), dim3(512), 0, 0, out, src, src_words);
+    hipLaunchKernelGGL((probe<GAP, MODE, K, NOPK>), dim3(blocks), dim3(512), 0, 0, out, src, src_words);
     hipMemcpy(h.data(), out, words * 4, hipMemcpyDeviceToHost);
     for (size_t i = 0; i < words / 4; ++i) {
       const uint32_t tag = (uint32_t)i;
@@ -201,7 +207,8 @@ void run(uint32_t* out, const uint32_t* src, int src_words, int blocks, const ch
     }
     trials += (int)(words / 4);
   }
-  printf("%-44s gap %3d: %8d corrupted dwords (%d first-dword) of %d stores x 4", name, GAP, bad, bad_first, trials);
+  printf("%-44s gap %3d %-9s: %9d corrupted dwords (%d first-dword) of %d stores x 4", name, GAP,
+         NOPK ? (NOPK == 1 ? "s_nop 0" : "s_nop 1") : "VALU", bad, bad_first, trials);
   if (bad) {
     printf("  lanes:");
     for (int l = 0; l < 64; ++l)
@@ -218,19 +225,19 @@ int main() {
   hipMalloc(&out, (size_t)blocks * WAVES * ITERS * 64 * 16);
   hipMemset(src, 0x5a, (size_t)src_words * 4);
   run<0, 0, 0>(out, src, src_words, blocks, "no other traffic");
-  run<0, 3, 8>(out, src, src_words, blocks, "8 VGPR loads before the store");
-  run<0, 1, 8>(out, src, src_words, blocks, "8 LDS-DMA loads before the store");
   run<1, 0, 0>(out, src, src_words, blocks, "no other traffic");
   run<2, 0, 0>(out, src, src_words, blocks, "no other traffic");
+  run<1, 0, 0, 1>(out, src, src_words, blocks, "no other traffic");
+  run<2, 0, 0, 1>(out, src, src_words, blocks, "no other traffic");
+  run<3, 0, 0, 1>(out, src, src_words, blocks, "no other traffic");
+  run<1, 0, 0, 2>(out, src, src_words, blocks, "no other traffic");
+  run<2, 0, 0, 2>(out, src, src_words, blocks, "no other traffic");
+  run<1, 1, 8, 2>(out, src, src_words, blocks, "8 LDS-DMA loads before the store");
+  run<2, 1, 8, 2>(out, src, src_words, blocks, "8 LDS-DMA loads before the store");
+  run<1, 2, 8, 2>(out, src, src_words, blocks, "partner waves stream LDS-DMA");
+  run<2, 2, 8, 1>(out, src, src_words, blocks, "partner waves stream LDS-DMA");
+  run<4, 2, 8, 1>(out, src, src_words, blocks, "partner waves stream LDS-DMA");
   run<2, 1, 8>(out, src, src_words, blocks, "8 LDS-DMA loads before the store");
-  run<4, 1, 8>(out, src, src_words, blocks, "8 LDS-DMA loads before the store");
-  run<16, 1, 8>(out, src, src_words, blocks, "8 LDS-DMA loads before the store");
-  run<64, 1, 8>(out, src, src_words, blocks, "8 LDS-DMA loads before the store");
-  run<0, 4, 8>(out, src, src_words, blocks, "8 LDS-DMA loads, expcnt(0) after the store");
-  run<0, 5, 8>(out, src, src_words, blocks, "8 LDS-DMA loads, vmcnt(0) after the store");
-  run<0, 2, 8>(out, src, src_words, blocks, "partner waves stream LDS-DMA");
-  run<16, 2, 8>(out, src, src_words, blocks, "partner waves stream LDS-DMA");
-  run<0, 6, 8>(out, src, src_words, blocks, "partner LDS-DMA, expcnt(0) after the store");
   run8<0, 0, 0>(out, src, src_words, blocks, "8 stores in flight");
   run8<2, 0, 0>(out, src, src_words, blocks, "8 stores in flight");
   run8<4, 0, 0>(out, src, src_words, blocks, "8 stores in flight");
