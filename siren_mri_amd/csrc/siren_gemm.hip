@@ -402,18 +402,25 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
 // fp32 nt_gemm (exact-fp32 MFMA 32x32x2). Register-staged A (and P for DX) tiles, 32 rows per
 // tile, padded LDS rows (K+1 floats) for conflict-free column reads; same epilogue scheme.
 // ------------------------------------------------------------------------------------------
-template <int MODE>
+// KMAX 512 (hidden width 257..512, fp32 mode): the K range is two chunks of 256; the wave's W
+// columns of one chunk are in registers at a time (reloaded from L2 per chunk and tile: 1 KB per
+// lane per tile against 256 fp32 MFMAs of 64 cycles), and the A tile is single-buffered (its
+// 32 x 513 floats twice would not fit beside the C staging).
+template <int MODE, int KMAX = 256>
 __global__ __launch_bounds__(512) void nt_f32_kernel(NTArgs a) {
   using PT = Prec<kPrecF32>;
-  constexpr int KMAX = 256;
+  static_assert(KMAX == 256 || KMAX == 512, "fp32 GEMM K bound");
   constexpr int BM = 32;
   constexpr int AROW = KMAX + 1;
   constexpr int A_BYTES = BM * AROW * 4;
+  constexpr int NABUF = KMAX == 256 ? 2 : 1;
   constexpr int C_BYTES = BM * 256 * 4;
-  constexpr int NKS = KMAX / 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * A_BYTES + 2 * C_BYTES];
+  constexpr int NKC = 128;                 // K steps (of 2) per register chunk
+  constexpr int NCH = KMAX / 256;          // chunks
+  constexpr int AQ = KMAX / 64;            // A-tile float4 units per thread (32 rows x KMAX / 4 / 512)
+  __shared__ __attribute__((aligned(16))) char smem[NABUF * A_BYTES + 2 * C_BYTES];
   float* const As0 = (float*)smem;
-  char* const Cs0 = smem + 2 * A_BYTES;
+  char* const Cs0 = smem + NABUF * A_BYTES;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -432,18 +439,24 @@ __global__ __launch_bounds__(512) void nt_f32_kernel(NTArgs a) {
   const int a_cpr = K >> 2, c_cpr = ncols >> 2;
 
   const float* Wb = (const float*)a.W + batch * a.w_bstride + (int64_t)(n0 + col_l) * K;
-  float wf[NKS];
+  float wf[NKC];
+  auto load_w = [&](int c) {
 #pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) wf[ks] = (ks < nks && col_ok) ? Wb[2 * ks + h] : 0.f;
+    for (int ks = 0; ks < NKC; ++ks) {
+      const int kk = NKC * c + ks;
+      wf[ks] = (kk < nks && col_ok) ? Wb[2 * kk + h] : 0.f;
+    }
+  };
+  load_w(0);
   constexpr bool FWDLIKE = MODE == MODE_FWD || MODE == MODE_FIRST;
   float bcol = 0.f;
   if constexpr (FWDLIKE) bcol = col_ok ? a.bias[batch * a.bias_bstride + n0 + col_l] : 0.f;
 
-  f32x4 areg[4], preg[4];
+  f32x4 areg[AQ], preg[4];
   auto load_tile = [&](int64_t t) {
     const int64_t m0 = t * BM;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < AQ; ++q) {
       const int u = tid + 512 * q;
       const int r = u / a_cpr, c = u - r * a_cpr;
       const bool in = r < BM && m0 + r < rows;
@@ -459,7 +472,11 @@ __global__ __launch_bounds__(512) void nt_f32_kernel(NTArgs a) {
         areg[q] = in ? *(const f32x4*)((const float*)a.A + (rowbase + m0 + r) * K + c * 4)
                      : f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      if constexpr (MODE == MODE_DX) {
+    }
+    if constexpr (MODE == MODE_DX) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int u = tid + 512 * q;
         const int rp = u / c_cpr, cp = u - rp * c_cpr;
         preg[q] = (rp < BM && m0 + rp < rows)
                       ? *(const f32x4*)((const float*)a.Paux + (rowbase + m0 + rp) * N + n0 + cp * 4)
@@ -468,9 +485,9 @@ __global__ __launch_bounds__(512) void nt_f32_kernel(NTArgs a) {
     }
   };
   auto store_tile = [&](int buf) {
-    float* As = As0 + buf * (A_BYTES / 4);
+    float* As = As0 + (NABUF == 2 ? buf : 0) * (A_BYTES / 4);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < AQ; ++q) {
       const int u = tid + 512 * q;
       const int r = u / a_cpr, c = u - r * a_cpr;
       if (r < BM) {
@@ -478,7 +495,11 @@ __global__ __launch_bounds__(512) void nt_f32_kernel(NTArgs a) {
         for (int e = 0; e < 4; ++e)
           As[r * AROW + c * 4 + e] = (MODE == MODE_FWD) ? PT::sinp(areg[q][e]) : areg[q][e];
       }
-      if constexpr (MODE == MODE_DX) {
+    }
+    if constexpr (MODE == MODE_DX) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int u = tid + 512 * q;
         const int rp = u / c_cpr, cp = u - rp * c_cpr;
         if (rp < BM) *(f32x4*)(Cs0 + buf * C_BYTES + (rp * ncols + cp * 4) * 4) = preg[q];
       }
@@ -498,10 +519,15 @@ __global__ __launch_bounds__(512) void nt_f32_kernel(NTArgs a) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
     if (wave_on) {
-      const float* As = As0 + cur * (A_BYTES / 4);
+      const float* As = As0 + (NABUF == 2 ? cur : 0) * (A_BYTES / 4);
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks)
-        if (ks < nks) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[r32 * AROW + 2 * ks + h], wf[ks], acc, 0, 0, 0);
+      for (int c = 0; c < NCH; ++c) {
+        if (NCH > 1 && (c > 0 || t != blockIdx.x)) load_w(c);  // (chunk 0 of the first tile: loaded above)
+#pragma unroll
+        for (int ks = 0; ks < NKC; ++ks)
+          if (NKC * c + ks < nks)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[r32 * AROW + 2 * (NKC * c + ks) + h], wf[ks], acc, 0, 0, 0);
+      }
       float* Cs = (float*)(Cs0 + cur * C_BYTES);
 #pragma unroll
       for (int e = 0; e < 16 && col_ok; ++e) {

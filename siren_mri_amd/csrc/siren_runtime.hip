@@ -502,7 +502,8 @@ int launch_nt(const NTArgs& a, int64_t nb, int kclass, hipStream_t st) {
     else hipLaunchKernelGGL((nt_bf16_kernel<MODE, 512, TOP, BOT>), grid, dim3(512), 0, st, a);
   } else {
     static_assert(PREC == kPrecBF16 || !(TOP || BOT), "backward fusions are bf16-mode paths");
-    hipLaunchKernelGGL((nt_f32_kernel<MODE>), grid, dim3(512), 0, st, a);
+    if (kmax == 256) hipLaunchKernelGGL((nt_f32_kernel<MODE>), grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((nt_f32_kernel<MODE, 512>), grid, dim3(512), 0, st, a);
   }
   tmark_end(kclass, st);
   static const char* const names[] = {"nt_gemm fwd", "nt_gemm dx", "nt_gemm first", "nt_gemm dx-input"};
@@ -1424,13 +1425,12 @@ int siren_mlp_check(const siren_mlp_desc* d) {
     return fail(SIREN_EINVAL, "empty input (batch=%lld rows=%lld)", (long long)d->batch,
                 (long long)d->rows_per_batch);
   if (d->batch > 65535) return fail(SIREN_EINVAL, "batch %lld > 65535", (long long)d->batch);
-  const int kmax = d->prec == SIREN_PREC_BF16 ? 512 : 256;  // MFMA K bound of the GEMM kernels
+  const int kmax = 512;  // MFMA K bound of the GEMM kernels (fp32: two register chunks of 256)
   if (d->dims[0] < 1 || (wide_input(d) && first_kp(d) > kmax))
-    return fail(SIREN_EINVAL, "in_features=%d unsupported (1..%d for this precision)", d->dims[0],
-                d->prec == SIREN_PREC_BF16 ? 512 : 256);
+    return fail(SIREN_EINVAL, "in_features=%d unsupported (1..%d)", d->dims[0], kmax);
   if (d->dims[L] < 1 || d->dims[L] > 8)
     return fail(SIREN_EINVAL, "out_features=%d unsupported (1..8)", d->dims[L]);
-  const int hmax = d->prec == SIREN_PREC_BF16 ? 512 : 256;
+  const int hmax = 512;
   for (int l = 1; l < L; ++l)
     if (d->dims[l] < 32 || d->dims[l] % 32 != 0 || d->dims[l] > hmax)
       return fail(SIREN_EINVAL, "hidden width dims[%d]=%d must be a multiple of 32 in [32, %d]",

@@ -88,9 +88,8 @@ def test_batched_weights_hypernet_shape(precision):
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 @pytest.mark.parametrize("dims", [[2, 96, 96, 1], [2, 160, 224, 96, 1], [3, 32, 480, 2]])
 def test_irregular_hidden_widths(precision, dims):
-    # widths that are multiples of 32 but not powers of two (LDS swizzle must stay inside a row)
-    if precision == "fp32" and max(dims[1:-1]) > 256:
-        pytest.skip("fp32 hidden widths are bounded by 256")
+    # widths that are multiples of 32 but not powers of two (LDS swizzle must stay inside a row);
+    # fp32 widths above 256 run the two-chunk K = 512 form of the fp32 GEMM
     params = orc.siren_init(dims, seed=sum(dims))
     x = torch.rand(1, 517, dims[0], generator=torch.Generator().manual_seed(2)) * 2 - 1
     _check(x, params, precision)
@@ -200,3 +199,30 @@ def test_cpu_tensor_raises():
     params = orc.siren_init(dims, seed=0)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         siren_mlp(torch.zeros(1, 4, 2), [W for W, _ in params], [b for _, b in params])
+
+
+@pytest.mark.parametrize("nh", [1, 3])
+def test_fp32_hidden_512(nh):
+    """SingleBVPNet(hidden_features=512) in the default (fp32) arithmetic — modules.py:125-126 allows
+    any width: forward, every gradient and dx against the fp64 oracle at the fp32 tolerances."""
+    dims = orc.siren_dims(2, 512, nh, 1)
+    params = orc.siren_init(dims, seed=512 + nh)
+    x = orc.get_mgrid(40).unsqueeze(0)
+    lw = torch.randn(1, 40 * 40, 1, generator=torch.Generator().manual_seed(3))
+    _check(x, params, "fp32", loss_w=lw)
+
+
+def test_fp32_hidden_512_module_and_gradient():
+    """The module path (SingleBVPNet, default precision) at hidden 512 and its analytic gradient."""
+    from siren_mri_amd import diff_operators, modules
+    torch.manual_seed(4)
+    m = modules.SingleBVPNet(type="sine", hidden_features=512, num_hidden_layers=2).to(DEV)
+    coords = orc.get_mgrid(24)[None]
+    o = m({"coords": coords.to(DEV)})
+    g = diff_operators.gradient(o["model_out"], o["model_in"])
+    sd = m.state_dict()
+    ps = [(sd[f"net.net.{i}.0.weight"].double().cpu(), sd[f"net.net.{i}.0.bias"].double().cpu()) for i in range(4)]
+    x = coords.double().clone().requires_grad_(True)
+    y = orc.siren_forward(x, ps)
+    assert orc.norm_rel(o["model_out"].detach().cpu(), y.detach()) < 1e-5
+    assert orc.norm_rel(g.detach().cpu(), orc.gradient(y, x).detach()) < 1e-5

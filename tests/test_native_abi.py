@@ -42,12 +42,10 @@ def test_check_accepts_reference_configs():
     for dims, kw in [([2, 256, 256, 256, 256, 1], dict(rows_per_batch=512 * 512)),
                      ([2, 256, 256, 1], dict(rows_per_batch=64 * 64)),
                      ([16, 256, 256, 256, 256, 2], dict(batch=32, rows_per_batch=16384, weights_batched=True)),
-                     # config 4 (2*60 Fourier features) and config 5 (2*228, hidden 512: bf16 only)
+                     # config 4 (2*60 Fourier features) and config 5 (2*228, hidden 512; fp32 too)
                      ([120, 256, 256, 256, 256, 2], dict(batch=32, rows_per_batch=16384, weights_batched=True)),
                      ([456] + [512] * 5 + [2], dict(batch=32, rows_per_batch=16384, weights_batched=True))]:
         for prec in (_native.PREC_F32, _native.PREC_BF16):
-            if prec == _native.PREC_F32 and max(dims[:-1]) > 256:
-                continue
             d = _desc(dims, prec=prec, **kw)
             assert lib.siren_mlp_check(ctypes.byref(d)) == 0, _native.last_error()
             assert lib.siren_mlp_saved_bytes(ctypes.byref(d)) > 0
