@@ -144,14 +144,24 @@ def test_wide_input_config5_shape_bf16():
     _check(x, params, "bf16")
 
 
-def test_wide_input_fp32_bound():
-    from siren_mri_amd.ops import siren_mlp
-    from siren_mri_amd._native import NativeError
+def test_wide_input_fp32_456():
+    """Config 5's Fourier-feature width (2 x 228 = 456 inputs) in fp32: layer 0 on the two-chunk
+    K = 512 fp32 GEMM (it was rejected before round 4)."""
     dims = [456, 256, 1]
     params = orc.siren_init(dims, seed=1)
-    with pytest.raises(NativeError, match="in_features"):
-        siren_mlp(torch.zeros(1, 4, 456, device=DEV), [W.to(DEV) for W, _ in params],
-                  [b.to(DEV) for _, b in params], precision="fp32")
+    x = torch.rand(1, 300, 456, generator=torch.Generator().manual_seed(6)) * 2 - 1
+    _check(x, params, "fp32")
+
+
+def test_wide_input_bound():
+    from siren_mri_amd.ops import siren_mlp
+    from siren_mri_amd._native import NativeError
+    dims = [600, 256, 1]
+    params = orc.siren_init(dims, seed=1)
+    for prec in ("fp32", "bf16"):
+        with pytest.raises(NativeError, match="in_features"):
+            siren_mlp(torch.zeros(1, 4, 600, device=DEV), [W.to(DEV) for W, _ in params],
+                      [b.to(DEV) for _, b in params], precision=prec)
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
@@ -170,14 +180,17 @@ def test_wide_hidden_bf16():
     _check(x, params, "bf16")
 
 
-def test_wide_hidden_fp32_rejected():
+def test_hidden_width_bound():
+    """Hidden widths above 512 are rejected in both arithmetics (fp32 supports up to 512 since
+    round 4: test_fp32_hidden_512)."""
     from siren_mri_amd.ops import siren_mlp
     from siren_mri_amd._native import NativeError
-    dims = orc.siren_dims(2, 512, 1, 1)
+    dims = orc.siren_dims(2, 544, 1, 1)
     params = orc.siren_init(dims, seed=9)
-    with pytest.raises(NativeError, match="hidden width"):
-        siren_mlp(torch.zeros(1, 4, 2, device=DEV), [W.to(DEV) for W, _ in params],
-                  [b.to(DEV) for _, b in params], precision="fp32")
+    for prec in ("fp32", "bf16"):
+        with pytest.raises(NativeError, match="hidden width"):
+            siren_mlp(torch.zeros(1, 4, 2, device=DEV), [W.to(DEV) for W, _ in params],
+                      [b.to(DEV) for _, b in params], precision=prec)
 
 
 def test_metric_size_fp32_forward():

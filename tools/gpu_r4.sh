@@ -12,6 +12,8 @@ for st in "$@"; do
       timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_jvp.py tests/test_gpu_metric_parity.py tests/test_gpu_modules.py -s > $out/jvp_tests.txt 2>&1 || exit $? ;;
     fwd)
       timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_fwdreg.py tests/test_gpu_fused.py tests/test_gpu_freg_magic.py tests/test_gpu_wide.py tests/test_gpu_metric_parity.py -s > $out/fwd_tests.txt 2>&1 || exit $? ;;
+    stack)
+      timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_siren_stack.py -s > $out/stack_tests.txt 2>&1 || exit $? ;;
     new)
       timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
         tests/test_gpu_sincos.py tests/test_gpu_jvp.py tests/test_gpu_ddp2.py -s > $out/new_tests.txt 2>&1 || exit $? ;;
