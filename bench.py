@@ -72,10 +72,11 @@ KCLASS_NAMES = {
     13: "pair_ring_bf16_kernel<top> (top hidden layer + output layer: dX and dW roles)",
     14: "pair_ring_bf16_kernel<bottom> (layer 1 + first layer, P_0 rebuilt: dX and dW roles)",
 }
-# kernel symbol of each class at the M shape (C = 2 inputs, O = 1 output), as rocprofv3 names it
+# kernel symbol of each class at the M shape (C = 2 inputs, O = 1 output), as rocprofv3 names it (the
+# M step's forward is the fused-loss form, siren_mri_amd/fusion.py)
 KCLASS_SYMBOL = {
     "bf16": {1: "siren::nt_bf16_kernel<0, 256, false, false>", 2: "siren::nt_bf16_kernel<1, 256, false, false>",
-             3: "siren::tn_dw_kernel<1, false, false>", 4: "siren::fused_fwd_reg_kernel<2, 1, 0>",
+             3: "siren::tn_dw_kernel<1, false, false>", 4: "siren::fused_fwd_reg_kernel<2, 1, 0, true>",
              5: "siren::bwd_ring_bf16_kernel", 6: "siren::dx_ring_bf16_kernel<0, false, false, 0>",
              7: "siren::dw_ring_bf16_kernel<0, 0>", 8: "siren::dx_ring_bf16_kernel<2, true, true, 0>",
              9: "siren::dw_ring_bf16_kernel<2, 0>", 10: "siren::dx_ring_bf16_kernel<0, false, false, 1>",
@@ -83,7 +84,7 @@ KCLASS_SYMBOL = {
              12: "siren::pair_ring_bf16_kernel<0, false, false, 0, 0>",
              13: "siren::pair_ring_bf16_kernel<0, false, false, 1, 0>",
              14: "siren::pair_ring_bf16_kernel<2, true, true, 0, 2>"},
-    "fp32": {1: "siren::nt_f32_kernel<0>", 2: "siren::nt_f32_kernel<1>", 3: "siren::tn_dw_kernel<0, false, false>"},
+    "fp32": {1: "siren::nt_f32_kernel<0, 256>", 2: "siren::nt_f32_kernel<1, 256>", 3: "siren::tn_dw_kernel<0, false, false>"},
 }
 CONFIG_DEFAULT_STEPS = {"m": (50, 10), "c1": (50, 10), "c2": (50, 10), "c3": (20, 5), "c4": (10, 3),
                         "m_fp32": (10, 3), "m_shard8": (50, 10)}
@@ -165,7 +166,7 @@ def build_fit(cfg, args, dev, rank, world, precision, shard_of=None):
     """M / C1 / C2: the train_img.py fit (image_mse, Adam 1e-4) of one image. shard_of=N: this
     process computes rank 0's row shard of an N-way strong-scaling split, without the exchange (the
     compute-only bound of the N-GPU speed-up)."""
-    from siren_mri_amd import dataio, loss_functions, modules, training
+    from siren_mri_amd import dataio, fusion, loss_functions, modules, training
     from siren_mri_amd.training_ddp import GradAllReducer, shard_rows
     side, nh = {"m": (512, 3), "c1": (64, 1), "c2": (256, 3)}[cfg]
     torch.manual_seed(0)
@@ -196,10 +197,14 @@ def build_fit(cfg, args, dev, rank, world, precision, shard_of=None):
     one = torch.ones((), device=dev)  # the backward's seed, allocated once (not a fill kernel per step)
 
     def step():
+        # training.train's step: the target staged for the forward's fused loss epilogue
+        # (siren_mri_amd/fusion.py), then model -> image_mse's reduction (sum / 128^2 over this
+        # rank's coordinates: in a strong-scaling shard the partial sums over the ranks add up to
+        # the whole image's loss) -> backward
+        fusion.stage_image_loss(tgt, weight=loss_functions.KSPACE_WEIGHT)
         out = model(model_input)
-        # image_mse's reduction (sum / 128^2) over this rank's coordinates: in a strong-scaling
-        # shard the partial sums over the ranks add up to the whole image's loss
         loss = loss_functions.weighted_sse(out["model_out"], tgt)
+        fusion.clear()
         loss.backward(one)
         if reducer is not None:
             reducer()
@@ -268,7 +273,7 @@ def build_c4(args, dev, rank, world, precision, encoder_precision="bf16"):
     # searched once during the warm-up steps
     torch.backends.cudnn.benchmark = True
     from functools import partial
-    from siren_mri_amd import loss_functions, meta_modules, training
+    from siren_mri_amd import fusion, loss_functions, meta_modules, training
     from siren_mri_amd.features import GaussianFourierFeatureTransform
     from siren_mri_amd.training_ddp import GradAllReducer
     torch.manual_seed(0)
@@ -291,8 +296,10 @@ def build_c4(args, dev, rank, world, precision, encoder_precision="bf16"):
     def step():
         mi = dict(inp)
         mi["coords"] = ff(inp["coords"])
+        fusion.stage_image_loss(gt["img"])  # as training.train: the fused DC + loss epilogue
         out = model(mi)
         losses = loss_fn(out, gt)
+        fusion.clear()
         loss = sum(v.mean() for v in losses.values())
         if reducer is not None:
             reducer.begin()
@@ -778,8 +785,8 @@ def main():
             others["m_shard8"]["strong_scaling_bound_8gpu"] = round(res["ms_per_step"] / sh["ms_per_step"], 2)
         result["configs"] = others
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # the metric config's CPU sample: 3 warm-up + 5 timed full steps need ~16 s
-        result["cpu_baseline"] = cpu_baseline(args.config, max(args.cpu_budget_s, 20.0 if args.config == "m" else 0.0))
+        # the metric config's CPU sample: 3 warm-up + 5 timed full steps need ~20 s
+        result["cpu_baseline"] = cpu_baseline(args.config, max(args.cpu_budget_s, 24.0 if args.config == "m" else 0.0))
         if args.config == "m" and not args.no_other_configs:
             result["cpu_baselines"] = {c: cpu_baseline(c, args.cpu_budget_s) for c in ("c1", "c2", "c3", "c4")}
     if rank == 0:

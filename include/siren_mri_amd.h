@@ -98,6 +98,41 @@ int siren_mlp_backward(const siren_mlp_desc* d, const float* x, const float* dy,
                        float* dx, void* stream);
 
 /*
+ * Forward with a fused image loss (replaces, in one launch, the SIREN
+ * forward (modules.py:146-164), DataConsistencyInKspace (data_consistency.py:32-48) and
+ * image_mse's masked k-space SSE (loss_functions.py:66-101, utils.py:25-40)). Rows are the
+ * SIREN's [batch * rows_per_batch, O] outputs; for each element p = DC(y) (when k0 is given:
+ * (1 - mask) y + mask k0, or the noisy form), d = hf (p - target) (hf indexed by the row within its
+ * weight set), loss = weight * sum d^2 (deterministic order), y_dc = p and
+ * dy = 2 weight hf d dDC/dy — dL/dy for a unit upstream gradient, which siren_mlp_backward_ex
+ * scales by the device scalar dy_scale (the loss's upstream gradient) inside its output-layer
+ * kernels. Shapes: the bf16 register-resident forward's (siren_mlp_loss_check).
+ */
+typedef struct siren_loss_desc {
+  const float* target;  /* [B * N, O]                                                  */
+  const float* k0;      /* [B, O, N] k-space planes (NCHW), or NULL (no data consistency) */
+  const float* mask;    /* [B, O, N] sampling mask, or NULL                             */
+  const float* hf;      /* [N] high-frequency mask, or NULL                             */
+  int64_t hf_len;       /* entries of hf (= rows_per_batch)                             */
+  float noise;          /* DataConsistencyInKspace noise_lvl (0: noiseless)              */
+  float weight;         /* image_mse's 1 / 128^2                                        */
+  float* y_dc;          /* [B * N, O] DC(y) (with k0), or NULL                          */
+  float* dy;            /* [B * N, O] dL/dy for a unit upstream gradient                */
+  float* loss;          /* [1]                                                          */
+  void* loss_workspace; /* siren_sse_workspace_bytes(), zero-initialised once, one per stream */
+  int64_t loss_workspace_bytes;
+} siren_loss_desc;
+int siren_mlp_loss_check(const siren_mlp_desc* d, const siren_loss_desc* l);
+int siren_mlp_forward_loss(const siren_mlp_desc* d, const siren_loss_desc* l, const float* x, float* y,
+                           void* saved, int64_t saved_bytes, void* workspace, int64_t workspace_bytes,
+                           void* stream);
+/* siren_mlp_backward with dL/dy = dy * (*dy_scale) (dy_scale: device pointer, NULL = 1). */
+int siren_mlp_backward_ex(const siren_mlp_desc* d, const float* x, const float* dy, const float* dy_scale,
+                          const void* saved, int64_t saved_bytes, void* workspace,
+                          int64_t workspace_bytes, float* const* dweight, float* const* dbias,
+                          float* dx, void* stream);
+
+/*
  * Analytic spatial derivatives of the SIREN output w.r.t. its input (tangent streams carried
  * through the fused layers instead of an autograd graph). Replaces diff_operators.gradient
  * (diff_operators.py:39-43: grad[n][k] = sum_c dy_c/dx_k) and, with order 2, laplace

@@ -30,6 +30,9 @@ EXPORTED_SYMBOLS = (
     "siren_mlp_workspace_bytes",
     "siren_mlp_forward",
     "siren_mlp_backward",
+    "siren_mlp_loss_check",
+    "siren_mlp_forward_loss",
+    "siren_mlp_backward_ex",
     "siren_jvp_saved_bytes",
     "siren_jvp_workspace_bytes",
     "siren_jvp_forward",
@@ -87,6 +90,25 @@ class SirenMLPDesc(ctypes.Structure):
     ]
 
 
+class SirenLossDesc(ctypes.Structure):
+    """Mirror of ``siren_loss_desc`` (include/siren_mri_amd.h)."""
+
+    _fields_ = [
+        ("target", ctypes.c_void_p),
+        ("k0", ctypes.c_void_p),
+        ("mask", ctypes.c_void_p),
+        ("hf", ctypes.c_void_p),
+        ("hf_len", ctypes.c_int64),
+        ("noise", ctypes.c_float),
+        ("weight", ctypes.c_float),
+        ("y_dc", ctypes.c_void_p),
+        ("dy", ctypes.c_void_p),
+        ("loss", ctypes.c_void_p),
+        ("loss_workspace", ctypes.c_void_p),
+        ("loss_workspace_bytes", ctypes.c_int64),
+    ]
+
+
 ADAM_MAX_TENSORS = 48
 
 
@@ -138,6 +160,13 @@ def _declare(lib):
                                        ctypes.POINTER(vp), ctypes.POINTER(vp), vp, vp]
     lib.siren_mlp_backward.restype = ctypes.c_int
     ci = ctypes.c_int
+    LP = ctypes.POINTER(SirenLossDesc)
+    lib.siren_mlp_loss_check.argtypes = [P, LP]
+    lib.siren_mlp_loss_check.restype = ci
+    lib.siren_mlp_forward_loss.argtypes = [P, LP, vp, vp, vp, i64, vp, i64, vp]
+    lib.siren_mlp_forward_loss.restype = ci
+    lib.siren_mlp_backward_ex.argtypes = [P, vp, vp, vp, vp, i64, vp, i64, ctypes.POINTER(vp), ctypes.POINTER(vp), vp, vp]
+    lib.siren_mlp_backward_ex.restype = ci
     lib.siren_jvp_saved_bytes.argtypes = [P, ci]
     lib.siren_jvp_saved_bytes.restype = i64
     lib.siren_jvp_workspace_bytes.argtypes = [P, ci]
@@ -253,6 +282,21 @@ def stream_handle(device: torch.device) -> int:
     """The current HIP stream of `device` as an integer (torch's raw getter: no Stream object)."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
     return torch._C._cuda_getCurrentRawStream(idx)
+
+
+_SSE_WS: dict = {}
+
+
+def sse_workspace(device) -> torch.Tensor:
+    """The per-(device, stream) partial-sum / hand-off-counter workspace of the deterministic loss
+    reductions (siren_sse_workspace_bytes; zeroed once, left zeroed by every launch): two launches
+    that may run concurrently never share one."""
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    ws = _SSE_WS.get(key)
+    if ws is None:
+        ws = torch.zeros(int(lib().siren_sse_workspace_bytes()), dtype=torch.uint8, device=device)
+        _SSE_WS[key] = ws
+    return ws
 
 
 def make_desc(dims, weights, biases, *, w0: float, prec: int, outermost_linear: bool,

@@ -314,4 +314,22 @@ DEV bf16x8 tr16_value(const TrFrag& f) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// Data consistency in k-space (data_consistency.py:8-48): (1 - m) p + m k0, or
+// (1 - m) p + m (p + v k0) / (1 + v) (noisy), in the reference's operation order with no fused
+// multiply-adds (bit-identical to PyTorch's elementwise chain); used by siren_kspace.hip and by the
+// forward's fused output-layer loss (siren_fwdreg.hip).
+DEV float dc_value(float p, float k, float m, float noise) {
+  const float keep = __fmul_rn(__fsub_rn(1.f, m), p);
+  if (noise > 0.f) {
+    const float mix = __fdiv_rn(__fadd_rn(p, __fmul_rn(noise, k)), __fadd_rn(1.f, noise));
+    return __fadd_rn(keep, __fmul_rn(m, mix));
+  }
+  return __fadd_rn(keep, __fmul_rn(m, k));
+}
+// d out / d pred of dc_value
+DEV float dc_coef(float m, float noise) {
+  const float keep = __fsub_rn(1.f, m);
+  return noise > 0.f ? __fadd_rn(keep, __fdiv_rn(m, __fadd_rn(1.f, noise))) : keep;
+}
+
 }  // namespace siren

@@ -116,6 +116,19 @@ struct FwdRegArgs {
   int O, nh, sine_out;
   int cin;                    // inputs of layer 0 (= C, or 5..16 for the wide form C = 16)
   float w0;
+  // LOSS instantiations: image_mse's (masked k-space) SSE of the output,
+  // with the data consistency of DataConsistencyInKspace applied first, in the output layer's
+  // epilogue. Layouts as siren_kspace.hip: rows [B*N, O]; k0 / mask NCHW planes [B, O, N].
+  const float* ltgt;          // [B*N, O] target
+  const float* lk0;           // [B, O, N] k-space samples, or null (no data consistency)
+  const float* lmask;         // [B, O, N] sampling mask
+  const float* lhf;           // [N] high-frequency mask, or null
+  float* ldc;                 // [B*N, O] DC(y) (model_out of the DC module), or null
+  float* ldy;                 // [B*N, O] dL/dy for a unit upstream gradient
+  float* lloss;               // [1] the loss
+  float* lpart;               // [grid] per-workgroup partial sums
+  unsigned* lcounter;         // zero between launches (the last workgroup resets it)
+  float lnoise, lweight;
 #ifdef SIREN_FREG_CLOCK
   long long* clk;             // diagnostic builds only: [grid][4] s_memtime / s_memrealtime stamps
 #endif
@@ -160,6 +173,10 @@ DEV constexpr int freg_in0(int ks, int h) { return 32 * (ks >> 1) + 16 * (ks & 1
 // (builtin stores, data held until an s_waitcnt vmcnt(0) at K step SIREN_FREG_WAITAT)
 #ifndef SIREN_FREG_STORE_WS2
 #define SIREN_FREG_STORE_WS2 1
+#endif
+// LOSS forms: 1 = the output layer loads its rows' targets before its MFMAs (latency hidden)
+#ifndef SIREN_FREG_LOSS_PREFETCH
+#define SIREN_FREG_LOSS_PREFETCH 1
 #endif
 #ifndef SIREN_FREG_WAITAT
 #if SIREN_FREG_STORE_WS2
@@ -209,12 +226,17 @@ struct RegPrepArgs {
 // launched back to back; each reads the weight bounds and the one whose form does not apply exits
 // at once (one kernel holding both forms needs more than 256 VGPRs). Without the bounds (null
 // wbound) FORM 0 does the work.
+// LOSS: the output layer's epilogue also computes the fused image loss (FwdRegArgs l* fields): per
+// output element p = DC(y) (if k0), d = hf (p - t), the loss sum d^2 (per-lane, per-workgroup,
+// then the last workgroup adds the workgroup sums in index order: deterministic), DC(y) and
+// dL/dy = 2 w hf d dDC/dy (the backward's output-layer kernels scale it by the loss's upstream
+// gradient, TopArgs::dy_scale). The arithmetic is ksse_fwd_kernel's / ksse_bwd_kernel's.
 #ifdef SIREN_FWDREG_DECL_ONLY  // the kernels are compiled in siren_fwdreg_inst.hip
-template <int C, int OC, int FORM>
+template <int C, int OC, int FORM, bool LOSS = false>
 __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a);
 __global__ __launch_bounds__(256) void prep_reg_kernel(RegPrepArgs a);
 #else
-template <int C, int OC, int FORM>
+template <int C, int OC, int FORM, bool LOSS = false>
 __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   constexpr int F = 256, NKS = 16, NB = 8;
   constexpr bool WIDE = C > 4;
@@ -619,9 +641,26 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     freg_drain();  // the next layer's first fragments (prefetched) land before any control flow
   };
 
+  float lsum = 0.f;  // LOSS: this lane's sum of d^2 over its rounds
   // output layer: y = H W_L^T + b_L (MFMA rows = outputs), beside the last hidden block's epilogue
   auto output_layer = [&](h16x8 (&Hin)[NKS], auto mtag) __attribute__((always_inline)) {
     if constexpr (WIDE) load_xw(tcur + G);  // the next round's inputs
+    // LOSS: this lane's targets (and high-frequency weight) are loaded before the output layer's
+    // MFMAs, so their latency hides behind them instead of following the y stores
+    constexpr int NE = OC == 1 ? 1 : 4;
+    float ltv[NE];
+    float lhv = 1.f;
+    if constexpr (LOSS && SIREN_FREG_LOSS_PREFETCH) {
+      const int64_t r0 = tcur * FREG_WG_ROWS;
+      const int yrow = wave * FREG_WROWS + j;
+      const bool live = r0 + yrow < rows;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        const int o = 4 * hh + e;
+        ltv[e] = (live && o < O) ? a.ltgt[(batch * rows + r0 + yrow) * O + o] : 0.f;
+      }
+      if (a.lhf && live) lhv = a.lhf[r0 + yrow];
+    }
     f32x16 accO = accNx;
     Epi ep;
     const uint32_t va_nxt = slot_va(0);  // the next round's first block
@@ -656,6 +695,34 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
         __builtin_amdgcn_raw_buffer_store_b32(zb, ry, yv, 4 * e, 0);
         store_complete(zb);
 #endif
+        if constexpr (LOSS) {
+          if (yrow < nv && e < NE) {
+            const int o = 4 * hh + e;
+            const int64_t n = r0 + yrow;                    // the row within its weight set
+            const int64_t q = (batch * rows + n) * O + o;   // [B*N, O] element
+            float p = z;
+            float coef = 1.f;
+            if (a.lk0) {
+              const int64_t pl = (batch * O + o) * rows + n;  // NCHW plane element
+              const float m = a.lmask[pl];
+              p = dc_value(z, a.lk0[pl], m, a.lnoise);
+              coef = dc_coef(m, a.lnoise);
+              a.ldc[q] = p;
+            }
+#if SIREN_FREG_LOSS_PREFETCH
+            const float h = lhv;
+            const float t = ltv[e < NE ? e : 0];
+#else
+            const float h = a.lhf ? a.lhf[n] : 1.f;
+            const float t = a.ltgt[q];
+#endif
+            const float dd = __fmul_rn(h, __fsub_rn(p, t));
+            lsum = fmaf(dd, dd, lsum);
+            float v = h * (dd * (2.f * a.lweight));
+            if (a.lk0) v *= coef;
+            a.ldy[q] = v;
+          }
+        }
       }
     }
     freg_drain();  // the next round's first fragments
@@ -770,6 +837,40 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
 #endif
   // no LDS-DMA may land after the workgroup has released its LDS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (LOSS) {
+    // workgroup sum (waves in order), then the last workgroup to finish adds the workgroup sums in
+    // index order (the hand-off of siren_loss.hip / siren_kspace.hip)
+    __shared__ float lred[8];
+    __shared__ unsigned lticket;
+    const float ws_ = wave_sum(lsum);
+    if (lane == 0) lred[wave] = ws_;
+    __syncthreads();
+    const unsigned nwg = gridDim.x * gridDim.y, wg = blockIdx.y * gridDim.x + blockIdx.x;
+    if (tid == 0) {
+      float sacc = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) sacc += lred[w];
+      __hip_atomic_store(a.lpart + wg, sacc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lticket = __hip_atomic_fetch_add(a.lcounter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (lticket == nwg - 1) {
+      float sacc = 0.f;
+      for (unsigned b = tid; b < nwg; b += 512) sacc += __hip_atomic_load(a.lpart + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sacc = wave_sum(sacc);
+      __syncthreads();
+      if (lane == 0) lred[wave] = sacc;
+      __syncthreads();
+      if (tid == 0) {
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) tot += lred[w];
+        a.lloss[0] = tot * a.lweight;
+        __hip_atomic_store(a.lcounter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
 #ifdef SIREN_FREG_CLOCK
   if (tid == 0) {
     const long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();

@@ -32,6 +32,7 @@ constexpr int TOP_MAXO = 2;
 struct TopArgs {
   const void* Ptop;    // [rows, F_top] phase of the last sine layer
   const float* dy;     // [rows, O]
+  const float* dy_scale;  // [1] device scalar multiplying dy (the upstream gradient of a fused loss), or null
   const float* WL;     // [nb_w][O, F_top]
   int64_t wl_bstride;
   float* partL;        // tn_dw only: dW_L / db_L partial slabs [split][nb][O*F_top + O]
@@ -212,6 +213,7 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
   };
   // TOP: the dZ_top tile is formed from the register-staged P_top phases, the dy tile (LDS-DMA)
   // and W_L (LDS), exactly as last_bwd_kernel forms it, and written into the A image.
+  const float dys = (TOP && a.top.dy_scale) ? *a.top.dy_scale : 1.f;
   if constexpr (TOP) {
     for (int i = tid; i < TOP_MAXO * K; i += 512) {
       const int o = i / K, f = i - o * K;
@@ -230,7 +232,7 @@ __global__ __launch_bounds__(512) void nt_bf16_kernel(NTArgs a) {
         const u16x8 ph = *(const u16x8*)p;
         float g[TOP_MAXO];
 #pragma unroll
-        for (int o = 0; o < TOP_MAXO; ++o) g[o] = o < a.top.O ? gt[r * a.top.O + o] : 0.f;
+        for (int o = 0; o < TOP_MAXO; ++o) g[o] = o < a.top.O ? gt[r * a.top.O + o] * dys : 0.f;
         bf16x8 v;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -646,6 +648,7 @@ __global__ __launch_bounds__(256) void tn_dw_kernel(TNArgs a) {
   u16x8 tph[TOP ? UPT : 1];
   float tg[TOP ? UPT : 1][TOP_MAXO];
   float twl[TOP_MAXO][TOP ? VEC : 1];
+  const float dys = (TOP && a.top.dy_scale) ? *a.top.dy_scale : 1.f;
   float tdw[TOP_MAXO][TOP ? VEC : 1];
   float tdb[TOP_MAXO];
   if constexpr (TOP) {
@@ -672,7 +675,7 @@ __global__ __launch_bounds__(256) void tn_dw_kernel(TNArgs a) {
         const int64_t rr = rowbase + (in ? row : 0);
         tph[q] = in ? *(const u16x8*)((const uint16_t*)a.top.Ptop + rr * a.M + ci) : u16x8{};
 #pragma unroll
-        for (int o = 0; o < TOP_MAXO; ++o) tg[q][o] = (in && o < a.top.O) ? a.top.dy[rr * a.top.O + o] : 0.f;
+        for (int o = 0; o < TOP_MAXO; ++o) tg[q][o] = (in && o < a.top.O) ? a.top.dy[rr * a.top.O + o] * dys : 0.f;
       } else if (row < r_end && ci < a.M) {
         dreg[q] = *(const d_in_t*)((const grad_t*)a.D + (rowbase + row) * a.M + ci);
       } else {
@@ -1024,6 +1027,7 @@ DEV void dx_ring_body_v1(const NTArgs& a, char* smem, const int64_t t0, const in
 
   // TOP: this thread's W_L columns for the in-place dZ_top pass (chunk tid % 32 is fixed)
   float twl[TOPO > 0 ? TOPO : 1][8];
+  const float dys = (TOPO > 0 && a.top.dy_scale) ? *a.top.dy_scale : 1.f;
   if constexpr (TOPO > 0) {
 #pragma unroll
     for (int o = 0; o < TOPO; ++o)
@@ -1101,7 +1105,7 @@ DEV void dx_ring_body_v1(const NTArgs& a, char* smem, const int64_t t0, const in
         const u16x8 ph = *(const u16x8*)p;
         float g[TOP_MAXO];
 #pragma unroll
-        for (int o = 0; o < TOP_MAXO; ++o) g[o] = o < TOPO ? gt[r * TOPO + o] : 0.f;
+        for (int o = 0; o < TOP_MAXO; ++o) g[o] = o < TOPO ? gt[r * TOPO + o] * dys : 0.f;
         bf16x8 v;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -1268,6 +1272,7 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
 
   // TOPO: this thread's W_L columns for the in-place dZ_top pass (chunk tid % 32 is fixed)
   float twl[TOPO > 0 ? TOPO : 1][8];
+  const float dys = (TOPO > 0 && a.top.dy_scale) ? *a.top.dy_scale : 1.f;
   if constexpr (TOPO > 0) {
 #pragma unroll
     for (int o = 0; o < TOPO; ++o)
@@ -1372,7 +1377,7 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
         const u16x8 ph = *(const u16x8*)pp;
         float gg[TOP_MAXO];
 #pragma unroll
-        for (int o = 0; o < TOP_MAXO; ++o) gg[o] = o < TOPO ? gt[r * TOPO + o] : 0.f;
+        for (int o = 0; o < TOP_MAXO; ++o) gg[o] = o < TOPO ? gt[r * TOPO + o] * dys : 0.f;
         bf16x8 v;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -1867,6 +1872,7 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
   // TOPO: W_L columns of this thread's chunk, dW_L / db_L sums
   constexpr int TO = TOPO > 0 ? TOPO : 1;
   float twl[TO][8], tdw[TO][8], tdb[TO];
+  const float dys = (TOPO > 0 && a.top.dy_scale) ? *a.top.dy_scale : 1.f;
 #pragma unroll
   for (int o = 0; o < TO; ++o) {
     tdb[o] = 0.f;
@@ -1919,7 +1925,7 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
       const u16x8 pt = *(const u16x8*)(Db + off);
       float gg[TOP_MAXO];
 #pragma unroll
-      for (int o = 0; o < TOP_MAXO; ++o) gg[o] = o < TOPO ? gt[o] : 0.f;
+      for (int o = 0; o < TOP_MAXO; ++o) gg[o] = o < TOPO ? gt[o] * dys : 0.f;
       bf16x8 dz;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {

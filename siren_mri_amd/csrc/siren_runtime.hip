@@ -512,7 +512,7 @@ int launch_nt(const NTArgs& a, int64_t nb, int kclass, hipStream_t st) {
 
 // Register-resident forward (siren_fwdreg.hip): one weight-prep launch, one forward launch.
 int fused_forward_reg(const siren_mlp_desc* d, const Geo& g, const Layout& lo, const float* x, float* y,
-                      char* saved, char* wbuf, hipStream_t st) {
+                      char* saved, char* wbuf, hipStream_t st, const siren_loss_desc* L = nullptr) {
   const int F = d->dims[1], nh = g.L - 2;
   _Float16* wreg = (_Float16*)(wbuf + lo.frag_off);
   _Float16* wlreg = wreg + g.nb * (int64_t)nh * F * F;
@@ -558,6 +558,19 @@ int fused_forward_reg(const siren_mlp_desc* d, const Geo& g, const Layout& lo, c
   a.sine_out = d->outermost_linear ? 0 : 1;
   a.cin = d->dims[0];
   a.w0 = d->w0;
+  if (L) {
+    a.ltgt = L->target;
+    a.lk0 = L->k0;
+    a.lmask = L->mask;
+    a.lhf = L->hf;
+    a.ldc = L->y_dc;
+    a.ldy = L->dy;
+    a.lloss = L->loss;
+    a.lpart = (float*)L->loss_workspace;
+    a.lcounter = (unsigned*)((char*)L->loss_workspace + SSE_MAX_BLOCKS * 4);
+    a.lnoise = L->noise;
+    a.lweight = L->weight;
+  }
   const int64_t tiles = cdiv(g.rows, FREG_WG_ROWS);
   const int64_t per = std::max<int64_t>(1, 256 / g.nb);
   dim3 grid((unsigned)std::min<int64_t>(tiles, per), (unsigned)g.nb);
@@ -569,6 +582,17 @@ int fused_forward_reg(const siren_mlp_desc* d, const Geo& g, const Layout& lo, c
   static const KernelFn wide[2][2] = {SIREN_FREG_FORMS(16, 0), SIREN_FREG_FORMS(16, 1)};
 #undef SIREN_FREG_FORMS
   const KernelFn* k = fused_wide(d) ? wide[a.O == 1 ? 1 : 0] : table[a.O == 1 ? 1 : 0][d->dims[0] - 1];
+  if (L) {  // the fused-loss forms (siren_mlp_loss_check admitted this shape)
+    static const KernelFn lnarrow[FUSED_MAXC] = {fused_fwd_reg_kernel<1, 1, 0, true>, fused_fwd_reg_kernel<2, 1, 0, true>,
+                                                 fused_fwd_reg_kernel<3, 1, 0, true>, fused_fwd_reg_kernel<4, 1, 0, true>};
+    static const KernelFn lwide[2] = {fused_fwd_reg_kernel<16, 0, 0, true>, fused_fwd_reg_kernel<16, 1, 0, true>};
+    const KernelFn kl = fused_wide(d) ? lwide[a.O == 1 ? 1 : 0] : lnarrow[d->dims[0] - 1];
+    a.wbound = nullptr;  // the fract form alone (no magic-form exit test on an unwritten bound)
+    tmark_begin(SIREN_KCLASS_FWD_FUSED, st);
+    hipLaunchKernelGGL(kl, grid, dim3(512), 0, st, a);
+    tmark_end(SIREN_KCLASS_FWD_FUSED, st);
+    return check_launch("fused_fwd_reg (loss)");
+  }
   tmark_begin(SIREN_KCLASS_FWD_FUSED, st);
   // magic form (option freg_magic): both forms are launched, the one whose form does not apply to
   // these weights exits at its start (siren_fwdreg.hip); otherwise the fract form alone
@@ -815,7 +839,8 @@ int launch_pair(const siren_mlp_desc* d, const Geo& g, const Layout& lo, int kin
 
 template <int PREC>
 int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, const char* saved,
-                  char* ws, float* const* dW, float* const* db, float* dx, hipStream_t st) {
+                  char* ws, float* const* dW, float* const* db, float* dx, hipStream_t st,
+                  const float* dy_scale = nullptr) {
   const Geo g = geo_of(d);
   const Layout lo = layout_of(d);
   int rc = SIREN_OK;
@@ -864,6 +889,7 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
     a.W = d->weight[l];
     a.b = d->bias[l];
     a.dy = dy;
+    a.dy_scale = dy_scale;
     a.dZ = ws + lo.dz_off[cur];
     a.part = part;
     a.rows_per_batch = g.rows;
@@ -886,6 +912,7 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
     const int FL = d->dims[g.L - 1];
     ta.Ptop = P(g.L - 2);
     ta.dy = dy;
+    ta.dy_scale = dy_scale;
     ta.WL = d->weight[g.L - 1];
     ta.wl_bstride = d->weights_batched ? (int64_t)O * FL : 0;
     ta.partL = (float*)(ws + lo.partL_off);
@@ -1497,6 +1524,68 @@ int siren_mlp_backward(const siren_mlp_desc* d, const float* x, const float* dy,
                                     dx, st);
   return backward_impl<kPrecF32>(d, x, dy, (const char*)saved, (char*)workspace, dweight, dbias, dx,
                                  st);
+}
+
+int siren_mlp_loss_check(const siren_mlp_desc* d, const siren_loss_desc* l) {
+  int rc = siren_mlp_check(d);
+  if (rc) return rc;
+  if (!l) return fail(SIREN_EINVAL, "null loss descriptor");
+  if (d->prec != SIREN_PREC_BF16 || !g_fused_forward || !g_fwd_reg || !fused_shape(d) || d->num_layers < 3)
+    return fail(SIREN_EINVAL, "fused loss: needs the bf16 register-resident forward's shapes");
+  if (!d->outermost_linear) return fail(SIREN_EINVAL, "fused loss: needs outermost_linear");
+  if (g_freg_magic) return fail(SIREN_EINVAL, "fused loss: not with option freg_magic");
+  const int O = d->dims[d->num_layers];
+  if (!fused_wide(d) && O != 1) return fail(SIREN_EINVAL, "fused loss: 1..4 inputs need one output");
+  if (!l->target || !l->dy || !l->loss || !l->loss_workspace)
+    return fail(SIREN_EINVAL, "fused loss: null target / dy / loss / workspace");
+  if (l->loss_workspace_bytes < siren_sse_workspace_bytes())
+    return fail(SIREN_ENOSPACE, "fused loss: workspace %lld < %lld bytes", (long long)l->loss_workspace_bytes,
+                (long long)siren_sse_workspace_bytes());
+  if ((l->k0 == nullptr) != (l->mask == nullptr) || (l->k0 == nullptr) != (l->y_dc == nullptr))
+    return fail(SIREN_EINVAL, "fused loss: k0, mask and y_dc are given together or not at all");
+  if (l->hf && l->hf_len != d->rows_per_batch)
+    return fail(SIREN_EINVAL, "fused loss: hf has %lld entries for %lld rows per weight set", (long long)l->hf_len,
+                (long long)d->rows_per_batch);
+  const Geo g = geo_of(d);
+  const int64_t wgs = std::min<int64_t>(cdiv(g.rows, FREG_WG_ROWS), std::max<int64_t>(1, 256 / g.nb)) * g.nb;
+  if (wgs > SSE_MAX_BLOCKS) return fail(SIREN_EINVAL, "fused loss: %lld workgroups > %d", (long long)wgs, SSE_MAX_BLOCKS);
+  return SIREN_OK;
+}
+
+int siren_mlp_forward_loss(const siren_mlp_desc* d, const siren_loss_desc* l, const float* x, float* y, void* saved,
+                           int64_t saved_bytes, void* workspace, int64_t workspace_bytes, void* stream) {
+  int rc = siren_mlp_loss_check(d, l);
+  if (rc) return rc;
+  const Layout lo = layout_of(d);
+  if (saved && saved_bytes < lo.saved_bytes)
+    return fail(SIREN_ENOSPACE, "saved buffer %lld < %lld bytes", (long long)saved_bytes, (long long)lo.saved_bytes);
+  if (workspace_bytes < lo.ws_bytes || !workspace)
+    return fail(SIREN_ENOSPACE, "workspace %lld < %lld bytes", (long long)workspace_bytes, (long long)lo.ws_bytes);
+  if (!x || !y) return fail(SIREN_EINVAL, "null x or y");
+  g_err.clear();
+  const Geo g = geo_of(d);
+  char* wbuf = saved ? (char*)saved : (char*)workspace;
+  return fused_forward_reg(d, g, lo, x, y, (char*)saved, wbuf, (hipStream_t)stream, l);
+}
+
+int siren_mlp_backward_ex(const siren_mlp_desc* d, const float* x, const float* dy, const float* dy_scale,
+                          const void* saved, int64_t saved_bytes, void* workspace, int64_t workspace_bytes,
+                          float* const* dweight, float* const* dbias, float* dx, void* stream) {
+  int rc = siren_mlp_check(d);
+  if (rc) return rc;
+  const Layout lo = layout_of(d);
+  if (!saved || saved_bytes < lo.saved_bytes)
+    return fail(SIREN_ENOSPACE, "saved buffer %lld < %lld bytes", (long long)saved_bytes, (long long)lo.saved_bytes);
+  if (workspace_bytes < lo.ws_bytes || !workspace)
+    return fail(SIREN_ENOSPACE, "workspace %lld < %lld bytes", (long long)workspace_bytes, (long long)lo.ws_bytes);
+  if (!x || !dy || !dweight || !dbias) return fail(SIREN_EINVAL, "null argument");
+  for (int l = 0; l < d->num_layers; ++l)
+    if (!dweight[l] || !dbias[l]) return fail(SIREN_EINVAL, "layer %d: null gradient output", l);
+  hipStream_t st = (hipStream_t)stream;
+  g_err.clear();
+  if (d->prec == SIREN_PREC_BF16)
+    return backward_impl<kPrecBF16>(d, x, dy, (const char*)saved, (char*)workspace, dweight, dbias, dx, st, dy_scale);
+  return backward_impl<kPrecF32>(d, x, dy, (const char*)saved, (char*)workspace, dweight, dbias, dx, st, dy_scale);
 }
 
 int64_t siren_jvp_saved_bytes(const siren_mlp_desc* d, int order) {

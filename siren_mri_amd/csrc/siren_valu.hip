@@ -44,6 +44,7 @@ struct LastBwdArgs {
   const float* W;      // [nb_w][O, F]
   const float* b;      // [nb_w][O]
   const float* dy;     // [rows, O]
+  const float* dy_scale;  // [1] device scalar multiplying dy (a fused loss's upstream gradient), or null
   void* dZ;            // [rows, F] grad_t
   float* part;         // split s, batch b slab at part + s*split_stride + b*(O*F + O)
   int64_t rows_per_batch;
@@ -243,6 +244,7 @@ __global__ __launch_bounds__(256) void last_bwd_kernel(LastBwdArgs a) {
   if (r_end > a.rows_per_batch) r_end = a.rows_per_batch;
   float w[IT][MAXO][8];
   float dw[IT][MAXO][8];
+  const float dys = a.dy_scale ? *a.dy_scale : 1.f;
   float db[MAXO];
 #pragma unroll
   for (int it = 0; it < IT; ++it)
@@ -269,7 +271,7 @@ __global__ __launch_bounds__(256) void last_bwd_kernel(LastBwdArgs a) {
     const int64_t row = batch * a.rows_per_batch + (r < r_end ? r : r0);
     const phase_t* pr = (const phase_t*)a.P + row * a.F;
 #pragma unroll
-    for (int o = 0; o < MAXO; ++o) gq[k][o] = (o < a.O) ? a.dy[row * a.O + o] : 0.f;
+    for (int o = 0; o < MAXO; ++o) gq[k][o] = (o < a.O) ? a.dy[row * a.O + o] * dys : 0.f;
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
       const int f = 256 * it + 8 * l32;

@@ -19,7 +19,7 @@ import torch
 import torch.nn as nn
 from torch import Tensor
 
-from . import _native
+from . import _native, fusion
 from .ops import _LIB
 
 _LIB.define("dc_forward(Tensor pred, Tensor k0, Tensor mask, float noise) -> Tensor")
@@ -97,6 +97,14 @@ class DataConsistencyInKspace(nn.Module):
     def forward(self, prediction, k0, mask):
         if _native_ok(prediction, k0, mask):
             noise = float(self.noise_lvl) if self.noise_lvl else 0.0
+            st = fusion.staged()
+            if st is not None and st.result is not None and st.result[0] is prediction and st.result[1] is not None:
+                sk0, smask, snoise = st.result[4]
+                if sk0 is k0 and smask is mask and snoise == noise:
+                    # computed by the forward's fused output epilogue (fusion.py)
+                    out = st.result[1]
+                    out._siren_dc = (prediction, k0, mask, noise)
+                    return out
             out = torch.ops.siren_mri_amd.dc_forward(prediction, k0, mask, noise)
             out._siren_dc = (prediction, k0, mask, noise)
             return out

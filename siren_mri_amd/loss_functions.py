@@ -19,12 +19,13 @@ from __future__ import annotations
 
 import torch
 
-from . import _native, diff_operators
+from . import _native, diff_operators, fusion
 from .data_consistency import dc_source
 from .dataio import lin2img
 from .utils import create_circular_mask_torch
 
 _KSPACE_WEIGHT = 1.0 / (128 * 128)
+KSPACE_WEIGHT = _KSPACE_WEIGHT  # image_mse's normalisation (loss_functions.py:101)
 _MASKS: dict = {}
 
 
@@ -39,18 +40,10 @@ def _high_freq_mask(device):
     return m
 
 
-_SSE_WS: dict = {}
-
-
 def _sse_workspace(device):
     # one workspace per (device, stream): its block sums and ticket must not be shared by two
     # launches that may run concurrently
-    key = (device, torch.cuda.current_stream(device).cuda_stream)
-    ws = _SSE_WS.get(key)
-    if ws is None:
-        ws = torch.zeros(int(_native.lib().siren_sse_workspace_bytes()), dtype=torch.uint8, device=device)
-        _SSE_WS[key] = ws
-    return ws
+    return _native.sse_workspace(device)
 
 
 class _WeightedSSE(torch.autograd.Function):
@@ -168,6 +161,25 @@ def set_kspace_fusion(enabled: bool) -> None:
     _FUSE_DC = bool(enabled)
 
 
+def high_freq_flat(device):
+    """image_mse's 128x128 high-frequency mask, flattened to the SIREN's [N] row order."""
+    return _hf_flat(device)
+
+
+def _staged_loss(out, tgt, hf_applied, weight):
+    """The forward's fused loss (fusion.py) when `out` is its output (DC(y) with data consistency),
+    `tgt` the staged target and the reduction the same; None otherwise."""
+    st = fusion.staged()
+    if st is None or st.result is None:
+        return None
+    y, y_dc, loss, st_hf, _dc = st.result
+    if out is not (y_dc if y_dc is not None else y) or tgt is not st.tgt:
+        return None
+    if bool(hf_applied) != bool(st_hf) or float(weight) != st.weight:
+        return None
+    return loss
+
+
 def _hf_flat(device):
     key = ("flat", device)
     m = _MASKS.get(key)
@@ -199,6 +211,10 @@ def weighted_sse(pred, tgt, weight=_KSPACE_WEIGHT, mask=None):
     """sum |m (pred - tgt)|^2 * weight over any shape (image_mse's reduction without the
     lin2img reshape): the loss of a coordinate shard of an image in a sharded fit, whose partial
     sums over the ranks' shards add up to image_mse of the whole image."""
+    if mask is None:
+        staged = _staged_loss(pred, tgt, False, weight)
+        if staged is not None:
+            return staged
     if pred.is_cuda and pred.dtype == torch.float32 and tgt.dtype == torch.float32 and not tgt.requires_grad:
         return _WeightedSSE.apply(pred, tgt.to(pred.device), mask, weight)
     diff = pred - tgt
@@ -211,6 +227,12 @@ def image_mse(mask, model_output, gt, high_freq=True):
     """Weighted k-space SSE: sum |m * (pred - gt)|^2 / 128^2 (a sum over the batch). On the GPU
     the native k-space op reads model_out / gt in their [B, N, C] layout (no lin2img copies); a
     model_out produced by the native DataConsistencyInKspace has the DC folded into the op."""
+    out, tgt = model_output["model_out"], gt["img"]
+    if out.dim() == 3:
+        side = int(round(out.shape[1] ** 0.5))
+        staged = _staged_loss(out, tgt, high_freq and side * side == out.shape[1] and side == 128, _KSPACE_WEIGHT)
+        if staged is not None:
+            return {"img_loss": staged}
     fused = _kspace_image_mse(model_output["model_out"], gt["img"], high_freq)
     if fused is not None:
         return {"img_loss": fused}

@@ -18,7 +18,7 @@ from collections import OrderedDict
 import torch
 from torch import nn
 
-from . import data_consistency, modules
+from . import data_consistency, fusion, modules
 
 
 def hyper_weight_init(m, in_features_main_net):
@@ -103,6 +103,10 @@ class ConvolutionalNeuralProcessImplicit2DHypernetFourierFeatures(nn.Module):
         else:
             embedding = model_input["embedding"]
         hypo_params = self.hyper_net(embedding)
+        if "img_sparse" in model_input:
+            # the planes of the DC below, for a staged fused loss (fusion.py)
+            fusion.stage_dc(model_input["img_sparse"], model_input["dc_mask"],
+                            float(self.dc.noise_lvl) if self.dc.noise_lvl else 0.0)
         out = self.hypo_net(model_input, params=hypo_params)
         model_out = out["model_out"]
         if "img_sparse" in model_input:

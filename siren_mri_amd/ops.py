@@ -31,7 +31,7 @@ from typing import List, Sequence, Tuple
 import torch
 from torch import Tensor
 
-from . import _native
+from . import _native, fusion
 
 _DEFAULT_PRECISION = "fp32"
 
@@ -141,7 +141,10 @@ _LIB = torch.library.Library("siren_mri_amd", "DEF")
 _LIB.define("sine_mlp_fwd(Tensor x, Tensor[] weights, Tensor[] biases, float w0, int prec, bool outermost_linear, "
             "bool batched, bool keep) -> (Tensor, Tensor)")
 _LIB.define("sine_mlp_bwd(Tensor dy, Tensor x, Tensor[] weights, Tensor[] biases, Tensor saved, float w0, int prec, "
-            "bool outermost_linear, bool batched, bool need_dx) -> (Tensor, Tensor[], Tensor[])")
+            "bool outermost_linear, bool batched, bool need_dx, Tensor? dy_scale=None) -> (Tensor, Tensor[], Tensor[])")
+_LIB.define("sine_mlp_fwd_loss(Tensor x, Tensor[] weights, Tensor[] biases, float w0, int prec, bool batched, "
+            "Tensor tgt, Tensor? k0, Tensor? mask, Tensor? hf, float noise, float weight) "
+            "-> (Tensor, Tensor, Tensor, Tensor, Tensor)")
 
 
 def sine_mlp_fwd(x: Tensor, weights: List[Tensor], biases: List[Tensor], w0: float, prec: int,
@@ -175,8 +178,9 @@ def _sine_mlp_fwd_fake(x, weights, biases, w0, prec, outermost_linear, batched, 
 
 def sine_mlp_bwd(dy: Tensor, x: Tensor, weights: List[Tensor], biases: List[Tensor], saved: Tensor, w0: float,
                  prec: int, outermost_linear: bool, batched: bool,
-                 need_dx: bool) -> Tuple[Tensor, List[Tensor], List[Tensor]]:
-    """siren_mlp_backward: (dx or an empty tensor, dW per layer, db per layer)."""
+                 need_dx: bool, dy_scale: Tensor | None = None) -> Tuple[Tensor, List[Tensor], List[Tensor]]:
+    """siren_mlp_backward_ex: (dx or an empty tensor, dW per layer, db per layer); dL/dy = dy times
+    the device scalar dy_scale when given (a fused loss's upstream gradient)."""
     if saved.numel() == 0:
         raise RuntimeError("siren_mri_amd: sine_mlp_bwd needs the saved buffer of a forward run with keep=True")
     geo = _geo_of(x, weights, batched)
@@ -194,15 +198,19 @@ def sine_mlp_bwd(dy: Tensor, x: Tensor, weights: List[Tensor], biases: List[Tens
     dx = torch.empty_like(xc) if need_dx else xc.new_empty((0,))
     n = len(ws)
     VP = ctypes.c_void_p * n
-    rc = _native.lib().siren_mlp_backward(ctypes.byref(desc), xc.data_ptr(), dyc.data_ptr(), saved.data_ptr(),
-                                          saved_bytes, work.data_ptr(), ws_bytes,
-                                          VP(*[t.data_ptr() for t in dW]), VP(*[t.data_ptr() for t in db]),
-                                          dx.data_ptr() if need_dx else None, _native.stream_handle(dev))
-    _native.check(rc, "siren_mlp_backward")
+    sc = None
+    if dy_scale is not None:
+        sc = dy_scale.detach().reshape(()).to(device=dev, dtype=torch.float32).contiguous()
+    rc = _native.lib().siren_mlp_backward_ex(ctypes.byref(desc), xc.data_ptr(), dyc.data_ptr(),
+                                             sc.data_ptr() if sc is not None else None, saved.data_ptr(),
+                                             saved_bytes, work.data_ptr(), ws_bytes,
+                                             VP(*[t.data_ptr() for t in dW]), VP(*[t.data_ptr() for t in db]),
+                                             dx.data_ptr() if need_dx else None, _native.stream_handle(dev))
+    _native.check(rc, "siren_mlp_backward_ex")
     return dx, dW, db
 
 
-def _sine_mlp_bwd_fake(dy, x, weights, biases, saved, w0, prec, outermost_linear, batched, need_dx):
+def _sine_mlp_bwd_fake(dy, x, weights, biases, saved, w0, prec, outermost_linear, batched, need_dx, dy_scale=None):
     return (torch.empty_like(x) if need_dx else x.new_empty((0,)),
             [torch.empty_like(w) for w in weights], [torch.empty_like(b) for b in biases])
 
@@ -285,6 +293,167 @@ torch.library.register_fake("siren_mri_amd::sine_mlp_fwd", _sine_mlp_fwd_fake, l
 torch.library.register_fake("siren_mri_amd::sine_mlp_bwd", _sine_mlp_bwd_fake, lib=_LIB)
 
 
+# ---------------------------------------------------------------- forward with the fused image loss
+def _loss_desc(tgt, k0, mask, hf, noise, weight, y_dc, dy, loss, lws):
+    ld = _native.SirenLossDesc()
+    ld.target = tgt.data_ptr()
+    ld.k0 = k0.data_ptr() if k0 is not None else None
+    ld.mask = mask.data_ptr() if mask is not None else None
+    ld.hf = hf.data_ptr() if hf is not None else None
+    ld.hf_len = hf.numel() if hf is not None else 0
+    ld.noise = float(noise)
+    ld.weight = float(weight)
+    ld.y_dc = y_dc.data_ptr() if (k0 is not None and y_dc is not None) else None
+    ld.dy = dy.data_ptr()
+    ld.loss = loss.data_ptr()
+    ld.loss_workspace = lws.data_ptr()
+    ld.loss_workspace_bytes = lws.numel()
+    return ld
+
+
+_LOSS_OK = {}
+
+
+def fused_loss_supported(geo: _Geometry, prec: int, has_dc: bool, hf_len: int) -> bool:
+    """siren_mlp_loss_check for a geometry (cached; pointer-free descriptors)."""
+    key = (tuple(geo.dims), geo.batch, geo.rows, geo.batched, prec, has_dc, hf_len, _native.options_epoch())
+    hit = _LOSS_OK.get(key)
+    if hit is None:
+        d = _native.describe_only(geo.dims, prec=prec, weights_batched=geo.batched, batch=geo.batch,
+                                  rows_per_batch=geo.rows)
+        ld = _native.SirenLossDesc()
+        ld.target = ld.dy = ld.loss = ld.loss_workspace = 256
+        if has_dc:
+            ld.k0 = ld.mask = ld.y_dc = 256
+        if hf_len:
+            ld.hf, ld.hf_len = 256, hf_len
+        ld.loss_workspace_bytes = int(_native.lib().siren_sse_workspace_bytes())
+        hit = _native.lib().siren_mlp_loss_check(ctypes.byref(d), ctypes.byref(ld)) == 0
+        if len(_LOSS_OK) > 256:
+            _LOSS_OK.clear()
+        _LOSS_OK[key] = hit
+    return hit
+
+
+def sine_mlp_fwd_loss(x: Tensor, weights: List[Tensor], biases: List[Tensor], w0: float, prec: int, batched: bool,
+                      tgt: Tensor, k0: Tensor | None, mask: Tensor | None, hf: Tensor | None, noise: float,
+                      weight: float):
+    """siren_mlp_forward_loss: (y, DC(y) or an empty tensor, loss, dL/dy for a unit upstream
+    gradient, saved)."""
+    _require_device(x)
+    geo = _geo_of(x, weights, batched)
+    ws = [w.contiguous() for w in weights]
+    bs = [b.contiguous() for b in biases]
+    xc = x.contiguous()
+    dev = x.device
+    desc = _native.make_desc(geo.dims, ws, bs, w0=w0, prec=prec, outermost_linear=True,
+                             weights_batched=geo.batched, batch=geo.batch, rows_per_batch=geo.rows)
+    saved_bytes, ws_bytes = _sizes(geo, prec, True)
+    saved = torch.empty(saved_bytes, dtype=torch.uint8, device=dev)
+    work = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    shape = geo.lead_shape + (geo.dims[-1],)
+    y = torch.empty(shape, dtype=torch.float32, device=dev)
+    y_dc = torch.empty(shape, dtype=torch.float32, device=dev) if k0 is not None else y.new_empty((0,))
+    dy = torch.empty(shape, dtype=torch.float32, device=dev)
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    tc = tgt.contiguous()
+    kc = k0.contiguous() if k0 is not None else None
+    mc = mask.contiguous() if mask is not None else None
+    hc = hf.contiguous() if hf is not None else None
+    ld = _loss_desc(tc, kc, mc, hc, noise, weight, y_dc, dy, loss, _native.sse_workspace(dev))
+    rc = _native.lib().siren_mlp_forward_loss(ctypes.byref(desc), ctypes.byref(ld), xc.data_ptr(), y.data_ptr(),
+                                              saved.data_ptr(), saved_bytes, work.data_ptr(), ws_bytes,
+                                              _native.stream_handle(dev))
+    _native.check(rc, "siren_mlp_forward_loss")
+    return y, y_dc, loss, dy, saved
+
+
+def _sine_mlp_fwd_loss_fake(x, weights, biases, w0, prec, batched, tgt, k0, mask, hf, noise, weight):
+    geo = _geo_of(x, weights, batched)
+    saved_bytes, _ = _sizes(geo, prec, True)
+    shape = geo.lead_shape + (geo.dims[-1],)
+    y = x.new_empty(shape, dtype=torch.float32)
+    return (y, x.new_empty(shape if k0 is not None else (0,), dtype=torch.float32), x.new_empty((), dtype=torch.float32),
+            x.new_empty(shape, dtype=torch.float32), x.new_empty((saved_bytes,), dtype=torch.uint8))
+
+
+class _SineMLPLossAutograd(torch.autograd.Function):
+    """One autograd node for the forward with the fused image loss: outputs (y, DC(y), loss). Its
+    backward forms dL/dy = dL/dloss * dy_unit (+ the gradients arriving at y and DC(y), if any) and
+    runs the native backward; with only the loss's gradient, dL/dloss goes to the output-layer
+    kernels as a device scalar (no dL/dy tensor, no extra launch)."""
+
+    @staticmethod
+    def forward(ctx, meta, x, tgt, k0, mask, hf, *params):
+        w0, prec, batched, n, noise, weight = meta
+        with torch._C._AutoDispatchBelowAutograd():
+            y, y_dc, loss, dyu, saved = torch.ops.siren_mri_amd.sine_mlp_fwd_loss(
+                x, list(params[:n]), list(params[n:]), w0, prec, batched, tgt, k0, mask, hf, noise, weight)
+        ctx.meta = meta
+        ctx.has_dc = k0 is not None
+        ctx.save_for_backward(x, saved, dyu, mask, *params)
+        ctx.set_materialize_grads(False)
+        return y, y_dc, loss
+
+    @staticmethod
+    def backward(ctx, gy, gdc, gloss):
+        w0, prec, batched, n, noise, weight = ctx.meta
+        t = ctx.saved_tensors
+        x, saved, dyu, mask, ws, bs = t[0], t[1], t[2], t[3], list(t[4:4 + n]), list(t[4 + n:])
+        if torch.is_grad_enabled():
+            raise RuntimeError("siren_mri_amd: double backward through a fused SIREN loss is not provided; "
+                               "run it unfused (siren_mri_amd.fusion.set_enabled(False))")
+        parts = []
+        if gy is not None:
+            parts.append(gy)
+        if gdc is not None and ctx.has_dc:
+            parts.append(torch.ops.siren_mri_amd.dc_backward(gdc, mask, noise))
+        scale = None
+        if gloss is not None and not parts:
+            dy, scale = dyu, gloss
+        elif parts:
+            dy = parts[0] if len(parts) == 1 else sum(parts)
+            if gloss is not None:
+                dy = dy + dyu * gloss
+        else:
+            return (None,) * (6 + 2 * n)
+        need_dx = ctx.needs_input_grad[1]
+        dx, dW, db = torch.ops.siren_mri_amd.sine_mlp_bwd(dy, x, ws, bs, saved, w0, prec, True, batched, need_dx,
+                                                          scale)
+        return (None, dx if need_dx else None, None, None, None, None, *dW, *db)
+
+
+def _fused_loss_forward(st, x, ws, bs, w0, prec, geo):
+    """The staged image loss (fusion.py) on this SIREN forward, or None when it does not apply."""
+    from . import loss_functions
+    O = geo.dims[-1]
+    shape = geo.lead_shape + (O,)
+    tgt = st.tgt
+    if tuple(tgt.shape) != tuple(shape) or tgt.device != x.device:
+        return None
+    side = int(round(geo.rows ** 0.5))
+    hf = loss_functions.high_freq_flat(x.device) if (st.high_freq and side * side == geo.rows and side == 128) else None
+    k0 = mask = None
+    noise = 0.0
+    if st.dc is not None:
+        k0, mask, noise = st.dc
+        if not (isinstance(k0, Tensor) and isinstance(mask, Tensor) and k0.is_cuda and k0.dtype == torch.float32
+                and mask.dtype == torch.float32 and k0.dim() == 4 and k0.shape == mask.shape
+                and k0.shape[0] == geo.batch and k0.shape[1] == O and k0[0, 0].numel() == geo.rows
+                and not k0.requires_grad and not mask.requires_grad):
+            k0 = mask = None
+    if not fused_loss_supported(geo, prec, k0 is not None, hf.numel() if hf is not None else 0):
+        return None
+    meta = (float(w0), prec, geo.batched, len(ws), float(noise), float(st.weight))
+    y, y_dc, loss = _SineMLPLossAutograd.apply(meta, x, tgt, k0, mask, hf, *ws, *bs)
+    st.result = (y, y_dc if k0 is not None else None, loss, hf is not None, (k0, mask, noise) if k0 is not None else None)
+    return y
+
+
+_LIB.impl("sine_mlp_fwd_loss", sine_mlp_fwd_loss, "CUDA")
+torch.library.register_fake("siren_mri_amd::sine_mlp_fwd_loss", _sine_mlp_fwd_loss_fake, lib=_LIB)
+
+
 def siren_mlp(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[torch.Tensor], *,
               w0: float = 30.0, precision: str | None = None, outermost_linear: bool = True,
               return_saved: bool = False):
@@ -300,6 +469,11 @@ def siren_mlp(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence
     if geo.squeeze_w:
         ws, bs = [w[0] for w in ws], [b[0] for b in bs]
     keep = torch.is_grad_enabled() and (x.requires_grad or any(t.requires_grad for t in ws + bs))
+    st = fusion.pending()
+    if st is not None and keep and outermost_linear and not return_saved and prec == _native.PREC_BF16:
+        y = _fused_loss_forward(st, x, ws, bs, w0, prec, geo)
+        if y is not None:
+            return y
     y, saved = torch.ops.siren_mri_amd.sine_mlp_fwd(x, ws, bs, float(w0), prec, bool(outermost_linear),
                                                     geo.batched, keep)
     return (y, saved) if return_saved else y

@@ -30,7 +30,7 @@ import time
 import numpy as np
 import torch
 
-from . import utils
+from . import fusion, utils
 
 
 class _NullWriter:
@@ -139,8 +139,15 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
             if fourier_feat_transformer is not None:
                 model_input["coords"] = fourier_feat_transformer(model_input["coords"])
 
-            model_output = model(model_input)
-            losses = loss_fn(model_output, gt)
+            # image_mse's target, staged for the SIREN forward's fused loss epilogue (fusion.py:
+            # one launch for forward + data consistency + loss; the losses pick its result up)
+            if "img" in gt:
+                fusion.stage_image_loss(gt["img"])
+            try:
+                model_output = model(model_input)
+                losses = loss_fn(model_output, gt)
+            finally:
+                fusion.clear()
             train_loss = compute_loss(losses, loss_schedules, total_steps, writer)
             train_losses_dev.append(train_loss.detach().reshape(()))
             summary_step = not total_steps % steps_til_summary

@@ -204,3 +204,28 @@ def test_checkpoint_compat_ddp_prefix_and_b_files(tmp_path):
     ft2 = features.GaussianFourierFeatureTransform(2, mapping_size_spatial=8, scale=21)
     checkpoints.load_b_matrix(ft2, str(tmp_path / "run"), 3)
     assert torch.equal(ft2.get_B(), ft.get_B())
+
+
+def test_fusion_staging_rules():
+    """fusion.py: only a CUDA fp32 target without grad is staged; set_enabled(False) clears and
+    refuses; pending() is the record until the forward stores its result; clear() ends the step."""
+    from siren_mri_amd import fusion
+    fusion.clear()
+    assert fusion.stage_image_loss(torch.zeros(1, 4, 1)) is None and fusion.staged() is None
+    # a CUDA-looking record is built by hand on CPU (the rules, not the kernel)
+    st = fusion.Staged(torch.zeros(1), True, 0.5)
+    fusion._STAGED[0] = st
+    assert fusion.pending() is st
+    fusion.stage_dc("k0", "mask", 0.25)
+    assert st.dc == ("k0", "mask", 0.25)
+    st.result = ("y", None, "loss", False, None)
+    assert fusion.pending() is None and fusion.staged() is st
+    fusion.stage_dc("k1", "m1", 0.0)  # after the forward: no effect
+    assert st.dc == ("k0", "mask", 0.25)
+    fusion.set_enabled(False)
+    try:
+        assert fusion.staged() is None and not fusion.enabled()
+    finally:
+        fusion.set_enabled(True)
+    fusion.clear()
+    assert fusion.staged() is None

@@ -61,7 +61,7 @@ def test_no_store_data_rewritten_inside_the_measured_window(disassembly):
 
 def test_forward_stores_carry_their_wait_states(disassembly):
     """The register-resident forward's phase-code and y stores are asm stores followed by s_nop 1
-    (siren_common.h store_b128_ws2 / store_b32_ws2): checked on the disassembly of all 20 forms."""
+    (siren_common.h store_b128_ws2 / store_b32_ws2): checked on the disassembly of all 26 forms."""
     import re
     forms = 0
     for dis in disassembly:
@@ -72,4 +72,4 @@ def test_forward_stores_carry_their_wait_states(disassembly):
             for i, ln in enumerate(lines):
                 if ln.startswith("buffer_store"):
                     assert lines[i + 1].startswith("s_nop 1"), (m.group(1), ln, lines[i + 1])
-    assert forms == 20  # 5 input forms x 2 output classes x 2 epilogue forms
+    assert forms == 26  # 5 input forms x 2 output classes x 2 epilogue forms + 6 fused-loss forms

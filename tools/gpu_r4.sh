@@ -17,6 +17,11 @@ for st in "$@"; do
     new)
       timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
         tests/test_gpu_sincos.py tests/test_gpu_jvp.py tests/test_gpu_ddp2.py -s > $out/new_tests.txt 2>&1 || exit $? ;;
+    floss)
+      timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+        tests/test_gpu_fused_loss.py tests/test_gpu_kspace.py tests/test_gpu_loss.py tests/test_gpu_modules.py -s > $out/floss_tests.txt 2>&1 || exit $? ;;
+    c4)
+      timeout -k 10 300 python -u bench.py --config c4 --no-cpu-baseline --no-psnr --no-other-configs > $out/c4.json 2> $out/c4.err || exit $? ;;
     all)
       timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > $out/all_tests.txt 2>&1 || exit $? ;;
     bench)
