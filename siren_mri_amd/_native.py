@@ -45,6 +45,12 @@ EXPORTED_SYMBOLS = (
     "siren_adam_step",
     "siren_adam_scalars",
     "siren_sse_workspace_bytes",
+    "siren_enc_workspace_bytes",
+    "siren_enc_relu_bwd",
+    "siren_enc_res_fwd",
+    "siren_enc_res_bwd",
+    "siren_enc_pixfc_fwd",
+    "siren_enc_pixfc_bwd",
     "siren_sse_forward",
     "siren_sse_backward",
     "siren_dc_forward",
@@ -133,6 +139,9 @@ class SirenAdamDesc(ctypes.Structure):
         ("exp_avg", ctypes.c_void_p * ADAM_MAX_TENSORS),
         ("exp_avg_sq", ctypes.c_void_p * ADAM_MAX_TENSORS),
         ("dev_scalars", ctypes.c_void_p),
+        ("dev_step", ctypes.c_void_p),
+        ("dev_table", ctypes.c_void_p),
+        ("table_n", ctypes.c_int64),
     ]
 
 
@@ -194,6 +203,18 @@ def _declare(lib):
     lib.siren_adam_scalars.restype = ctypes.c_int
     lib.siren_sse_workspace_bytes.argtypes = []
     lib.siren_sse_workspace_bytes.restype = i64
+    lib.siren_enc_workspace_bytes.argtypes = []
+    lib.siren_enc_workspace_bytes.restype = i64
+    lib.siren_enc_relu_bwd.argtypes = [vp, vp, vp, vp, vp, i64, ci, vp, i64, vp]
+    lib.siren_enc_relu_bwd.restype = ci
+    lib.siren_enc_res_fwd.argtypes = [vp, vp, vp, i64, ci, vp]
+    lib.siren_enc_res_fwd.restype = ci
+    lib.siren_enc_res_bwd.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, ci, vp, i64, vp]
+    lib.siren_enc_res_bwd.restype = ci
+    lib.siren_enc_pixfc_fwd.argtypes = [vp, vp, vp, vp, ci, i64, ci, vp, i64, vp]
+    lib.siren_enc_pixfc_fwd.restype = ci
+    lib.siren_enc_pixfc_bwd.argtypes = [vp, vp, vp, vp, vp, vp, ci, i64, ci, vp, i64, vp]
+    lib.siren_enc_pixfc_bwd.restype = ci
     lib.siren_sse_forward.argtypes = [vp, vp, vp, i64, i64, f32, vp, vp, vp, i64, vp]
     lib.siren_sse_forward.restype = ctypes.c_int
     lib.siren_sse_backward.argtypes = [vp, vp, i64, i64, vp, f32, vp, vp]
@@ -296,6 +317,20 @@ def sse_workspace(device) -> torch.Tensor:
     if ws is None:
         ws = torch.zeros(int(lib().siren_sse_workspace_bytes()), dtype=torch.uint8, device=device)
         _SSE_WS[key] = ws
+    return ws
+
+
+_ENC_WS: dict = {}
+
+
+def enc_workspace(device) -> torch.Tensor:
+    """Per-(device, stream) workspace of the encoder passes' channel sums (siren_enc_workspace_bytes;
+    zeroed once, left zeroed by every launch)."""
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    ws = _ENC_WS.get(key)
+    if ws is None:
+        ws = torch.zeros(int(lib().siren_enc_workspace_bytes()), dtype=torch.uint8, device=device)
+        _ENC_WS[key] = ws
     return ws
 
 

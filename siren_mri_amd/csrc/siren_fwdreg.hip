@@ -174,10 +174,6 @@ DEV constexpr int freg_in0(int ks, int h) { return 32 * (ks >> 1) + 16 * (ks & 1
 #ifndef SIREN_FREG_STORE_WS2
 #define SIREN_FREG_STORE_WS2 1
 #endif
-// LOSS forms: 1 = the output layer loads its rows' targets before its MFMAs (latency hidden)
-#ifndef SIREN_FREG_LOSS_PREFETCH
-#define SIREN_FREG_LOSS_PREFETCH 1
-#endif
 #ifndef SIREN_FREG_WAITAT
 #if SIREN_FREG_STORE_WS2
 #define SIREN_FREG_WAITAT -1
@@ -645,22 +641,6 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   // output layer: y = H W_L^T + b_L (MFMA rows = outputs), beside the last hidden block's epilogue
   auto output_layer = [&](h16x8 (&Hin)[NKS], auto mtag) __attribute__((always_inline)) {
     if constexpr (WIDE) load_xw(tcur + G);  // the next round's inputs
-    // LOSS: this lane's targets (and high-frequency weight) are loaded before the output layer's
-    // MFMAs, so their latency hides behind them instead of following the y stores
-    constexpr int NE = OC == 1 ? 1 : 4;
-    float ltv[NE];
-    float lhv = 1.f;
-    if constexpr (LOSS && SIREN_FREG_LOSS_PREFETCH) {
-      const int64_t r0 = tcur * FREG_WG_ROWS;
-      const int yrow = wave * FREG_WROWS + j;
-      const bool live = r0 + yrow < rows;
-#pragma unroll
-      for (int e = 0; e < NE; ++e) {
-        const int o = 4 * hh + e;
-        ltv[e] = (live && o < O) ? a.ltgt[(batch * rows + r0 + yrow) * O + o] : 0.f;
-      }
-      if (a.lhf && live) lhv = a.lhf[r0 + yrow];
-    }
     f32x16 accO = accNx;
     Epi ep;
     const uint32_t va_nxt = slot_va(0);  // the next round's first block
@@ -696,7 +676,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
         store_complete(zb);
 #endif
         if constexpr (LOSS) {
-          if (yrow < nv && e < NE) {
+          if (yrow < nv) {
             const int o = 4 * hh + e;
             const int64_t n = r0 + yrow;                    // the row within its weight set
             const int64_t q = (batch * rows + n) * O + o;   // [B*N, O] element
@@ -709,13 +689,8 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
               coef = dc_coef(m, a.lnoise);
               a.ldc[q] = p;
             }
-#if SIREN_FREG_LOSS_PREFETCH
-            const float h = lhv;
-            const float t = ltv[e < NE ? e : 0];
-#else
             const float h = a.lhf ? a.lhf[n] : 1.f;
             const float t = a.ltgt[q];
-#endif
             const float dd = __fmul_rn(h, __fsub_rn(p, t));
             lsum = fmaf(dd, dd, lsum);
             float v = h * (dd * (2.f * a.lweight));

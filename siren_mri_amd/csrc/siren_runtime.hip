@@ -17,6 +17,7 @@
 #include "siren_adam.hip"
 #include "siren_loss.hip"
 #include "siren_kspace.hip"
+#include "siren_encoder.hip"
 
 using namespace siren;
 
@@ -174,9 +175,11 @@ int64_t split_stride(const Geo& g, int64_t slab) { return align_up(g.nb * slab, 
 
 // pair_ring_bf16_kernel: npair input-gradient / weight-gradient workgroup pairs per weight set
 // (a multiple of 8, so the grid is a multiple of 16 and every pair shares an XCD); with nb <= 16
-// weight sets all 2 * npair * nb workgroups are resident together (one per CU).
+// weight sets all 2 * npair * nb workgroups are resident together (one per CU). Past that (configs
+// 4/5: 32 slices, 512 workgroups) the two workgroups of a pair are still dispatched next to each
+// other (speed only; correctness never depends on residency).
 constexpr int64_t kMaxPairs = 128;
-bool pair_ok(const Geo& g) { return g.nb <= 16; }
+bool pair_ok(const Geo& g) { return g.nb <= 64; }
 int64_t pair_count(const Geo& g) {
   const int64_t ntiles = cdiv(g.rows, 32);
   const int64_t np = std::max<int64_t>(8, (kMaxPairs / g.nb) / 8 * 8);
@@ -434,9 +437,18 @@ int dispatch_first_bwd(const FirstBwdArgs& a, int64_t nsplit, int64_t nb, hipStr
     if (it == 1) hipLaunchKernelGGL((first_bwd_kernel<PREC, 1, 4>), grid, dim3(256), 0, st, a);
     else if (it == 2) hipLaunchKernelGGL((first_bwd_kernel<PREC, 2, 4>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((first_bwd_kernel<PREC, 4, 4>), grid, dim3(256), 0, st, a);
-  } else if (!a.dx && a.F <= 256) {
-    if (a.C == 16) hipLaunchKernelGGL((first_bwd_wide_kernel<PREC, 16>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((first_bwd_wide_kernel<PREC, 0>), grid, dim3(256), 0, st, a);
+  } else if (a.F <= 256 && (!a.dx || (PREC == kPrecBF16 && a.F == 256))) {
+    // weight gradient without dx; the input gradient (bf16 mode) as its own MFMA launch
+    FirstBwdArgs aw = a;
+    aw.dx = nullptr;
+    if (a.C == 16) hipLaunchKernelGGL((first_bwd_wide_kernel<PREC, 16>), grid, dim3(256), 0, st, aw);
+    else hipLaunchKernelGGL((first_bwd_wide_kernel<PREC, 0>), grid, dim3(256), 0, st, aw);
+    if (a.dx) {
+      int rc = check_launch("first_bwd_wide");
+      if (rc) return rc;
+      const int64_t ntile = cdiv(a.rows_per_batch, 32);
+      hipLaunchKernelGGL(first_dx_wide_kernel, dim3((unsigned)cdiv(ntile, 4), (unsigned)nb), dim3(256), 0, st, a);
+    }
   } else {
     if (it == 1) hipLaunchKernelGGL((first_bwd_kernel<PREC, 1, 16>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((first_bwd_kernel<PREC, 2, 16>), grid, dim3(256), 0, st, a);
@@ -1689,6 +1701,115 @@ int siren_adam_scalars(double* t, double lr, double beta1, double beta2, float* 
 
 int64_t siren_sse_workspace_bytes(void) { return (int64_t)SSE_MAX_BLOCKS * 4 + 256; }
 
+// ---------------------------------------------------------------- conv encoder epilogues
+int64_t siren_enc_workspace_bytes(void) { return ENC_WS_FLOATS * 4 + 256; }
+
+namespace {
+// shared checks; fills the plane geometry and the block split of a [P, C] pass
+int enc_setup(EncArgs& a, int64_t P, int C, void* ws, int64_t ws_bytes, bool need_ws, int64_t rows_per_block_min,
+              const char* what) {
+  memset(&a, 0, sizeof(a));
+  if (P < 0 || C < 8 || C > ENC_MAXC || (C & (C - 1)) != 0)
+    return fail(SIREN_EINVAL, "%s: C = %d must be a power of two in [8, %d] (P = %lld)", what, C, ENC_MAXC, (long long)P);
+  if (need_ws && (!ws || ws_bytes < siren_enc_workspace_bytes()))
+    return fail(SIREN_ENOSPACE, "%s: workspace %lld < %lld bytes", what, (long long)ws_bytes,
+                (long long)siren_enc_workspace_bytes());
+  a.P = P;
+  a.C = C;
+  a.part = (float*)ws;
+  a.ticket = ws ? (unsigned*)((char*)ws + ENC_WS_FLOATS * 4) : nullptr;
+  const int ppi = 256 / (C / 8);
+  int64_t nblk = std::min<int64_t>(ENC_MAX_BLOCKS, std::max<int64_t>(1, cdiv(P, rows_per_block_min)));
+  a.chunk = align_up(cdiv(std::max<int64_t>(P, 1), nblk), ppi);
+  return SIREN_OK;
+}
+}  // namespace
+
+int siren_enc_relu_bwd(const void* g1, const void* g2, const void* y, void* out, float* db, int64_t P, int C, void* ws,
+                       int64_t ws_bytes, void* stream) {
+  EncArgs a;
+  int rc = enc_setup(a, P, C, ws, ws_bytes, db != nullptr, 512, "enc_relu_bwd");
+  if (rc) return rc;
+  if (!g1 || !y || !out) return fail(SIREN_EINVAL, "enc_relu_bwd: null plane");
+  if (P == 0) return SIREN_OK;
+  a.g1 = (const bf16*)g1;
+  a.g2 = (const bf16*)g2;
+  a.y = (const bf16*)y;
+  a.out = (bf16*)out;
+  a.db = db;
+  hipLaunchKernelGGL(enc_relu_bwd_kernel, dim3((unsigned)cdiv(P, a.chunk)), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("enc_relu_bwd");
+}
+
+int siren_enc_res_fwd(const void* a_pre, const void* x, void* out, int64_t P, int C, void* stream) {
+  EncArgs a;
+  int rc = enc_setup(a, P, C, nullptr, 0, false, 512, "enc_res_fwd");
+  if (rc) return rc;
+  if (!a_pre || !x || !out) return fail(SIREN_EINVAL, "enc_res_fwd: null plane");
+  if (P == 0) return SIREN_OK;
+  a.a = (const bf16*)a_pre;
+  a.g1 = (const bf16*)x;
+  a.out = (bf16*)out;
+  hipLaunchKernelGGL(enc_res_fwd_kernel, dim3((unsigned)std::min<int64_t>(cdiv(P * C / 8, 256), 8192)), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  return check_launch("enc_res_fwd");
+}
+
+int siren_enc_res_bwd(const void* g1, const void* g2, const void* out, const void* a_pre, void* gskip, void* ga,
+                      float* db, int64_t P, int C, void* ws, int64_t ws_bytes, void* stream) {
+  EncArgs a;
+  int rc = enc_setup(a, P, C, ws, ws_bytes, db != nullptr, 512, "enc_res_bwd");
+  if (rc) return rc;
+  if (!g1 || !out || !a_pre || !gskip || !ga) return fail(SIREN_EINVAL, "enc_res_bwd: null plane");
+  if (P == 0) return SIREN_OK;
+  a.g1 = (const bf16*)g1;
+  a.g2 = (const bf16*)g2;
+  a.y = (const bf16*)out;
+  a.a = (const bf16*)a_pre;
+  a.out = (bf16*)gskip;
+  a.out2 = (bf16*)ga;
+  a.db = db;
+  hipLaunchKernelGGL(enc_res_bwd_kernel, dim3((unsigned)cdiv(P, a.chunk)), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("enc_res_bwd");
+}
+
+int siren_enc_pixfc_fwd(const void* a_pre, const float* w, const float* bias, float* e, int B, int64_t P, int C,
+                        void* ws, int64_t ws_bytes, void* stream) {
+  EncArgs a;
+  int rc = enc_setup(a, P, C, ws, ws_bytes, true, 512, "enc_pixfc_fwd");
+  if (rc) return rc;
+  if (!a_pre || !w || !bias || !e || B < 1) return fail(SIREN_EINVAL, "enc_pixfc_fwd: null pointer or B < 1");
+  const int64_t nchunk = cdiv(P, a.chunk);
+  if (nchunk * B > ENC_MAX_BLOCKS || (int64_t)B * C > ENC_WS_FLOATS)
+    return fail(SIREN_EINVAL, "enc_pixfc_fwd: %lld blocks > %d", (long long)(nchunk * B), ENC_MAX_BLOCKS);
+  if (P == 0) return fail(SIREN_EINVAL, "enc_pixfc_fwd: no pixels");
+  a.a = (const bf16*)a_pre;
+  a.w = w;
+  a.bias = bias;
+  a.e = e;
+  a.B = B;
+  hipLaunchKernelGGL(enc_pixfc_fwd_kernel, dim3((unsigned)nchunk, (unsigned)B), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("enc_pixfc_fwd");
+}
+
+int siren_enc_pixfc_bwd(const float* g, const void* a_pre, const float* w, void* ga, float* db, float* gw, int B,
+                        int64_t P, int C, void* ws, int64_t ws_bytes, void* stream) {
+  EncArgs a;
+  int rc = enc_setup(a, P, C, ws, ws_bytes, true, 64, "enc_pixfc_bwd");
+  if (rc) return rc;
+  if (!g || !a_pre || !w || !ga || !db || !gw || B < 1) return fail(SIREN_EINVAL, "enc_pixfc_bwd: null pointer or B < 1");
+  if (P == 0) return fail(SIREN_EINVAL, "enc_pixfc_bwd: no pixels");
+  a.gin = g;
+  a.a = (const bf16*)a_pre;
+  a.w = w;
+  a.out = (bf16*)ga;
+  a.db = db;
+  a.e = gw;
+  a.B = B;
+  hipLaunchKernelGGL(enc_pixfc_bwd_kernel, dim3((unsigned)cdiv(P, a.chunk)), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("enc_pixfc_bwd");
+}
+
 int siren_sse_forward(const float* pred, const float* tgt, const float* mask, int64_t n, int64_t mask_n,
                       float weight, float* d, float* loss, void* workspace, int64_t ws_bytes, void* stream) {
   if (n < 0 || !loss || (n > 0 && (!pred || !tgt || !d)) || (mask && mask_n <= 0))
@@ -1828,6 +1949,11 @@ int siren_adam_step(const siren_adam_desc* d, void* stream) {
   a.step = d->step_size;
   a.bc2_sqrt = d->bias_correction2_sqrt;
   a.dev = d->dev_scalars;
+  a.tstep = d->dev_step;
+  if (d->dev_step && (!d->dev_table || d->table_n < 1))
+    return fail(SIREN_EINVAL, "adam: dev_step needs dev_table with table_n >= 1");
+  a.table = d->dev_table;
+  a.table_n = d->table_n;
   a.maximize = d->maximize;
   if (maxn == 0) return SIREN_OK;
   hipLaunchKernelGGL(adam_kernel, dim3(grid1d(maxn, 1024), (unsigned)d->num_tensors), dim3(256), 0,

@@ -532,6 +532,58 @@ __global__ __launch_bounds__(256) void first_bwd_wide_kernel(FirstBwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// first_dx_wide (bf16 mode, F = 256, 5..16 inputs): the wide first layer's input gradient
+// dx = dZ_0 W_0 ([rows, 256] x [256, C]) on the bf16 MFMA, beside first_bwd_wide_kernel (which has
+// no input gradient). Per wave, 32-row tiles: the A operand is the tile's dZ_0 rows straight from
+// HBM (16-byte loads), the B operand W_0 split into bf16 hi (columns 0..15) and lo (16..31) parts
+// held in registers, so acc[:, c] + acc[:, 16 + c] is dZ_0 W_0 to ~2^-16 of W_0 (the precision of
+// the bottom pair's dx, dx_ring_body_v2bot). The hi and lo halves meet in lanes n and n + 16.
+// (first_bwd_kernel's 64 lanes per row took ~1.4 ms of the C4 step for this product.)
+__global__ __launch_bounds__(256) void first_dx_wide_kernel(FirstBwdArgs a) {
+  constexpr int F = 256, NKS = F / 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 31, kh = lane >> 5;
+  const int64_t batch = blockIdx.y;
+  const int C = a.C;
+  // B fragments: lane (n, kh) holds B[16 ks + 8 kh + e][n], B = [W_0 hi | W_0 lo] (K = features)
+  const float* W = a.W + batch * a.w_bstride;
+  bf16x8 wb[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int f = 16 * ks + 8 * kh + e, c = n & 15;
+      const float w = c < C ? W[f * C + c] : 0.f;
+      const bf16 hi = (bf16)w;
+      wb[ks][e] = n < 16 ? hi : (bf16)(w - (float)hi);
+    }
+  const int64_t rows = a.rows_per_batch;
+  const bf16* dz = (const bf16*)a.dZ + batch * rows * F;
+  float* dx = a.dx + batch * rows * C;
+  const int64_t ntile = (rows + 31) / 32;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < ntile; t += (int64_t)gridDim.x * 4) {
+    const int64_t r0 = t * 32;
+    const int64_t ra = r0 + n < rows ? r0 + n : rows - 1;
+    const bf16* src = dz + ra * F + 8 * kh;
+    bf16x8 av[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) av[ks] = *(const bf16x8*)(src + 16 * ks);
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[ks], wb[ks], acc, 0, 0, 0);
+    // acc[e] = C[i][n], i = (e & 3) + 8 (e >> 2) + 4 kh; column n < 16: hi part, n + 16: lo part
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const float lo = __shfl_xor(acc[e], 16, 32);
+      const int64_t r = r0 + (e & 3) + 8 * (e >> 2) + 4 * kh;
+      if (n < C && r < rows) dx[r * C + n] = acc[e] + lo;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // reduce: out[e] = sum_s part[s * split_stride + e] for e < total (= nb * slab). Element e of
 // batch slab b goes to out0[b*n_first + r] (r < n_first) or out1[b*(slab-n_first) + r-n_first].
 // Block = 32 float4 columns x 8 split lanes; split_stride % 4 == 0.

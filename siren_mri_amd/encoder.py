@@ -1,0 +1,216 @@
+"""bf16 forward and backward of ConvImgEncoder (modules.py:340-380, Conv2dResBlock modules.py:433-450)
+as ONE autograd node (configs 4/5).
+
+The reference's autograd chain runs, around each convolution, a ReLU, its mask in the backward, a
+bias-gradient reduction and the residual adds as separate passes over 134 MB planes (C4: 32 x 128^2
+x 128 channels in bf16), and the final Linear over the 16,384 pixels as a cast copy + GEMV. Here:
+
+  forward   conv (MIOpen, bf16 NHWC) + ReLU in place; each residual block's tail
+            relu(relu(a) + x) in one pass (siren_enc_res_fwd); relu_2 + the pixel Linear in one
+            reduction (siren_enc_pixfc_fwd, fp32 out).
+  backward  the pixel Linear's three gradients and conv_1x1's ReLU mask + bias gradient in one pass
+            (siren_enc_pixfc_bwd); each block's mask / skip / bias-gradient work in one pass
+            (siren_enc_res_bwd, siren_enc_relu_bwd, the skip gradient added inside the next mask
+            pass instead of by a separate add); conv input gradients as FORWARD convolutions with
+            the flipped, transposed filter (stride 1, 'same' padding: the same GEMM, on the faster
+            forward kernels); conv weight gradients alone (aten.convolution_backward, weight mask).
+
+Arithmetic as the bf16 autocast path (modules.py ConvImgEncoder precision='bf16'): bf16 operands and
+activations, fp32 accumulation, fp32 master weights and gradients; the conv bias gradients and the
+pixel Linear are accumulated in fp32 (the autocast chain rounds them through bf16).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _native
+
+_CL = torch.channels_last
+_FUSED = [True]
+
+
+def set_fused(enabled: bool) -> None:
+    """Process-wide switch: the fused node (default) or the autocast chain (A/B, tests)."""
+    _FUSED[0] = bool(enabled)
+
+
+def fused_enabled() -> bool:
+    return _FUSED[0]
+
+
+def _ok_channels(c: int) -> bool:
+    return 8 <= c <= 256 and (c & (c - 1)) == 0
+
+
+def supported(enc) -> bool:
+    """The layer structure this node takes (ConvImgEncoder as modules.py builds it)."""
+    convs = [enc.conv_theta] + [m for m in enc.cnn if isinstance(m, torch.nn.Conv2d)]
+    if not all(c.stride == (1, 1) and c.dilation == (1, 1) and c.groups == 1 and c.bias is not None
+               and c.kernel_size[0] == c.kernel_size[1] and c.kernel_size[0] % 2 == 1
+               and c.padding == (c.kernel_size[0] // 2,) * 2 for c in convs):
+        return False
+    return all(_ok_channels(c.out_channels) for c in convs)
+
+
+def _w_bf16(w):
+    return w.detach().to(torch.bfloat16).contiguous(memory_format=_CL)
+
+
+def _w_flip(wb):
+    """Filter of the input gradient as a forward convolution: W'[ci][co] = W[co][ci] rotated 180."""
+    return wb.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL)
+
+
+def _conv(x, wb, bb, pad):
+    # NHWC planes for the passes below (MIOpen returns channels-last for channels-last operands;
+    # the call is a no-op then)
+    return F.conv2d(x, wb, bb, padding=pad).contiguous(memory_format=_CL)
+
+
+def _wgrad(g, x, wb, pad):
+    return torch.ops.aten.convolution_backward(g, x, wb, None, [1, 1], [pad, pad], [1, 1], False, [0, 0], 1,
+                                               [False, True, False])[1]
+
+
+def _plane(t):
+    """(P, C) of an NHWC tensor (channels-last contiguous)."""
+    n, c, h, w = t.shape
+    return n * h * w, c
+
+
+class _EncoderBF16(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, enc, I, *params):
+        dev = I.device
+        lib = _native.lib()
+        stream = _native.stream_handle(dev)
+        ws = _native.enc_workspace(dev)
+        convs = ctx.convs = enc._enc_layers
+        wbs = [_w_bf16(c.weight) for c in convs]
+        bbs = [c.bias.detach().to(torch.bfloat16) for c in convs]
+        x0 = I.detach().to(torch.bfloat16).contiguous(memory_format=_CL)
+        saved = [x0]
+        # conv_theta + relu, cnn[0] + relu
+        t = F.relu_(_conv(x0, wbs[0], bbs[0], convs[0].padding[0]))
+        saved.append(t)
+        t = F.relu_(_conv(t, wbs[1], bbs[1], convs[1].padding[0]))
+        saved.append(t)
+        k = 2
+        for _ in range(enc._enc_nblocks):
+            h = F.relu_(_conv(t, wbs[k], bbs[k], convs[k].padding[0]))
+            a = _conv(h, wbs[k + 1], bbs[k + 1], convs[k + 1].padding[0])
+            out = torch.empty_like(a)
+            P, C = _plane(a)
+            _native.check(lib.siren_enc_res_fwd(a.data_ptr(), t.data_ptr(), out.data_ptr(), P, C, stream),
+                          "siren_enc_res_fwd")
+            saved += [h, a, out]
+            t = out
+            k += 2
+        a = _conv(t, wbs[k], bbs[k], convs[k].padding[0])  # the 1x1 conv; relu_2 is in the pixfc pass
+        saved.append(a)
+        B = a.shape[0]
+        P = a.shape[2] * a.shape[3]
+        C = a.shape[1]
+        fc = enc.fc
+        e = torch.empty(B, C, dtype=torch.float32, device=dev)
+        _native.check(lib.siren_enc_pixfc_fwd(a.data_ptr(), fc.weight.detach().contiguous().data_ptr(),
+                                              fc.bias.detach().data_ptr(), e.data_ptr(), B, P, C, ws.data_ptr(),
+                                              ws.numel(), stream), "siren_enc_pixfc_fwd")
+        ctx.enc = enc
+        ctx.wbs = wbs
+        ctx.save_for_backward(*saved)
+        ctx.set_materialize_grads(False)
+        return e
+
+    @staticmethod
+    def backward(ctx, ge):
+        enc, convs, wbs = ctx.enc, ctx.convs, ctx.wbs
+        nparams = 2 * len(convs) + 2
+        if ge is None:
+            return (None, None) + (None,) * nparams
+        saved = list(ctx.saved_tensors)
+        dev = ge.device
+        lib = _native.lib()
+        stream = _native.stream_handle(dev)
+        ws = _native.enc_workspace(dev)
+        wsp, wsn = ws.data_ptr(), ws.numel()
+        fc = enc.fc
+        gW = [None] * len(convs)
+        gb = [None] * len(convs)
+        # relu_2 + pixel Linear, and the 1x1 conv's mask / bias gradient
+        a = saved.pop()
+        B, C = a.shape[0], a.shape[1]
+        P = a.shape[2] * a.shape[3]
+        gec = ge.detach().to(torch.float32).contiguous()
+        ga = torch.empty_like(a)
+        k = len(convs) - 1
+        gb[k] = torch.empty(C, dtype=torch.float32, device=dev)
+        gfw = torch.empty(P, dtype=torch.float32, device=dev)
+        _native.check(lib.siren_enc_pixfc_bwd(gec.data_ptr(), a.data_ptr(), fc.weight.detach().contiguous().data_ptr(),
+                                              ga.data_ptr(), gb[k].data_ptr(), gfw.data_ptr(), B, P, C, wsp, wsn,
+                                              stream), "siren_enc_pixfc_bwd")
+        g_fc_w = gfw.view_as(fc.weight)
+        g_fc_b = gec.sum().reshape(fc.bias.shape)
+        xin = saved[-1]  # the 1x1 conv's input (the last block's output, or cnn[0]'s)
+        pad = convs[k].padding[0]
+        gW[k] = _wgrad(ga, xin, wbs[k], pad)
+        g1 = _conv(ga, _w_flip(wbs[k]), None, pad)
+        g2 = None
+        # residual blocks, last to first
+        for _ in range(enc._enc_nblocks):
+            k -= 2
+            out = saved.pop()
+            a = saved.pop()
+            h = saved.pop()
+            t = saved[-1]  # the block's input
+            P, C = _plane(a)
+            gskip = torch.empty_like(a)
+            ga = torch.empty_like(a)
+            gb[k + 1] = torch.empty(C, dtype=torch.float32, device=dev)
+            _native.check(lib.siren_enc_res_bwd(g1.data_ptr(), g2.data_ptr() if g2 is not None else None,
+                                                out.data_ptr(), a.data_ptr(), gskip.data_ptr(), ga.data_ptr(),
+                                                gb[k + 1].data_ptr(), P, C, wsp, wsn, stream), "siren_enc_res_bwd")
+            pad = convs[k + 1].padding[0]
+            gW[k + 1] = _wgrad(ga, h, wbs[k + 1], pad)
+            gh = _conv(ga, _w_flip(wbs[k + 1]), None, pad)
+            ghm = torch.empty_like(h)
+            P, C = _plane(h)
+            gb[k] = torch.empty(C, dtype=torch.float32, device=dev)
+            _native.check(lib.siren_enc_relu_bwd(gh.data_ptr(), None, h.data_ptr(), ghm.data_ptr(), gb[k].data_ptr(),
+                                                 P, C, wsp, wsn, stream), "siren_enc_relu_bwd")
+            pad = convs[k].padding[0]
+            gW[k] = _wgrad(ghm, t, wbs[k], pad)
+            g1 = _conv(ghm, _w_flip(wbs[k]), None, pad)
+            g2 = gskip
+        # cnn[0] and conv_theta (each followed by a ReLU); no gradient into the image
+        for k in (1, 0):
+            y = saved.pop()
+            xin = saved[-1]
+            P, C = _plane(y)
+            gm = torch.empty_like(y)
+            gb[k] = torch.empty(C, dtype=torch.float32, device=dev)
+            _native.check(lib.siren_enc_relu_bwd(g1.data_ptr(), g2.data_ptr() if g2 is not None else None,
+                                                 y.data_ptr(), gm.data_ptr(), gb[k].data_ptr(), P, C, wsp, wsn,
+                                                 stream), "siren_enc_relu_bwd")
+            pad = convs[k].padding[0]
+            gW[k] = _wgrad(gm, xin, wbs[k], pad)
+            if k == 1:
+                g1 = _conv(gm, _w_flip(wbs[k]), None, pad)
+                g2 = None
+        grads = []
+        for k, c in enumerate(convs):
+            grads.append(gW[k].to(torch.float32).contiguous(memory_format=_CL)
+                         if c.weight.is_contiguous(memory_format=_CL) else gW[k].to(torch.float32).contiguous())
+            grads.append(gb[k])
+        grads += [g_fc_w, g_fc_b]
+        return (None, None, *grads)
+
+
+def encoder_bf16(enc, I):
+    """ConvImgEncoder.forward for precision='bf16' on the GPU (see the module docstring)."""
+    params = []
+    for c in enc._enc_layers:
+        params += [c.weight, c.bias]
+    params += [enc.fc.weight, enc.fc.bias]
+    return _EncoderBF16.apply(enc, I, *params)

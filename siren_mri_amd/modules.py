@@ -318,14 +318,39 @@ class ConvImgEncoder(nn.Module):
         self.image_resolution = image_resolution
         self._nhwc = False
 
+    def _layers(self):
+        """The convolutions in order (conv_theta, cnn[0], each block's two, the 1x1) for the fused
+        bf16 node (siren_mri_amd/encoder.py), or None when the structure is not the built one."""
+        from . import encoder
+        if "_enc_layers" not in self.__dict__:
+            layers = None
+            mods = list(self.cnn)
+            blocks = [m for m in mods if isinstance(m, Conv2dResBlock)]
+            if (len(mods) == len(blocks) + 3 and isinstance(mods[0], nn.Conv2d) and isinstance(mods[1], nn.ReLU)
+                    and all(isinstance(m, Conv2dResBlock) for m in mods[2:-1]) and isinstance(mods[-1], nn.Conv2d)
+                    and all(len(b.convs) == 4 and isinstance(b.convs[1], nn.ReLU) and isinstance(b.convs[3], nn.ReLU)
+                            for b in blocks)):
+                layers = [self.conv_theta, mods[0]]
+                for b in blocks:
+                    layers += [b.convs[0], b.convs[2]]
+                layers.append(mods[-1])
+            self.__dict__["_enc_layers"] = layers
+            self.__dict__["_enc_nblocks"] = len(blocks)
+            if layers is not None and not encoder.supported(self):
+                self.__dict__["_enc_layers"] = None
+        return self.__dict__["_enc_layers"]
+
     def forward(self, I):
         if self.precision == "bf16" and I.is_cuda:
+            from . import encoder
             if not self._nhwc:
                 # conv weights to channels-last once (their .grad follows the parameter's layout)
                 for m in self.modules():
                     if isinstance(m, nn.Conv2d):
                         m.weight.data = m.weight.data.contiguous(memory_format=torch.channels_last)
                 self._nhwc = True
+            if encoder.fused_enabled() and self._layers() is not None:
+                return encoder.encoder_bf16(self, I)
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 o = self.relu(self.conv_theta(I.contiguous(memory_format=torch.channels_last)))
                 o = self.relu_2(self.cnn(o))

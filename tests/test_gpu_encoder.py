@@ -1,0 +1,173 @@
+"""GPU: the fused bf16 conv-encoder node (siren_mri_amd/encoder.py) against
+the bf16 autocast chain it replaces and against the fp32 encoder (the reference's arithmetic,
+modules.py:340-380 / 433-450), and its native passes (siren_encoder.hip) against torch.
+
+Tolerances: the node's forward runs the same MIOpen convolutions as the autocast chain, so the
+embedding agrees to fp32 summation order (1e-5); its input gradients are forward convolutions on
+the flipped filter (another accumulation order, bf16-rounded planes), so parameter gradients agree
+to the bf16 level (2e-2 norm-relative); against fp32 no further off than the autocast chain.
+"""
+import pytest
+import torch
+
+from oracle import siren_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _encoder(precision, seed=0, blocks=2, hidden=128, k=7):
+    from siren_mri_amd import modules
+    torch.manual_seed(seed)
+    return modules.ConvImgEncoder(2, (128, 128), hidden_size=hidden, kernel_size=k, num_conv_res_blocks=blocks,
+                                  precision=precision).to(DEV)
+
+
+def _run(enc, I, ge):
+    enc.zero_grad(set_to_none=True)
+    e = enc(I)
+    e.backward(ge)
+    return e.detach().clone(), {n: p.grad.detach().clone() for n, p in enc.named_parameters()}
+
+
+@pytest.mark.parametrize("blocks,hidden,k", [(2, 128, 7), (1, 64, 5)])
+def test_fused_node_matches_autocast_chain(blocks, hidden, k):
+    from siren_mri_amd import encoder
+    enc = _encoder("bf16", blocks=blocks, hidden=hidden, k=k)
+    g = torch.Generator().manual_seed(1)
+    I = torch.randn(3, 2, 128, 128, generator=g).to(DEV)
+    ge = torch.randn(3, hidden, generator=g).to(DEV)
+    assert enc._layers() is not None
+    e_f, g_f = _run(enc, I, ge)
+    encoder.set_fused(False)
+    try:
+        e_c, g_c = _run(enc, I, ge)
+    finally:
+        encoder.set_fused(True)
+    assert orc.norm_rel(e_f.cpu(), e_c.cpu()) < 1e-5
+    assert g_f.keys() == g_c.keys()
+    for n in g_f:
+        assert orc.norm_rel(g_f[n].cpu(), g_c[n].cpu()) < 2e-2, n
+
+
+def test_fused_node_against_fp32_encoder():
+    """Against the fp32 encoder (the reference's arithmetic): the bf16 gradients of the first layers
+    sit ~5-10 % off after the ReLU masks and residual sums of a bf16 backward, for the autocast chain
+    as for the node; the node must be no further off than the chain it replaces."""
+    from siren_mri_amd import encoder
+    enc = _encoder("bf16", seed=2)
+    ref = _encoder("fp32", seed=2)
+    ref.load_state_dict(enc.state_dict())
+    g = torch.Generator().manual_seed(3)
+    I = torch.randn(2, 2, 128, 128, generator=g).to(DEV)
+    ge = torch.randn(2, 128, generator=g).to(DEV)
+    torch.backends.cudnn.allow_tf32 = False
+    e_f, g_f = _run(enc, I, ge)
+    encoder.set_fused(False)
+    try:
+        e_c, g_c = _run(enc, I, ge)
+    finally:
+        encoder.set_fused(True)
+    e_r, g_r = _run(ref, I, ge)
+    assert orc.norm_rel(e_f.cpu(), e_r.cpu()) < 3e-2
+    for n in g_f:
+        ef = orc.norm_rel(g_f[n].cpu(), g_r[n].cpu())
+        ec = orc.norm_rel(g_c[n].cpu(), g_r[n].cpu())
+        print(f"{n}: node {ef:.2e} autocast chain {ec:.2e}")
+        assert ef < 0.2 and ef <= 1.25 * ec + 5e-3, (n, ef, ec)
+
+
+def test_native_passes_deterministic():
+    """The passes' channel sums (block partials added in block order by the last block) repeat bit
+    for bit. (The whole node does not: MIOpen's convolutions of the residual blocks differ between
+    calls in the last bits, in the autocast chain as in the node.)"""
+    from siren_mri_amd import _native
+    lib = _native.lib()
+    st = _native.stream_handle(DEV)
+    ws = _ws()
+    B, P, C = 4, 16384, 128
+    g = torch.Generator().manual_seed(11)
+    a = torch.randn(B * P, C, generator=g).to(DEV).to(torch.bfloat16)
+    g1 = torch.randn(B * P, C, generator=g).to(DEV).to(torch.bfloat16)
+    w = torch.randn(P, generator=g).to(DEV)
+    bias = torch.zeros(1, device=DEV)
+    gin = torch.randn(B, C, generator=g).to(DEV)
+    res = []
+    for _ in range(4):
+        out = torch.empty_like(a)
+        db = torch.empty(C, device=DEV)
+        lib.siren_enc_relu_bwd(g1.data_ptr(), None, a.data_ptr(), out.data_ptr(), db.data_ptr(), B * P, C, ws.data_ptr(),
+                               ws.numel(), st)
+        e = torch.empty(B, C, device=DEV)
+        lib.siren_enc_pixfc_fwd(a.data_ptr(), w.data_ptr(), bias.data_ptr(), e.data_ptr(), B, P, C, ws.data_ptr(),
+                                ws.numel(), st)
+        ga, db2, gw = torch.empty_like(a), torch.empty(C, device=DEV), torch.empty(P, device=DEV)
+        lib.siren_enc_pixfc_bwd(gin.data_ptr(), a.data_ptr(), w.data_ptr(), ga.data_ptr(), db2.data_ptr(), gw.data_ptr(),
+                                B, P, C, ws.data_ptr(), ws.numel(), st)
+        res.append((db, e, db2, gw))
+    torch.cuda.synchronize()
+    for r in res[1:]:
+        for x, y in zip(res[0], r):
+            assert torch.equal(x, y)
+
+
+def _ws():
+    from siren_mri_amd import _native
+    return _native.enc_workspace(DEV)
+
+
+@pytest.mark.parametrize("C,P", [(128, 70000), (64, 4096), (8, 333)])
+def test_relu_bwd_and_res_passes_against_torch(C, P):
+    from siren_mri_amd import _native
+    lib = _native.lib()
+    st = _native.stream_handle(DEV)
+    ws = _ws()
+    g = torch.Generator().manual_seed(C + P)
+    mk = lambda: torch.randn(P, C, generator=g).to(DEV).to(torch.bfloat16)  # noqa: E731
+    g1, g2, y, a, x = mk(), mk(), mk(), mk(), mk()
+    out = torch.empty_like(g1)
+    db = torch.empty(C, device=DEV)
+    _native.check(lib.siren_enc_relu_bwd(g1.data_ptr(), g2.data_ptr(), y.data_ptr(), out.data_ptr(), db.data_ptr(),
+                                         P, C, ws.data_ptr(), ws.numel(), st), "relu_bwd")
+    ref = ((g1 + g2) * (y > 0)).to(torch.bfloat16)
+    assert torch.equal(out, ref)
+    torch.testing.assert_close(db, ref.float().sum(0), rtol=1e-5, atol=1e-4)
+    # res fwd / bwd
+    o = torch.empty_like(a)
+    _native.check(lib.siren_enc_res_fwd(a.data_ptr(), x.data_ptr(), o.data_ptr(), P, C, st), "res_fwd")
+    assert torch.equal(o, torch.relu(torch.relu(a) + x))
+    gs, ga = torch.empty_like(a), torch.empty_like(a)
+    _native.check(lib.siren_enc_res_bwd(g1.data_ptr(), None, o.data_ptr(), a.data_ptr(), gs.data_ptr(), ga.data_ptr(),
+                                        db.data_ptr(), P, C, ws.data_ptr(), ws.numel(), st), "res_bwd")
+    s_ref = g1 * (o > 0)
+    assert torch.equal(gs, s_ref)
+    assert torch.equal(ga, s_ref * (a > 0))
+    torch.testing.assert_close(db, ga.float().sum(0), rtol=1e-5, atol=1e-4)
+
+
+def test_pixel_linear_passes_against_torch():
+    from siren_mri_amd import _native
+    lib = _native.lib()
+    st = _native.stream_handle(DEV)
+    ws = _ws()
+    B, H, C = 5, 128, 128
+    P = H * H
+    g = torch.Generator().manual_seed(9)
+    a = torch.randn(B, H, H, C, generator=g).to(DEV).to(torch.bfloat16)
+    w = (torch.randn(P, generator=g) / 128).to(DEV)
+    bias = torch.randn(1, generator=g).to(DEV)
+    e = torch.empty(B, C, device=DEV)
+    _native.check(lib.siren_enc_pixfc_fwd(a.data_ptr(), w.data_ptr(), bias.data_ptr(), e.data_ptr(), B, P, C,
+                                          ws.data_ptr(), ws.numel(), st), "pixfc_fwd")
+    r = torch.relu(a.float()).reshape(B, P, C)
+    torch.testing.assert_close(e, torch.einsum("bpc,p->bc", r, w) + bias, rtol=1e-4, atol=1e-4)
+    gin = torch.randn(B, C, generator=g).to(DEV)
+    ga = torch.empty_like(a)
+    db = torch.empty(C, device=DEV)
+    gw = torch.empty(P, device=DEV)
+    _native.check(lib.siren_enc_pixfc_bwd(gin.data_ptr(), a.data_ptr(), w.data_ptr(), ga.data_ptr(), db.data_ptr(),
+                                          gw.data_ptr(), B, P, C, ws.data_ptr(), ws.numel(), st), "pixfc_bwd")
+    ga_ref = ((a.float() > 0) * gin[:, None, None, :] * w.reshape(1, H, H, 1)).to(torch.bfloat16)
+    assert torch.equal(ga, ga_ref)
+    torch.testing.assert_close(db, ga_ref.float().sum((0, 1, 2)), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(gw, torch.einsum("bc,bpc->p", gin, r), rtol=1e-4, atol=1e-3)

@@ -44,33 +44,39 @@ def test_adam_state_dict_round_trip_with_torch():
     assert torch.equal(o2.state[p]["exp_avg"], o1.state[p]["exp_avg"])
 
 
-def test_adam_graph_mode_replay_matches_eager():
+@pytest.mark.parametrize("sizes", [(300,), (300000, 77, 256 * 256)])
+def test_adam_graph_mode_replay_matches_eager(sizes):
     """enable_graph_mode(): bias corrections from a device step counter, so a hipGraph of the
-    step replays with the right t each time (same values as eager steps)."""
+    step replays with the right t each time (same values as eager steps). One launch per group:
+    the launch advances the counter itself (the last of its workgroups; (300000, ...) runs 293)."""
     from siren_mri_amd.optim import Adam
     g = torch.Generator().manual_seed(1)
-    init = torch.randn(300, generator=g)
-    grads = [torch.randn(300, generator=g).to(DEV) for _ in range(6)]
-    p_e = torch.nn.Parameter(init.clone().to(DEV))
-    o_e = Adam([p_e], lr=1e-2)
-    for gr in grads:
-        p_e.grad = gr.clone()
+    inits = [torch.randn(n, generator=g) for n in sizes]
+    grads = [[torch.randn(n, generator=g).to(DEV) for n in sizes] for _ in range(6)]
+    p_e = [torch.nn.Parameter(t.clone().to(DEV)) for t in inits]
+    o_e = Adam(p_e, lr=1e-2)
+    for gs in grads:
+        for p, gr in zip(p_e, gs):
+            p.grad = gr.clone()
         o_e.step()
-    p_g = torch.nn.Parameter(init.clone().to(DEV))
-    o_g = Adam([p_g], lr=1e-2)
+    p_g = [torch.nn.Parameter(t.clone().to(DEV)) for t in inits]
+    o_g = Adam(p_g, lr=1e-2)
     o_g.enable_graph_mode()
-    gbuf = torch.empty(300, device=DEV)
-    p_g.grad = gbuf
-    gbuf.copy_(grads[0])
+    gbuf = [torch.empty(n, device=DEV) for n in sizes]
+    for p, b, gr in zip(p_g, gbuf, grads[0]):
+        p.grad = b
+        b.copy_(gr)
     o_g.step()  # eager first step creates the device counter (t = 1)
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
         o_g.step()
-    for gr in grads[1:]:
-        gbuf.copy_(gr)
+    for gs in grads[1:]:
+        for b, gr in zip(gbuf, gs):
+            b.copy_(gr)
         graph.replay()
     torch.cuda.synchronize()
-    torch.testing.assert_close(p_g.detach(), p_e.detach(), rtol=1e-6, atol=1e-7)
+    for a, b in zip(p_g, p_e):
+        torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-6, atol=1e-7)
     o_g.sync_graph_steps()
     # the capture itself does not step: 1 eager + 5 replays = 6 steps, like the eager optimizer
-    assert float(o_g.state[p_g]["step"]) == 6.0
+    assert float(o_g.state[p_g[0]]["step"]) == 6.0

@@ -64,10 +64,13 @@ def _check(dims, B, N, seed, tol=(2e-3, 2e-2), need_dx=False):
     return y.detach()
 
 
-def test_config4_siren_batched_32x16384():
+@pytest.mark.parametrize("need_dx", [False, True])
+def test_config4_siren_batched_32x16384(need_dx):
     # the hypo-net of configs 4/5 (reference config hyperoptIV_homebrew): 8 Fourier features -> 16
-    # inputs, 3 hidden x 256, 2 outputs, 32 slices of 128^2 coordinates with per-slice weights
-    _check([16, 256, 256, 256, 256, 2], 32, 16384, seed=3)
+    # inputs, 3 hidden x 256, 2 outputs, 32 slices of 128^2 coordinates with per-slice weights.
+    # need_dx: SingleBVPNet's coordinate leaf requires grad, so the models ask for dx (the
+    # first_dx_wide MFMA launch beside first_bwd_wide)
+    _check([16, 256, 256, 256, 256, 2], 32, 16384, seed=3, need_dx=need_dx)
 
 
 def test_config4_small_siren_in120_32x16384():
