@@ -216,44 +216,52 @@ typedef struct siren_adam_desc {
   float* exp_avg_sq[SIREN_ADAM_MAX_TENSORS];
   const float* dev_scalars;      /* NULL, or device {step_size, bias_correction2_sqrt} read by the
                                     kernel (written by siren_adam_scalars: hipGraph replays) */
-  double* dev_step;              /* NULL, or device {t, ticket} (16 bytes, ticket zero between launches):
-                                    the launch itself advances t by one (graph mode without the extra
-                                    single-thread launch); dev_scalars is then ignored and the step's
-                                    {step_size, bias_correction2_sqrt} is dev_table[min(t, table_n) - 1]
-                                    (host-computed in double as siren_adam_scalars does; the host ends
-                                    the table where both corrections have reached their limit) */
-  const float* dev_table;        /* [table_n][2] device (dev_step only) */
-  int64_t table_n;
 } siren_adam_desc;
 int siren_adam_step(const siren_adam_desc* d, void* stream);
 /* Device-side bias corrections for graph-captured steps: *t += 1, then
  * out[0] = -(lr / (1 - beta1^t)), out[1] = sqrt(1 - beta2^t), computed in double and rounded to
  * float as the host path does (t, out: device pointers). One single-thread launch. */
 int siren_adam_scalars(double* t, double lr, double beta1, double beta2, float* out, void* stream);
+/* The same from a host-computed table ([n][2] {step_size, bias_correction2_sqrt} of t = 1 .. n, the
+ * last entry repeated past the end): *t += 1, out = table[t - 1]. No pow in the launch. */
+int siren_adam_scalars_table(double* t, const float* table, int64_t n, float* out, void* stream);
 
 /*
  * Configs 4/5's conv encoder (modules.py:340-380, 433-450) in bf16 channels-last: the passes around
- * the convolutions, each one launch over a [P, C] plane (P pixels, C a power of two in [8, 256]).
- * Channel sums (db) are deterministic: per-block partials in `ws` (siren_enc_workspace_bytes, zeroed
- * once and left zeroed), added in block order by the last block. g2 may be NULL.
+ * the (bias-free) convolutions, each one launch over a [P, C] plane (P pixels, C a power of two in
+ * [8, 256]). cb is the producing convolution's bf16 bias ([C], or NULL): the pre-activation is
+ * bf16(a + cb), the rounding of the conv + bias-add chain. Channel sums (db) are deterministic:
+ * per-block partials in `ws` (siren_enc_workspace_bytes, zeroed once and left zeroed), added in
+ * block order by the last block. g2 may be NULL.
+ *   bias_relu: y = relu(bf16(y + cb)) in place                         (conv bias + ReLU)
  *   relu_bwd : out = (g1 + g2) * (y > 0) (bf16), db[c] = sum_p out     (ReLU backward + conv bias grad)
- *   res_fwd  : out = relu(relu(a) + x)                                (Conv2dResBlock tail)
- *   res_bwd  : gskip = (g1 + g2) * (out > 0), ga = gskip * (a > 0), db[c] = sum_p ga
- *   pixfc_fwd: e[b][c] = sum_p relu(a[b][p][c]) w[p] + *bias           (relu_2 + fc over pixels)
- *   pixfc_bwd: ga[b][p][c] = (a > 0) g[b][c] w[p], db[c] = sum_{b,p} ga, gw[p] = sum_{b,c} g relu(a)
+ *   res_fwd  : out = relu(relu(a + cb) + x)                            (Conv2dResBlock tail)
+ *   res_bwd  : gskip = (g1 + g2) * (out > 0), ga = gskip * (a + cb > 0), db[c] = sum_p ga
+ *   pixfc_fwd: e[b][c] = sum_p relu(a[b][p][c] + cb[c]) w[p] + *bias   (relu_2 + fc over pixels)
+ *   pixfc_bwd: ga[b][p][c] = (a + cb > 0) g[b][c] w[p], db[c] = sum_{b,p} ga,
+ *              gw[p] = sum_{b,c} g relu(a + cb)
  * (P is per image for pixfc; a is [B][P][C].) Replaces the autograd chain of ConvImgEncoder's
- * ReLUs, residual adds, conv bias reductions and its Linear over the pixels.
+ * conv bias adds, ReLUs, residual adds, conv bias reductions and its Linear over the pixels.
  */
 int64_t siren_enc_workspace_bytes(void);
+/* Weight gradient of a 128 -> 128 channel, 5x5, stride-1, padding-2 convolution (Conv2dResBlock's,
+ * modules.py:433-450) from bf16 NHWC x and dy ([N][H][W][128], W a multiple of 64) into fp32 dw
+ * in the channels-last filter layout [co][kh][kw][ci]: split-K bf16-MFMA partials in ws
+ * (siren_conv_wrw_workspace_bytes) added in split order (deterministic). Replaces the convolution
+ * weight-gradient of the encoder's autograd chain. */
+int64_t siren_conv_wrw_workspace_bytes(int N, int H, int W);
+int siren_conv_wrw_k5(const void* x, const void* dy, int N, int H, int W, int C, float* dw, void* ws, int64_t ws_bytes,
+                      void* stream);
 int siren_enc_relu_bwd(const void* g1, const void* g2, const void* y, void* out, float* db, int64_t P, int C, void* ws,
                        int64_t ws_bytes, void* stream);
-int siren_enc_res_fwd(const void* a, const void* x, void* out, int64_t P, int C, void* stream);
-int siren_enc_res_bwd(const void* g1, const void* g2, const void* out, const void* a, void* gskip, void* ga,
-                      float* db, int64_t P, int C, void* ws, int64_t ws_bytes, void* stream);
-int siren_enc_pixfc_fwd(const void* a, const float* w, const float* bias, float* e, int B, int64_t P, int C, void* ws,
-                        int64_t ws_bytes, void* stream);
-int siren_enc_pixfc_bwd(const float* g, const void* a, const float* w, void* ga, float* db, float* gw, int B,
-                        int64_t P, int C, void* ws, int64_t ws_bytes, void* stream);
+int siren_enc_bias_relu(void* y, const void* cb, int64_t P, int C, void* stream);
+int siren_enc_res_fwd(const void* a, const void* cb, const void* x, void* out, int64_t P, int C, void* stream);
+int siren_enc_res_bwd(const void* g1, const void* g2, const void* out, const void* a, const void* cb, void* gskip,
+                      void* ga, float* db, int64_t P, int C, void* ws, int64_t ws_bytes, void* stream);
+int siren_enc_pixfc_fwd(const void* a, const void* cb, const float* w, const float* bias, float* e, int B, int64_t P,
+                        int C, void* ws, int64_t ws_bytes, void* stream);
+int siren_enc_pixfc_bwd(const float* g, const void* a, const void* cb, const float* w, void* ga, float* db, float* gw,
+                        int B, int64_t P, int C, void* ws, int64_t ws_bytes, void* stream);
 
 /*
  * Weighted sum of squared errors of image_mse (replaces loss_functions.py:66-101's

@@ -44,8 +44,12 @@ EXPORTED_SYMBOLS = (
     "siren_config_get",
     "siren_adam_step",
     "siren_adam_scalars",
+    "siren_adam_scalars_table",
     "siren_sse_workspace_bytes",
     "siren_enc_workspace_bytes",
+    "siren_conv_wrw_workspace_bytes",
+    "siren_conv_wrw_k5",
+    "siren_enc_bias_relu",
     "siren_enc_relu_bwd",
     "siren_enc_res_fwd",
     "siren_enc_res_bwd",
@@ -139,9 +143,7 @@ class SirenAdamDesc(ctypes.Structure):
         ("exp_avg", ctypes.c_void_p * ADAM_MAX_TENSORS),
         ("exp_avg_sq", ctypes.c_void_p * ADAM_MAX_TENSORS),
         ("dev_scalars", ctypes.c_void_p),
-        ("dev_step", ctypes.c_void_p),
-        ("dev_table", ctypes.c_void_p),
-        ("table_n", ctypes.c_int64),
+
     ]
 
 
@@ -201,19 +203,27 @@ def _declare(lib):
     f64 = ctypes.c_double
     lib.siren_adam_scalars.argtypes = [vp, f64, f64, f64, vp, vp]
     lib.siren_adam_scalars.restype = ctypes.c_int
+    lib.siren_adam_scalars_table.argtypes = [vp, vp, i64, vp, vp]
+    lib.siren_adam_scalars_table.restype = ctypes.c_int
     lib.siren_sse_workspace_bytes.argtypes = []
     lib.siren_sse_workspace_bytes.restype = i64
+    lib.siren_conv_wrw_workspace_bytes.argtypes = [ci, ci, ci]
+    lib.siren_conv_wrw_workspace_bytes.restype = i64
+    lib.siren_conv_wrw_k5.argtypes = [vp, vp, ci, ci, ci, ci, vp, vp, i64, vp]
+    lib.siren_conv_wrw_k5.restype = ci
     lib.siren_enc_workspace_bytes.argtypes = []
     lib.siren_enc_workspace_bytes.restype = i64
     lib.siren_enc_relu_bwd.argtypes = [vp, vp, vp, vp, vp, i64, ci, vp, i64, vp]
     lib.siren_enc_relu_bwd.restype = ci
-    lib.siren_enc_res_fwd.argtypes = [vp, vp, vp, i64, ci, vp]
+    lib.siren_enc_bias_relu.argtypes = [vp, vp, i64, ci, vp]
+    lib.siren_enc_bias_relu.restype = ci
+    lib.siren_enc_res_fwd.argtypes = [vp, vp, vp, vp, i64, ci, vp]
     lib.siren_enc_res_fwd.restype = ci
-    lib.siren_enc_res_bwd.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, ci, vp, i64, vp]
+    lib.siren_enc_res_bwd.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, ci, vp, i64, vp]
     lib.siren_enc_res_bwd.restype = ci
-    lib.siren_enc_pixfc_fwd.argtypes = [vp, vp, vp, vp, ci, i64, ci, vp, i64, vp]
+    lib.siren_enc_pixfc_fwd.argtypes = [vp, vp, vp, vp, vp, ci, i64, ci, vp, i64, vp]
     lib.siren_enc_pixfc_fwd.restype = ci
-    lib.siren_enc_pixfc_bwd.argtypes = [vp, vp, vp, vp, vp, vp, ci, i64, ci, vp, i64, vp]
+    lib.siren_enc_pixfc_bwd.argtypes = [vp, vp, vp, vp, vp, vp, vp, ci, i64, ci, vp, i64, vp]
     lib.siren_enc_pixfc_bwd.restype = ci
     lib.siren_sse_forward.argtypes = [vp, vp, vp, i64, i64, f32, vp, vp, vp, i64, vp]
     lib.siren_sse_forward.restype = ctypes.c_int

@@ -17,11 +17,19 @@ struct AdamArgs {
   int64_t numel[SIREN_ADAM_MAX_TENSORS];
   float one_minus_beta1, beta2, one_minus_beta2, eps, weight_decay, step, bc2_sqrt;
   const float* dev;  // null, or device {step, bc2_sqrt} (graph-captured steps)
-  double* tstep;     // null, or device {t, ticket}: this launch advances t (see adam_kernel)
-  const float* table;  // [table_n][2] {step, bc2_sqrt} of t = 1 .. table_n
-  int64_t table_n;
   int maximize;
 };
+
+// graph mode, table form: t += 1, out = the host-computed {step, bc2_sqrt} of step t (the last
+// entry past the table's end: the host ends it where both bias corrections have reached 1)
+__global__ void adam_scalars_table_kernel(double* t, const float* table, int64_t n, float* out) {
+  const double tt = *t + 1.0;
+  *t = tt;
+  int64_t k = (int64_t)tt - 1;
+  k = k < 0 ? 0 : k >= n ? n - 1 : k;
+  out[0] = table[2 * k];
+  out[1] = table[2 * k + 1];
+}
 
 __global__ void adam_scalars_kernel(double* t, double lr, double beta1, double beta2, float* out) {
   const double tt = *t + 1.0;
@@ -34,10 +42,6 @@ DEV float torch_lerp(float self, float end, float w) {
   return fabsf(w) < 0.5f ? self + w * (end - self) : end - (end - self) * (1.f - w);
 }
 
-// tstep: every workgroup takes the bias corrections of step t + 1 from the host-computed table; the
-// last workgroup to finish stores t + 1 and rearms the ticket. (Computing them here in double, as
-// adam_scalars_kernel does, made this launch 10x slower: pow's code and stack in every workgroup.) Each workgroup reads t before it takes its ticket, so the last one to
-// take a ticket writes after every read.
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   const int t = blockIdx.y;
   const int64_t n = a.numel[t];
@@ -45,23 +49,8 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   const float* gr = a.grad[t];
   float* m = a.exp_avg[t];
   float* v = a.exp_avg_sq[t];
-  __shared__ float sc[2];
-  __shared__ double st_next;
-  if (a.tstep) {
-    if (threadIdx.x == 0) {
-      const double tt = a.tstep[0] + 1.0;
-      st_next = tt;
-      // entries past the table's end equal its last one (the host ends the table where both bias
-      // corrections have reached 1 in double)
-      int64_t k = (int64_t)tt - 1;
-      k = k < 0 ? 0 : k >= a.table_n ? a.table_n - 1 : k;
-      sc[0] = a.table[2 * k];
-      sc[1] = a.table[2 * k + 1];
-    }
-    __syncthreads();
-  }
-  const float step = a.tstep ? sc[0] : a.dev ? a.dev[0] : a.step;
-  const float bc2_sqrt = a.tstep ? sc[1] : a.dev ? a.dev[1] : a.bc2_sqrt;
+  const float step = a.dev ? a.dev[0] : a.step;
+  const float bc2_sqrt = a.dev ? a.dev[1] : a.bc2_sqrt;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     float g = gr[i];
     if (a.maximize) g = -g;
@@ -75,14 +64,6 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
     m[i] = mv;
     v[i] = vv;
     p[i] = pv + step * (mv / d);
-  }
-  if (a.tstep && threadIdx.x == 0) {
-    unsigned* ticket = (unsigned*)(a.tstep + 1);
-    const unsigned nwg = gridDim.x * gridDim.y;
-    if (__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1) {
-      a.tstep[0] = st_next;
-      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
 }
 

@@ -1,0 +1,184 @@
+// siren_conv.hip — the weight gradient of the conv encoder's residual-block convolutions
+// (Conv2dResBlock, modules.py:433-450: 128 -> 128 channels, 5x5, stride 1, padding 2) in bf16
+// channels-last, on the bf16 MFMA:
+//
+//   dW[co][kh][kw][ci] = sum_{n,h,w} dY[n][h][w][co] X[n][h + kh - 2][w + kw - 2][ci]   (0 outside)
+//
+// i.e. 25 GEMMs (one per tap) of M = co, N = ci, K = N H W pixels. MIOpen's best solver for this
+// shape (igemm_wrw, bf16 NHWC) ran 0.6 ms per convolution in the C4 step (0.27 of the bf16 peak).
+//
+// Work split: workgroup (split, kh, co half) owns the 5 taps of one filter row for 64 output
+// channels — 40 accumulator blocks of 32 x 32, five per wave: wave w holds co block w & 1 and ci
+// block w >> 1 for all five kw (80 accumulator registers) — over a contiguous range of output
+// image rows (split-K), and writes one fp32 partial; conv_wrw_reduce_kernel adds the partials in
+// split order (deterministic) straight into the fp32, channels-last [co][kh][kw][ci] gradient.
+// Per 64-pixel chunk of an output row, the dY chunk (64 px x 64 co) and the X halo (68 px x 128 ci
+// of input row h + kh - 2, zeros outside the image) are staged in LDS (three stages; the global
+// loads of the chunk after next are in flight during this chunk's MFMAs); the MFMA operands come from
+// transposing reads (ds_read_b64_tr_b16: pixels are the K dimension), the five taps reading the X
+// halo at row offsets kw. LDS rows are padded to 192 / 320 bytes (4-row transposing reads on
+// distinct bank groups).
+#include <type_traits>
+
+#include "siren_common.h"
+
+namespace siren {
+
+constexpr int CW_C = 128;                    // channels (in and out)
+constexpr int CW_K = 5;                      // filter size
+constexpr int CW_PX = 64;                    // output pixels per chunk
+constexpr int CW_XROWS = CW_PX + CW_K - 1;   // 68 halo rows
+constexpr int CW_DROW = 96;                  // bf16 per staged dY row (64 co + 32 pad: 192 B)
+constexpr int CW_XROW = 160;                 // bf16 per staged X row (128 ci + 32 pad: 320 B)
+constexpr int CW_NB = 3;                     // LDS stages
+constexpr int CW_XPIECES = CW_XROWS * 16;    // 16-byte pieces of the X halo (1088)
+constexpr int CW_NXL = (CW_XPIECES + 511) / 512;  // per thread (3)
+constexpr int CW_SLAB = CW_K * CW_K * CW_C * CW_C;  // floats of one partial
+
+struct ConvWArgs {
+  const bf16* x;    // [N][H][W][128]
+  const bf16* dy;   // [N][H][W][128]
+  float* part;      // [nsplit][5 kh][5 kw][128 co][128 ci]
+  float* dw;        // [128 co][5 kh][5 kw][128 ci] (reduce)
+  int N, H, W;
+  int64_t rows_per_split;  // output image rows (of N * H) per split
+  int nsplit;
+};
+
+// Pipeline: chunk t + 2's global loads go to register set t % 2 while chunk t's MFMAs run; at the
+// top of iteration t + 1 that set is written to LDS stage (t + 2) % 3 (last read in iteration
+// t - 1, before the barrier that closed it); one barrier per chunk.
+__global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 sD[CW_NB][CW_PX * CW_DROW];
+  __shared__ __attribute__((aligned(16))) bf16 sX[CW_NB][CW_XROWS * CW_XROW];
+  const int split = blockIdx.x, kh = blockIdx.y, ch = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cb = wave & 1, ib = wave >> 1;
+  const int nrows = a.N * a.H;
+  const int64_t r0 = (int64_t)split * a.rows_per_split;
+  const int64_t r1 = r0 + a.rows_per_split < nrows ? r0 + a.rows_per_split : nrows;
+  const int nch = a.W / CW_PX;
+  const int64_t T = r1 > r0 ? (r1 - r0) * nch : 0;
+
+  f32x16 acc[CW_K];
+#pragma unroll
+  for (int k = 0; k < CW_K; ++k)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[k][e] = 0.f;
+
+  // loader: one dY piece per thread (row tid / 8, piece tid % 8 of the 64-channel half), X halo
+  // pieces p = tid + 512 i (row p / 16, piece p % 16; zeros outside the image)
+  // (two register sets, selected at compile time: the loop below is unrolled by two, since a
+  // run-time set index became indexed register moves)
+  u32x4_t dv[2], xv[2][CW_NXL];
+  const u32x4_t zero = {0u, 0u, 0u, 0u};
+  auto load = [&](int64_t t, auto set_c) {
+    constexpr int set = decltype(set_c)::value;
+    const int64_t r = r0 + t / nch;
+    const int px0 = (int)(t % nch) * CW_PX;
+    const int n = (int)(r / a.H), h = (int)(r % a.H);
+    const int xr = h + kh - CW_K / 2;
+    const bool rowok = xr >= 0 && xr < a.H;
+    dv[set] = *(const u32x4_t*)(a.dy + (((int64_t)n * a.H + h) * a.W + px0 + (tid >> 3)) * CW_C + 64 * ch +
+                                8 * (tid & 7));
+    const bf16* xrow = a.x + ((int64_t)n * a.H + (rowok ? xr : 0)) * a.W * CW_C;
+#pragma unroll
+    for (int i = 0; i < CW_NXL; ++i) {
+      const int p = tid + 512 * i;
+      const int w = px0 - CW_K / 2 + (p >> 4);
+      const bool ok = p < CW_XPIECES && rowok && w >= 0 && w < a.W;
+      xv[set][i] = ok ? *(const u32x4_t*)(xrow + (int64_t)w * CW_C + 8 * (p & 15)) : zero;
+    }
+  };
+  auto stage = [&](auto set_c, int buf) {
+    constexpr int set = decltype(set_c)::value;
+    *(u32x4_t*)(&sD[buf][(tid >> 3) * CW_DROW + 8 * (tid & 7)]) = dv[set];
+#pragma unroll
+    for (int i = 0; i < CW_NXL; ++i) {
+      const int p = tid + 512 * i;
+      if (p < CW_XPIECES) *(u32x4_t*)(&sX[buf][(p >> 4) * CW_XROW + 8 * (p & 15)]) = xv[set][i];
+    }
+  };
+
+  // transposing-read lane roles (tn_dw_kernel's): rows nb, nb + 4 of a 16-row K step, 4 columns.
+  // The reads are inline asm with counted lgkmcnt waits: hipcc puts an s_waitcnt vmcnt(0) in
+  // front of the ds_read_tr builtin, which would drain the next chunks' global loads every step.
+  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  const int ca = 32 * cb + 16 * (g & 1) + 4 * tp;   // co column within the half
+  const int cx = 32 * ib + 16 * (g & 1) + 4 * tp;   // ci column
+  const int r8 = 8 * (g >> 1) + tq;                  // row of K step 0
+  const uint32_t dbase = lds_addr(&sD[0][0]) + (uint32_t)((r8 * CW_DROW + ca) * 2);
+  const uint32_t xbase = lds_addr(&sX[0][0]) + (uint32_t)((r8 * CW_XROW + cx) * 2);
+  constexpr uint32_t DSTAGE = CW_PX * CW_DROW * 2, XSTAGE = CW_XROWS * CW_XROW * 2;
+  constexpr int DROWB = CW_DROW * 2, XROWB = CW_XROW * 2;
+
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  if (T > 0) {
+    load(0, S0{});
+    stage(S0{}, 0);
+  }
+  if (T > 1) load(1, S1{});
+  __syncthreads();
+  // iteration t: chunk t + 1 (register set (t + 1) & 1) to LDS, chunk t + 2's loads into set t & 1,
+  // chunk t's MFMAs
+  auto iter = [&](int64_t t, auto par_c) {
+    constexpr int par = decltype(par_c)::value;  // t & 1
+    using SN = std::integral_constant<int, par ^ 1>;
+    using SC = std::integral_constant<int, par>;
+    if (t + 1 < T) stage(SN{}, (int)((t + 1) % CW_NB));
+    if (t + 2 < T) load(t + 2, SC{});
+    const int buf = (int)(t % CW_NB);
+    const uint32_t db = dbase + buf * DSTAGE, xb = xbase + buf * XSTAGE;
+    static_for<0, CW_PX / 16>([&](auto ks_c) {
+      constexpr int ks = decltype(ks_c)::value;
+      TrFrag fa, fb[CW_K];
+      tr16_read<16 * ks * DROWB>(fa.lo, db);
+      tr16_read<16 * ks * DROWB + 4 * DROWB>(fa.hi, db);
+      static_for<0, CW_K>([&](auto kw_c) {
+        constexpr int kw = decltype(kw_c)::value;
+        tr16_read<(16 * ks + kw) * XROWB>(fb[kw].lo, xb);
+        tr16_read<(16 * ks + kw + 4) * XROWB>(fb[kw].hi, xb);
+      });
+      static_for<0, CW_K>([&](auto kw_c) {
+        constexpr int kw = decltype(kw_c)::value;
+        // A and B_0..B_kw landed: 2 + 2 (kw + 1) of the 12 reads
+        asm volatile("s_waitcnt lgkmcnt(%4)"
+                     : "+v"(fa.lo), "+v"(fa.hi), "+v"(fb[kw].lo), "+v"(fb[kw].hi)
+                     : "n"(8 - 2 * kw));
+        acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr16_value(fa), tr16_value(fb[kw]), acc[kw], 0, 0, 0);
+      });
+    });
+    __syncthreads();
+  };
+  for (int64_t t = 0; t < T; t += 2) {
+    iter(t, S0{});
+    if (t + 1 < T) iter(t + 1, S1{});
+  }
+
+  // partial: [split][kh][kw][co][ci]
+  float* P = a.part + ((int64_t)split * CW_K + kh) * CW_K * CW_C * CW_C;
+#pragma unroll
+  for (int kw = 0; kw < CW_K; ++kw) {
+    const int ci = 32 * ib + (lane & 31);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int co = 64 * ch + 32 * cb + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+      P[((int64_t)kw * CW_C + co) * CW_C + ci] = acc[kw][e];
+    }
+  }
+}
+
+// dw[co][kh][kw][ci] = sum_s part[s][kh][kw][co][ci], splits in order
+__global__ __launch_bounds__(256) void conv_wrw_reduce_kernel(ConvWArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // over [kh][kw][co][ci]
+  if (i >= CW_SLAB) return;
+  const int ci = (int)(i % CW_C);
+  const int co = (int)((i / CW_C) % CW_C);
+  const int tap = (int)(i / ((int64_t)CW_C * CW_C));  // kh * 5 + kw
+  float s = 0.f;
+  for (int sp = 0; sp < a.nsplit; ++sp) s += a.part[(int64_t)sp * CW_SLAB + i];
+  a.dw[((int64_t)co * CW_K * CW_K + tap) * CW_C + ci] = s;
+}
+
+}  // namespace siren

@@ -9,10 +9,14 @@
 // are folded into one pass each:
 //
 //   enc_relu_bwd     g = (g1 [+ g2]) * (y > 0) -> bf16, db[c] = sum_p g        (ReLU + bias grad)
-//   enc_res_fwd      out = relu(relu(a) + x)                                (res block tail)
-//   enc_res_bwd      s = (g1 [+ g2]) * (out > 0), ga = s * (a > 0), db[c] = sum_p ga
-//   enc_pixfc_fwd    e[b][c] = sum_p relu(a[b][p][c]) w[p] + bias           (relu_2 + fc over pixels)
-//   enc_pixfc_bwd    ga[b][p][c] = (a > 0) g[b][c] w[p], db[c] = sum ga, gw[p] = sum_bc g relu(a)
+//   enc_bias_relu    y = relu(y + cb)                                       (conv bias + ReLU)
+//   enc_res_fwd      out = relu(relu(a + cb) + x)                           (res block tail)
+//   enc_res_bwd      s = (g1 [+ g2]) * (out > 0), ga = s * (a + cb > 0), db[c] = sum_p ga
+//   enc_pixfc_fwd    e[b][c] = sum_p relu(a[b][p][c] + cb[c]) w[p] + bias   (relu_2 + fc over pixels)
+//   enc_pixfc_bwd    ga[b][p][c] = (a + cb > 0) g[b][c] w[p], db[c] = sum ga, gw[p] = sum_bc g relu(a + cb)
+//
+// The convolutions run without their bias (MIOpen adds it as a separate pass over the plane); cb
+// is added here with the same bf16 rounding.
 //
 // Thread mapping: a thread owns 8 channels (16 bytes) of one pixel, C / 8 threads per pixel.
 // Channel sums are per-thread fp32 partials over a block's pixels, summed over the block in a fixed
@@ -27,6 +31,7 @@ constexpr int ENC_MAXC = 256;
 // workspace: partial sums [ENC_MAX_BLOCKS][ENC_MAXC] (pixfc_fwd: [blocks][B][C] <= the same), then
 // the ticket
 constexpr int64_t ENC_WS_FLOATS = (int64_t)ENC_MAX_BLOCKS * ENC_MAXC;
+constexpr int ENC_U = 4;  // pixels per thread per iteration in the gradient passes
 
 struct EncArgs {
   const bf16* g1;     // incoming gradient (or a / x operands, see each kernel)
@@ -40,6 +45,8 @@ struct EncArgs {
   const float* gin;   // pixfc_bwd: [B][C] incoming gradient
   float* e;           // pixfc_fwd: [B][C] output; pixfc_bwd: gw [P_img]
   const float* bias;  // pixfc_fwd: [1] device scalar added to every output
+  const bf16* cb;     // [C] bias of the convolution that produced `a` (or y for bias_relu), or null:
+                      // the pre-activation is bf16(a + cb[c]), the conv + bias-add chain's rounding
   float* part;        // workspace partials
   unsigned* ticket;   // workspace ticket
   int64_t P;          // pixels of the plane (pixfc: per image)
@@ -51,6 +58,20 @@ DEV void load_bf16x8(const bf16* p, float (&v)[8]) {
   const bf16x8 t = *(const bf16x8*)p;
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = (float)t[e];
+}
+
+// the thread's 8 channel biases (zeros without a bias)
+DEV void load_bias8(const bf16* cb, int c0, float (&b)[8]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) b[e] = cb ? (float)cb[c0 + e] : 0.f;
+}
+
+// bf16(v + b): the separate bias add after a bias-free convolution
+DEV void add_bias8(float (&v)[8], const float (&b)[8], bool on) {
+  if (on) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (float)(bf16)(v[e] + b[e]);
+  }
 }
 
 // The block's channel sums (acc: this thread's 8 channels at c0) into part[blk][C], then the
@@ -72,31 +93,52 @@ DEV void enc_block_sum(const EncArgs& a, const float (&acc)[8], int c0, int pix,
     for (int r = 0; r < ppi; ++r) s += red[r * nc + c];
     __hip_atomic_store(a.part + (int64_t)blk * nc + c, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // every writing wave's stores complete before the barrier (a release fence covers the issuing
-  // wave's own stores only), so the ticket below is taken after all of this block's partials
-  __threadfence();
+  // hand-off without an L2 write-back (siren_loss.hip, sse_fwd_kernel): write-through (relaxed
+  // agent-scope = sc1) stores of the block's row drained by every writing lane, a barrier, then one
+  // relaxed agent-scope ticket; the last block reads the rows with sc1 loads
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __shared__ unsigned last;
   __syncthreads();
-  if (tid == 0) {
-    last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
-  }
+  if (tid == 0) last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
   __syncthreads();
   if (!last) return;
-  __atomic_thread_fence(__ATOMIC_ACQUIRE);
-  // ncol output columns: column k sums part[b][k % nc] over the blocks b whose rows carry it
-  // (every block for the channel sums; blocks of image k / nc for pixfc_fwd)
-  for (int k = tid; k < ncol; k += 256) {
+  // The rows are read eight loads at a time before any is added (a chain of single sc1 loads made
+  // this tail 0.2-0.5 ms), in a fixed order: deterministic.
+  auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  auto sum_rows = [&](const float* src, unsigned b0, unsigned b1, int64_t stride) {
     float s = 0.f;
-    if (ncol == nc) {
-      for (unsigned b = 0; b < nblk; ++b)
-        s += __hip_atomic_load(a.part + (int64_t)b * nc + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      const int img = k / nc, c = k - img * nc;
-      for (unsigned b = 0; b < gridDim.x; ++b)
-        s += __hip_atomic_load(a.part + ((int64_t)img * gridDim.x + b) * nc + c, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+    unsigned b = b0;
+    for (; b + 8 <= b1; b += 8) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = ld(src + (int64_t)(b + k) * stride);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += v[k];
     }
-    dst[k] = addend ? s + *addend : s;
+    for (; b < b1; ++b) s += ld(src + (int64_t)b * stride);
+    return s;
+  };
+  if (ncol == nc) {
+    // 256 / C threads per column, each a contiguous range of block rows, then those ranges in order
+    const int tpc = 256 / nc, c = tid % nc, q = tid / nc;
+    const unsigned per = (nblk + tpc - 1) / tpc;
+    const unsigned b0 = q * per < nblk ? q * per : nblk, b1 = b0 + per < nblk ? b0 + per : nblk;
+    const float s = sum_rows(a.part + c, b0, b1, nc);
+    __syncthreads();
+    red[tid] = s;
+    __syncthreads();
+    if (tid < nc) {
+      float t = 0.f;
+      for (int k = 0; k < tpc; ++k) t += red[k * nc + tid];
+      dst[tid] = addend ? t + *addend : t;
+    }
+  } else {
+    // pixfc_fwd: column k = (image, channel) sums that image's gridDim.x block rows
+    for (int k = tid; k < ncol; k += 256) {
+      const int img = k / nc, c = k - img * nc;
+      const float s = sum_rows(a.part + (int64_t)img * gridDim.x * nc + c, 0, gridDim.x, nc);
+      dst[k] = addend ? s + *addend : s;
+    }
   }
   if (tid == 0) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -110,34 +152,53 @@ __global__ __launch_bounds__(256) void enc_relu_bwd_kernel(EncArgs a) {
   float acc[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] = 0.f;
-  for (int64_t p = p0 + pix; p < p1; p += ppi) {
-    const int64_t off = p * a.C + c0;
-    float g[8], m[8];
-    load_bf16x8(a.g1 + off, g);
-    if (a.g2) {
-      float g2[8];
-      load_bf16x8(a.g2 + off, g2);
+  // ENC_U pixels per thread per iteration, every load issued before the first store (more bytes
+  // in flight: one pixel per iteration ran at ~3 TB/s)
+  for (int64_t p = p0 + pix; p < p1; p += ENC_U * ppi) {
+    float g[ENC_U][8], m[ENC_U][8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) g[e] += g2[e];
-    }
-    load_bf16x8(a.y + off, m);
-    bf16x8 o;
+    for (int u = 0; u < ENC_U; ++u) {
+      const int64_t q = p + u * ppi;
+      if (q < p1) {
+        const int64_t off = q * a.C + c0;
+        load_bf16x8(a.g1 + off, g[u]);
+        if (a.g2) {
+          float g2[8];
+          load_bf16x8(a.g2 + off, g2);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      o[e] = (bf16)(m[e] > 0.f ? g[e] : 0.f);
-      acc[e] += (float)o[e];
+          for (int e = 0; e < 8; ++e) g[u][e] += g2[e];
+        }
+        load_bf16x8(a.y + off, m[u]);
+      }
     }
-    *(bf16x8*)(a.out + off) = o;
+#pragma unroll
+    for (int u = 0; u < ENC_U; ++u) {
+      const int64_t q = p + u * ppi;
+      if (q < p1) {
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          o[e] = (bf16)(m[u][e] > 0.f ? g[u][e] : 0.f);
+          acc[e] += (float)o[e];
+        }
+        *(bf16x8*)(a.out + q * a.C + c0) = o;
+      }
+    }
   }
   if (a.db) enc_block_sum(a, acc, c0, pix, ppi, a.C, a.db, nullptr);
 }
 
-// out = relu(relu(a) + x), x = g1 (the block input)
+// out = relu(relu(bf16(a + cb)) + x), x = g1 (the block input)
 __global__ __launch_bounds__(256) void enc_res_fwd_kernel(EncArgs a) {
   const int64_t n8 = a.P * a.C / 8;
+  // the grid stride is a multiple of C / 8, so a thread's channel group is fixed
+  const int c0 = (int)((8 * ((int64_t)blockIdx.x * 256 + threadIdx.x)) % a.C);
+  float bb[8];
+  load_bias8(a.cb, c0, bb);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
     float v[8], x[8];
     load_bf16x8(a.a + 8 * i, v);
+    add_bias8(v, bb, a.cb != nullptr);
     load_bf16x8(a.g1 + 8 * i, x);
     bf16x8 o;
 #pragma unroll
@@ -150,36 +211,68 @@ __global__ __launch_bounds__(256) void enc_res_fwd_kernel(EncArgs a) {
   }
 }
 
+// y = relu(bf16(y + cb)) in place (a bias-free convolution's bias add and its ReLU, one pass)
+__global__ __launch_bounds__(256) void enc_bias_relu_kernel(EncArgs a) {
+  const int64_t n8 = a.P * a.C / 8;
+  const int c0 = (int)((8 * ((int64_t)blockIdx.x * 256 + threadIdx.x)) % a.C);
+  float bb[8];
+  load_bias8(a.cb, c0, bb);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    float v[8];
+    load_bf16x8(a.out + 8 * i, v);
+    add_bias8(v, bb, a.cb != nullptr);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)fmaxf(v[e], 0.f);
+    *(bf16x8*)(a.out + 8 * i) = o;
+  }
+}
+
 // s = (g1 [+ g2]) * (out > 0) -> out (the skip's gradient); ga = s * (a > 0) -> out2; db = sum ga
 __global__ __launch_bounds__(256) void enc_res_bwd_kernel(EncArgs a) {
   const int tpp = a.C / 8, ppi = 256 / tpp;
   const int pix = threadIdx.x / tpp, c0 = 8 * (threadIdx.x % tpp);
   const int64_t p0 = (int64_t)blockIdx.x * a.chunk;
   const int64_t p1 = p0 + a.chunk < a.P ? p0 + a.chunk : a.P;
-  float acc[8];
+  float acc[8], bb[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] = 0.f;
-  for (int64_t p = p0 + pix; p < p1; p += ppi) {
-    const int64_t off = p * a.C + c0;
-    float g[8], mo[8], ma[8];
-    load_bf16x8(a.g1 + off, g);
-    if (a.g2) {
-      float g2[8];
-      load_bf16x8(a.g2 + off, g2);
+  load_bias8(a.cb, c0, bb);
+  for (int64_t p = p0 + pix; p < p1; p += ENC_U * ppi) {
+    float g[ENC_U][8], mo[ENC_U][8], ma[ENC_U][8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) g[e] += g2[e];
-    }
-    load_bf16x8(a.y + off, mo);
-    load_bf16x8(a.a + off, ma);
-    bf16x8 s, ga;
+    for (int u = 0; u < ENC_U; ++u) {
+      const int64_t q = p + u * ppi;
+      if (q < p1) {
+        const int64_t off = q * a.C + c0;
+        load_bf16x8(a.g1 + off, g[u]);
+        if (a.g2) {
+          float g2[8];
+          load_bf16x8(a.g2 + off, g2);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      s[e] = (bf16)(mo[e] > 0.f ? g[e] : 0.f);
-      ga[e] = ma[e] > 0.f ? s[e] : (bf16)0.f;
-      acc[e] += (float)ga[e];
+          for (int e = 0; e < 8; ++e) g[u][e] += g2[e];
+        }
+        load_bf16x8(a.y + off, mo[u]);
+        load_bf16x8(a.a + off, ma[u]);
+      }
     }
-    *(bf16x8*)(a.out + off) = s;
-    *(bf16x8*)(a.out2 + off) = ga;
+#pragma unroll
+    for (int u = 0; u < ENC_U; ++u) {
+      const int64_t q = p + u * ppi;
+      if (q < p1) {
+        add_bias8(ma[u], bb, a.cb != nullptr);
+        bf16x8 sk, ga;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          sk[e] = (bf16)(mo[u][e] > 0.f ? g[u][e] : 0.f);
+          ga[e] = ma[u][e] > 0.f ? sk[e] : (bf16)0.f;
+          acc[e] += (float)ga[e];
+        }
+        const int64_t off = q * a.C + c0;
+        *(bf16x8*)(a.out + off) = sk;
+        *(bf16x8*)(a.out2 + off) = ga;
+      }
+    }
   }
   if (a.db) enc_block_sum(a, acc, c0, pix, ppi, a.C, a.db, nullptr);
 }
@@ -192,12 +285,14 @@ __global__ __launch_bounds__(256) void enc_pixfc_fwd_kernel(EncArgs a) {
   const int64_t p0 = (int64_t)blockIdx.x * a.chunk;
   const int64_t p1 = p0 + a.chunk < a.P ? p0 + a.chunk : a.P;
   const bf16* src = a.a + b * a.P * a.C;
-  float acc[8];
+  float acc[8], bb[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  load_bias8(a.cb, c0, bb);
   for (int64_t p = p0 + pix; p < p1; p += ppi) {
     float v[8];
     load_bf16x8(src + p * a.C + c0, v);
+    add_bias8(v, bb, a.cb != nullptr);
     const float wp = a.w[p];
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] = fmaf(fmaxf(v[e], 0.f), wp, acc[e]);
@@ -212,9 +307,10 @@ __global__ __launch_bounds__(256) void enc_pixfc_bwd_kernel(EncArgs a) {
   const int pix = threadIdx.x / tpp, c0 = 8 * (threadIdx.x % tpp);
   const int64_t p0 = (int64_t)blockIdx.x * a.chunk;
   const int64_t p1 = p0 + a.chunk < a.P ? p0 + a.chunk : a.P;
-  float acc[8];
+  float acc[8], bb[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  load_bias8(a.cb, c0, bb);
   for (int64_t p = p0 + pix; p < p1; p += ppi) {
     const float wp = a.w[p];
     float gw = 0.f;
@@ -222,6 +318,7 @@ __global__ __launch_bounds__(256) void enc_pixfc_bwd_kernel(EncArgs a) {
       const int64_t off = ((int64_t)b * a.P + p) * a.C + c0;
       float v[8];
       load_bf16x8(a.a + off, v);
+      add_bias8(v, bb, a.cb != nullptr);
       const f32x4 g0 = *(const f32x4*)(a.gin + (int64_t)b * a.C + c0);
       const f32x4 g1 = *(const f32x4*)(a.gin + (int64_t)b * a.C + c0 + 4);
       bf16x8 o;

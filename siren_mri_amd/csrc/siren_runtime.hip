@@ -18,6 +18,7 @@
 #include "siren_loss.hip"
 #include "siren_kspace.hip"
 #include "siren_encoder.hip"
+#include "siren_conv.hip"
 
 using namespace siren;
 
@@ -1693,6 +1694,12 @@ void siren_timing_disable(void) {
   g_timing = Timing();
 }
 
+int siren_adam_scalars_table(double* t, const float* table, int64_t n, float* out, void* stream) {
+  if (!t || !table || n < 1 || !out) return fail(SIREN_EINVAL, "adam_scalars_table: null pointer or empty table");
+  hipLaunchKernelGGL(adam_scalars_table_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, t, table, n, out);
+  return check_launch("adam_scalars_table");
+}
+
 int siren_adam_scalars(double* t, double lr, double beta1, double beta2, float* out, void* stream) {
   if (!t || !out) return fail(SIREN_EINVAL, "adam_scalars: null pointer");
   hipLaunchKernelGGL(adam_scalars_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, t, lr, beta1, beta2, out);
@@ -1725,6 +1732,42 @@ int enc_setup(EncArgs& a, int64_t P, int C, void* ws, int64_t ws_bytes, bool nee
 }
 }  // namespace
 
+int64_t siren_conv_wrw_workspace_bytes(int N, int H, int W) {
+  const int64_t rows = (int64_t)N * H;
+  const int64_t nsplit = std::max<int64_t>(1, std::min<int64_t>(25, rows));
+  return nsplit * CW_SLAB * 4;
+}
+
+int siren_conv_wrw_k5(const void* x, const void* dy, int N, int H, int W, int C, float* dw, void* ws, int64_t ws_bytes,
+                      void* stream) {
+  if (C != CW_C || N < 1 || H < 1 || W < CW_PX || W % CW_PX != 0)
+    return fail(SIREN_EINVAL, "conv_wrw_k5: needs C = %d and W a multiple of %d (C = %d, N = %d, H = %d, W = %d)", CW_C,
+                CW_PX, C, N, H, W);
+  if (!x || !dy || !dw) return fail(SIREN_EINVAL, "conv_wrw_k5: null pointer");
+  const int64_t rows = (int64_t)N * H;
+  const int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(25, rows));
+  if (!ws || ws_bytes < (int64_t)nsplit * CW_SLAB * 4)
+    return fail(SIREN_ENOSPACE, "conv_wrw_k5: workspace %lld < %lld bytes", (long long)ws_bytes,
+                (long long)nsplit * CW_SLAB * 4);
+  ConvWArgs a;
+  memset(&a, 0, sizeof(a));
+  a.x = (const bf16*)x;
+  a.dy = (const bf16*)dy;
+  a.part = (float*)ws;
+  a.dw = dw;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.nsplit = nsplit;
+  a.rows_per_split = cdiv(rows, nsplit);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(conv_wrw_k5_kernel, dim3((unsigned)nsplit, CW_K, 2), dim3(512), 0, st, a);
+  int rc = check_launch("conv_wrw_k5");
+  if (rc) return rc;
+  hipLaunchKernelGGL(conv_wrw_reduce_kernel, dim3((unsigned)cdiv(CW_SLAB, 256)), dim3(256), 0, st, a);
+  return check_launch("conv_wrw_reduce");
+}
+
 int siren_enc_relu_bwd(const void* g1, const void* g2, const void* y, void* out, float* db, int64_t P, int C, void* ws,
                        int64_t ws_bytes, void* stream) {
   EncArgs a;
@@ -1741,12 +1784,26 @@ int siren_enc_relu_bwd(const void* g1, const void* g2, const void* y, void* out,
   return check_launch("enc_relu_bwd");
 }
 
-int siren_enc_res_fwd(const void* a_pre, const void* x, void* out, int64_t P, int C, void* stream) {
+int siren_enc_bias_relu(void* y, const void* cb, int64_t P, int C, void* stream) {
+  EncArgs a;
+  int rc = enc_setup(a, P, C, nullptr, 0, false, 512, "enc_bias_relu");
+  if (rc) return rc;
+  if (!y) return fail(SIREN_EINVAL, "enc_bias_relu: null plane");
+  if (P == 0) return SIREN_OK;
+  a.out = (bf16*)y;
+  a.cb = (const bf16*)cb;
+  hipLaunchKernelGGL(enc_bias_relu_kernel, dim3((unsigned)std::min<int64_t>(cdiv(P * C / 8, 256), 8192)), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  return check_launch("enc_bias_relu");
+}
+
+int siren_enc_res_fwd(const void* a_pre, const void* cb, const void* x, void* out, int64_t P, int C, void* stream) {
   EncArgs a;
   int rc = enc_setup(a, P, C, nullptr, 0, false, 512, "enc_res_fwd");
   if (rc) return rc;
   if (!a_pre || !x || !out) return fail(SIREN_EINVAL, "enc_res_fwd: null plane");
   if (P == 0) return SIREN_OK;
+  a.cb = (const bf16*)cb;
   a.a = (const bf16*)a_pre;
   a.g1 = (const bf16*)x;
   a.out = (bf16*)out;
@@ -1755,8 +1812,8 @@ int siren_enc_res_fwd(const void* a_pre, const void* x, void* out, int64_t P, in
   return check_launch("enc_res_fwd");
 }
 
-int siren_enc_res_bwd(const void* g1, const void* g2, const void* out, const void* a_pre, void* gskip, void* ga,
-                      float* db, int64_t P, int C, void* ws, int64_t ws_bytes, void* stream) {
+int siren_enc_res_bwd(const void* g1, const void* g2, const void* out, const void* a_pre, const void* cb, void* gskip,
+                      void* ga, float* db, int64_t P, int C, void* ws, int64_t ws_bytes, void* stream) {
   EncArgs a;
   int rc = enc_setup(a, P, C, ws, ws_bytes, db != nullptr, 512, "enc_res_bwd");
   if (rc) return rc;
@@ -1766,6 +1823,7 @@ int siren_enc_res_bwd(const void* g1, const void* g2, const void* out, const voi
   a.g2 = (const bf16*)g2;
   a.y = (const bf16*)out;
   a.a = (const bf16*)a_pre;
+  a.cb = (const bf16*)cb;
   a.out = (bf16*)gskip;
   a.out2 = (bf16*)ga;
   a.db = db;
@@ -1773,10 +1831,10 @@ int siren_enc_res_bwd(const void* g1, const void* g2, const void* out, const voi
   return check_launch("enc_res_bwd");
 }
 
-int siren_enc_pixfc_fwd(const void* a_pre, const float* w, const float* bias, float* e, int B, int64_t P, int C,
-                        void* ws, int64_t ws_bytes, void* stream) {
+int siren_enc_pixfc_fwd(const void* a_pre, const void* cb, const float* w, const float* bias, float* e, int B,
+                        int64_t P, int C, void* ws, int64_t ws_bytes, void* stream) {
   EncArgs a;
-  int rc = enc_setup(a, P, C, ws, ws_bytes, true, 512, "enc_pixfc_fwd");
+  int rc = enc_setup(a, P, C, ws, ws_bytes, true, 1024, "enc_pixfc_fwd");
   if (rc) return rc;
   if (!a_pre || !w || !bias || !e || B < 1) return fail(SIREN_EINVAL, "enc_pixfc_fwd: null pointer or B < 1");
   const int64_t nchunk = cdiv(P, a.chunk);
@@ -1784,6 +1842,7 @@ int siren_enc_pixfc_fwd(const void* a_pre, const float* w, const float* bias, fl
     return fail(SIREN_EINVAL, "enc_pixfc_fwd: %lld blocks > %d", (long long)(nchunk * B), ENC_MAX_BLOCKS);
   if (P == 0) return fail(SIREN_EINVAL, "enc_pixfc_fwd: no pixels");
   a.a = (const bf16*)a_pre;
+  a.cb = (const bf16*)cb;
   a.w = w;
   a.bias = bias;
   a.e = e;
@@ -1792,15 +1851,16 @@ int siren_enc_pixfc_fwd(const void* a_pre, const float* w, const float* bias, fl
   return check_launch("enc_pixfc_fwd");
 }
 
-int siren_enc_pixfc_bwd(const float* g, const void* a_pre, const float* w, void* ga, float* db, float* gw, int B,
-                        int64_t P, int C, void* ws, int64_t ws_bytes, void* stream) {
+int siren_enc_pixfc_bwd(const float* g, const void* a_pre, const void* cb, const float* w, void* ga, float* db,
+                        float* gw, int B, int64_t P, int C, void* ws, int64_t ws_bytes, void* stream) {
   EncArgs a;
-  int rc = enc_setup(a, P, C, ws, ws_bytes, true, 64, "enc_pixfc_bwd");
+  int rc = enc_setup(a, P, C, ws, ws_bytes, true, 128, "enc_pixfc_bwd");
   if (rc) return rc;
   if (!g || !a_pre || !w || !ga || !db || !gw || B < 1) return fail(SIREN_EINVAL, "enc_pixfc_bwd: null pointer or B < 1");
   if (P == 0) return fail(SIREN_EINVAL, "enc_pixfc_bwd: no pixels");
   a.gin = g;
   a.a = (const bf16*)a_pre;
+  a.cb = (const bf16*)cb;
   a.w = w;
   a.out = (bf16*)ga;
   a.db = db;
@@ -1949,11 +2009,6 @@ int siren_adam_step(const siren_adam_desc* d, void* stream) {
   a.step = d->step_size;
   a.bc2_sqrt = d->bias_correction2_sqrt;
   a.dev = d->dev_scalars;
-  a.tstep = d->dev_step;
-  if (d->dev_step && (!d->dev_table || d->table_n < 1))
-    return fail(SIREN_EINVAL, "adam: dev_step needs dev_table with table_n >= 1");
-  a.table = d->dev_table;
-  a.table_n = d->table_n;
   a.maximize = d->maximize;
   if (maxn == 0) return SIREN_OK;
   hipLaunchKernelGGL(adam_kernel, dim3(grid1d(maxn, 1024), (unsigned)d->num_tensors), dim3(256), 0,

@@ -5,9 +5,10 @@ The reference's autograd chain runs, around each convolution, a ReLU, its mask i
 bias-gradient reduction and the residual adds as separate passes over 134 MB planes (C4: 32 x 128^2
 x 128 channels in bf16), and the final Linear over the 16,384 pixels as a cast copy + GEMV. Here:
 
-  forward   conv (MIOpen, bf16 NHWC) + ReLU in place; each residual block's tail
-            relu(relu(a) + x) in one pass (siren_enc_res_fwd); relu_2 + the pixel Linear in one
-            reduction (siren_enc_pixfc_fwd, fp32 out).
+  forward   bias-free convolutions (MIOpen, bf16 NHWC; with a bias PyTorch adds it in a separate
+            pass) followed by one pass each: bias + ReLU in place (siren_enc_bias_relu), each
+            residual block's tail relu(relu(a + b) + x) (siren_enc_res_fwd), and the 1x1 conv's bias
+            + relu_2 + the pixel Linear as one reduction (siren_enc_pixfc_fwd, fp32 out).
   backward  the pixel Linear's three gradients and conv_1x1's ReLU mask + bias gradient in one pass
             (siren_enc_pixfc_bwd); each block's mask / skip / bias-gradient work in one pass
             (siren_enc_res_bwd, siren_enc_relu_bwd, the skip gradient added inside the next mask
@@ -68,7 +69,22 @@ def _conv(x, wb, bb, pad):
     return F.conv2d(x, wb, bb, padding=pad).contiguous(memory_format=_CL)
 
 
+_WGRAD_NATIVE = [True]
+
+
 def _wgrad(g, x, wb, pad):
+    """dL/dW of a stride-1 'same' convolution: the native MFMA kernel for the residual blocks'
+    128 -> 128 5x5 shape (siren_conv_wrw_k5, fp32 out in the filter's channels-last layout),
+    MIOpen's weight-gradient convolution otherwise."""
+    co, ci, k, _ = wb.shape
+    n, _, h, w = x.shape
+    if _WGRAD_NATIVE[0] and co == ci == 128 and k == 5 and w % 64 == 0:
+        lib = _native.lib()
+        dw = torch.empty(wb.shape, dtype=torch.float32, device=x.device, memory_format=_CL)
+        ws = torch.empty(int(lib.siren_conv_wrw_workspace_bytes(n, h, w)), dtype=torch.uint8, device=x.device)
+        _native.check(lib.siren_conv_wrw_k5(x.data_ptr(), g.data_ptr(), n, h, w, ci, dw.data_ptr(), ws.data_ptr(),
+                                            ws.numel(), _native.stream_handle(x.device)), "siren_conv_wrw_k5")
+        return dw
     return torch.ops.aten.convolution_backward(g, x, wb, None, [1, 1], [pad, pad], [1, 1], False, [0, 0], 1,
                                                [False, True, False])[1]
 
@@ -91,32 +107,40 @@ class _EncoderBF16(torch.autograd.Function):
         bbs = [c.bias.detach().to(torch.bfloat16) for c in convs]
         x0 = I.detach().to(torch.bfloat16).contiguous(memory_format=_CL)
         saved = [x0]
-        # conv_theta + relu, cnn[0] + relu
-        t = F.relu_(_conv(x0, wbs[0], bbs[0], convs[0].padding[0]))
+
+        def bias_relu(y, k):
+            P, C = _plane(y)
+            _native.check(lib.siren_enc_bias_relu(y.data_ptr(), bbs[k].data_ptr(), P, C, stream), "siren_enc_bias_relu")
+            return y
+
+        # conv_theta + bias + relu, cnn[0] + bias + relu (bias-free convolutions, the bias added in
+        # the ReLU pass)
+        t = bias_relu(_conv(x0, wbs[0], None, convs[0].padding[0]), 0)
         saved.append(t)
-        t = F.relu_(_conv(t, wbs[1], bbs[1], convs[1].padding[0]))
+        t = bias_relu(_conv(t, wbs[1], None, convs[1].padding[0]), 1)
         saved.append(t)
         k = 2
         for _ in range(enc._enc_nblocks):
-            h = F.relu_(_conv(t, wbs[k], bbs[k], convs[k].padding[0]))
-            a = _conv(h, wbs[k + 1], bbs[k + 1], convs[k + 1].padding[0])
+            h = bias_relu(_conv(t, wbs[k], None, convs[k].padding[0]), k)
+            a = _conv(h, wbs[k + 1], None, convs[k + 1].padding[0])  # bias added in the tail pass
             out = torch.empty_like(a)
             P, C = _plane(a)
-            _native.check(lib.siren_enc_res_fwd(a.data_ptr(), t.data_ptr(), out.data_ptr(), P, C, stream),
-                          "siren_enc_res_fwd")
+            _native.check(lib.siren_enc_res_fwd(a.data_ptr(), bbs[k + 1].data_ptr(), t.data_ptr(), out.data_ptr(), P,
+                                                C, stream), "siren_enc_res_fwd")
             saved += [h, a, out]
             t = out
             k += 2
-        a = _conv(t, wbs[k], bbs[k], convs[k].padding[0])  # the 1x1 conv; relu_2 is in the pixfc pass
+        a = _conv(t, wbs[k], None, convs[k].padding[0])  # the 1x1 conv; its bias and relu_2 in the pixfc pass
         saved.append(a)
         B = a.shape[0]
         P = a.shape[2] * a.shape[3]
         C = a.shape[1]
         fc = enc.fc
         e = torch.empty(B, C, dtype=torch.float32, device=dev)
-        _native.check(lib.siren_enc_pixfc_fwd(a.data_ptr(), fc.weight.detach().contiguous().data_ptr(),
+        _native.check(lib.siren_enc_pixfc_fwd(a.data_ptr(), bbs[k].data_ptr(), fc.weight.detach().contiguous().data_ptr(),
                                               fc.bias.detach().data_ptr(), e.data_ptr(), B, P, C, ws.data_ptr(),
                                               ws.numel(), stream), "siren_enc_pixfc_fwd")
+        ctx.bbs = bbs
         ctx.enc = enc
         ctx.wbs = wbs
         ctx.save_for_backward(*saved)
@@ -125,7 +149,7 @@ class _EncoderBF16(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, ge):
-        enc, convs, wbs = ctx.enc, ctx.convs, ctx.wbs
+        enc, convs, wbs, bbs = ctx.enc, ctx.convs, ctx.wbs, ctx.bbs
         nparams = 2 * len(convs) + 2
         if ge is None:
             return (None, None) + (None,) * nparams
@@ -147,8 +171,8 @@ class _EncoderBF16(torch.autograd.Function):
         k = len(convs) - 1
         gb[k] = torch.empty(C, dtype=torch.float32, device=dev)
         gfw = torch.empty(P, dtype=torch.float32, device=dev)
-        _native.check(lib.siren_enc_pixfc_bwd(gec.data_ptr(), a.data_ptr(), fc.weight.detach().contiguous().data_ptr(),
-                                              ga.data_ptr(), gb[k].data_ptr(), gfw.data_ptr(), B, P, C, wsp, wsn,
+        _native.check(lib.siren_enc_pixfc_bwd(gec.data_ptr(), a.data_ptr(), bbs[k].data_ptr(),
+                                              fc.weight.detach().contiguous().data_ptr(), ga.data_ptr(), gb[k].data_ptr(), gfw.data_ptr(), B, P, C, wsp, wsn,
                                               stream), "siren_enc_pixfc_bwd")
         g_fc_w = gfw.view_as(fc.weight)
         g_fc_b = gec.sum().reshape(fc.bias.shape)
@@ -169,7 +193,8 @@ class _EncoderBF16(torch.autograd.Function):
             ga = torch.empty_like(a)
             gb[k + 1] = torch.empty(C, dtype=torch.float32, device=dev)
             _native.check(lib.siren_enc_res_bwd(g1.data_ptr(), g2.data_ptr() if g2 is not None else None,
-                                                out.data_ptr(), a.data_ptr(), gskip.data_ptr(), ga.data_ptr(),
+                                                out.data_ptr(), a.data_ptr(), bbs[k + 1].data_ptr(), gskip.data_ptr(),
+                                                ga.data_ptr(),
                                                 gb[k + 1].data_ptr(), P, C, wsp, wsn, stream), "siren_enc_res_bwd")
             pad = convs[k + 1].padding[0]
             gW[k + 1] = _wgrad(ga, h, wbs[k + 1], pad)

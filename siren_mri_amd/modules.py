@@ -42,10 +42,44 @@ class BatchLinear(nn.Linear, MetaModule):
             params = OrderedDict(self.named_parameters())
         bias = params.get("bias", None)
         weight = params["weight"]
+        if (input.dim() == 2 and weight.dim() == 2 and bias is not None and bias.dim() == 1 and input.is_cuda
+                and weight.shape[0] >= _WIDE_OUT and input.shape[0] <= 256):
+            return _WideOutLinear.apply(input, weight, bias)
         out = input.matmul(weight.transpose(-1, -2))
         if bias is not None:
             out = out + bias.unsqueeze(-2)
         return out
+
+
+_WIDE_OUT = 8192
+
+
+class _WideOutLinear(torch.autograd.Function):
+    """input @ W^T + b for few rows and many outputs (the HyperNetwork's heads that emit a 256x256
+    hypo-weight: [B <= 256, 128] -> [B, 65536]). Same values as the matmul + add chain; its
+    backward's input gradient g @ W ([B, 65536] x [65536, 128]) has a long K and a 32 x 128 output,
+    which the library GEMM ran on 4 workgroups (0.24 ms); here it is split over K into a batched
+    GEMM of 32 chunks and summed (a fixed order)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return torch.addmm(b, x, w.t())
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            n_out = w.shape[0]
+            s = 32 if n_out % 32 == 0 else 1
+            gs = g.reshape(g.shape[0], s, n_out // s).transpose(0, 1)      # [s, B, K/s]
+            gx = torch.bmm(gs, w.reshape(s, n_out // s, w.shape[1])).sum(0)  # [B, in]
+        if ctx.needs_input_grad[1]:
+            gw = g.t().mm(x)
+        if ctx.needs_input_grad[2]:
+            gb = g.sum(0)
+        return gx, gw, gb
 
 
 class Sine(nn.Module):

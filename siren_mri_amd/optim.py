@@ -28,15 +28,16 @@ class Adam(torch.optim.Adam):
     """torch.optim.Adam whose step is one native launch (see the module docstring).
 
     ``enable_graph_mode()`` makes the step hipGraph-capturable: the bias corrections come from a
-    device-side step counter instead of host floats baked into the captured launch — advanced by
-    the Adam launch itself when a group fits one launch, else by siren_adam_scalars (one extra
-    single-thread launch). The host-side ``state['step']`` keeps counting
+    device-side step counter instead of host floats baked into the captured launch — one
+    single-thread launch per group advances it and looks the step's scalars up in a table the host
+    computed once (siren_adam_scalars_table), or computes them (siren_adam_scalars). The host-side ``state['step']`` keeps counting
     eager calls only; ``sync_graph_steps()`` copies the device counters back into it."""
 
     _graph_mode = False
     # graph mode: {step_size, bias_correction2_sqrt} of steps 1, 2, ... up to the step where both
     # bias corrections reach 1 in double (the eager path's expressions; later steps repeat the last
-    # entry); betas so close to 1 that this takes more than _TABLE_MAX steps use siren_adam_scalars
+    # entry; siren_adam_scalars_table); betas so close to 1 that this takes more than _TABLE_MAX
+    # steps use siren_adam_scalars (the same expressions computed on the device)
     _TABLE_MAX = 1 << 22
 
     @classmethod
@@ -64,7 +65,7 @@ class Adam(torch.optim.Adam):
             dev = getattr(self, "_dev_step", {}).get(id(group))
             if dev is None:
                 continue
-            t = float(dev[0][0].item())
+            t = float(dev[0].item())
             for p in group["params"]:
                 if p in self.state and "step" in self.state[p]:
                     self.state[p]["step"].fill_(t)
@@ -136,33 +137,31 @@ class Adam(torch.optim.Adam):
             if not params:
                 continue
             stream = ctypes.c_void_p(_native.stream_handle(params[0].device))
-            dev_scalars = dev_step = dev_table = None
+            dev_scalars = None
             if self._graph_mode:
                 if len(by_step) != 1:
                     raise RuntimeError("siren_mri_amd.optim.Adam: graph mode needs one step count per group")
                 dev = self._dev_step.get(id(group))
                 if dev is None:
                     t0 = next(iter(by_step)) - 1
-                    # {t, ticket}: the ticket's bits start (and stay, between launches) zero
-                    dev = (torch.tensor([t0, 0.0], dtype=torch.float64, device=params[0].device),
+                    dev = (torch.full((1,), t0, dtype=torch.float64, device=params[0].device),
                            torch.zeros(2, dtype=torch.float32, device=params[0].device))
                     self._dev_step[id(group)] = dev
-                tab = None
-                if len(params) <= _native.ADAM_MAX_TENSORS:
-                    key = (float(group["lr"]), float(beta1), float(beta2))
-                    tables = self.__dict__.setdefault("_tables", {})
-                    tab = tables.get(id(group))
-                    if tab is None or tab[0] != key:
-                        tab = (key, self._scalar_table(*key, params[0].device))
-                        tables[id(group)] = tab
-                if tab is not None and tab[1] is not None:
-                    dev_step = dev[0].data_ptr()  # one launch: it advances the counter itself
-                    dev_table = tab[1]
+                key = (float(group["lr"]), float(beta1), float(beta2))
+                tables = self.__dict__.setdefault("_tables", {})
+                tab = tables.get(id(group))
+                if tab is None or tab[0] != key:
+                    tab = (key, self._scalar_table(*key, params[0].device))
+                    tables[id(group)] = tab
+                if tab[1] is not None:
+                    rc = lib.siren_adam_scalars_table(dev[0].data_ptr(), tab[1].data_ptr(), tab[1].shape[0],
+                                                      dev[1].data_ptr(), stream)
                 else:
-                    if lib.siren_adam_scalars(dev[0].data_ptr(), float(group["lr"]), float(beta1), float(beta2),
-                                              dev[1].data_ptr(), stream) != 0:
-                        raise _native.NativeError(_native.last_error())
-                    dev_scalars = dev[1].data_ptr()
+                    rc = lib.siren_adam_scalars(dev[0].data_ptr(), float(group["lr"]), float(beta1), float(beta2),
+                                                dev[1].data_ptr(), stream)
+                if rc != 0:
+                    raise _native.NativeError(_native.last_error())
+                dev_scalars = dev[1].data_ptr()
             for t, plist in by_step.items():
                 bc1 = 1 - beta1 ** t
                 bc2 = 1 - beta2 ** t
@@ -177,9 +176,6 @@ class Adam(torch.optim.Adam):
                     d.step_size = (group["lr"] / bc1) * -1
                     d.bias_correction2_sqrt = bc2 ** 0.5
                     d.dev_scalars = dev_scalars
-                    d.dev_step = dev_step
-                    d.dev_table = dev_table.data_ptr() if dev_table is not None else None
-                    d.table_n = dev_table.shape[0] if dev_table is not None else 0
                     for k, p in enumerate(chunk):
                         st = self.state[p]
                         d.numel[k] = p.numel()

@@ -99,11 +99,11 @@ def test_native_passes_deterministic():
         lib.siren_enc_relu_bwd(g1.data_ptr(), None, a.data_ptr(), out.data_ptr(), db.data_ptr(), B * P, C, ws.data_ptr(),
                                ws.numel(), st)
         e = torch.empty(B, C, device=DEV)
-        lib.siren_enc_pixfc_fwd(a.data_ptr(), w.data_ptr(), bias.data_ptr(), e.data_ptr(), B, P, C, ws.data_ptr(),
-                                ws.numel(), st)
+        lib.siren_enc_pixfc_fwd(a.data_ptr(), None, w.data_ptr(), bias.data_ptr(), e.data_ptr(), B, P, C,
+                                ws.data_ptr(), ws.numel(), st)
         ga, db2, gw = torch.empty_like(a), torch.empty(C, device=DEV), torch.empty(P, device=DEV)
-        lib.siren_enc_pixfc_bwd(gin.data_ptr(), a.data_ptr(), w.data_ptr(), ga.data_ptr(), db2.data_ptr(), gw.data_ptr(),
-                                B, P, C, ws.data_ptr(), ws.numel(), st)
+        lib.siren_enc_pixfc_bwd(gin.data_ptr(), a.data_ptr(), None, w.data_ptr(), ga.data_ptr(), db2.data_ptr(),
+                                gw.data_ptr(), B, P, C, ws.data_ptr(), ws.numel(), st)
         res.append((db, e, db2, gw))
     torch.cuda.synchronize()
     for r in res[1:]:
@@ -134,15 +134,20 @@ def test_relu_bwd_and_res_passes_against_torch(C, P):
     torch.testing.assert_close(db, ref.float().sum(0), rtol=1e-5, atol=1e-4)
     # res fwd / bwd
     o = torch.empty_like(a)
-    _native.check(lib.siren_enc_res_fwd(a.data_ptr(), x.data_ptr(), o.data_ptr(), P, C, st), "res_fwd")
-    assert torch.equal(o, torch.relu(torch.relu(a) + x))
+    cb = torch.randn(C, generator=g).to(DEV).to(torch.bfloat16)
+    ab = a + cb  # bf16 add: the conv + bias-add chain's rounding
+    _native.check(lib.siren_enc_res_fwd(a.data_ptr(), cb.data_ptr(), x.data_ptr(), o.data_ptr(), P, C, st), "res_fwd")
+    assert torch.equal(o, torch.relu(torch.relu(ab) + x))
     gs, ga = torch.empty_like(a), torch.empty_like(a)
-    _native.check(lib.siren_enc_res_bwd(g1.data_ptr(), None, o.data_ptr(), a.data_ptr(), gs.data_ptr(), ga.data_ptr(),
-                                        db.data_ptr(), P, C, ws.data_ptr(), ws.numel(), st), "res_bwd")
+    _native.check(lib.siren_enc_res_bwd(g1.data_ptr(), None, o.data_ptr(), a.data_ptr(), cb.data_ptr(), gs.data_ptr(),
+                                        ga.data_ptr(), db.data_ptr(), P, C, ws.data_ptr(), ws.numel(), st), "res_bwd")
     s_ref = g1 * (o > 0)
     assert torch.equal(gs, s_ref)
-    assert torch.equal(ga, s_ref * (a > 0))
+    assert torch.equal(ga, s_ref * (ab > 0))
     torch.testing.assert_close(db, ga.float().sum(0), rtol=1e-5, atol=1e-4)
+    yb = a.clone()
+    _native.check(lib.siren_enc_bias_relu(yb.data_ptr(), cb.data_ptr(), P, C, st), "bias_relu")
+    assert torch.equal(yb, torch.relu(ab))
 
 
 def test_pixel_linear_passes_against_torch():
@@ -154,20 +159,47 @@ def test_pixel_linear_passes_against_torch():
     P = H * H
     g = torch.Generator().manual_seed(9)
     a = torch.randn(B, H, H, C, generator=g).to(DEV).to(torch.bfloat16)
+    a_raw = a
     w = (torch.randn(P, generator=g) / 128).to(DEV)
     bias = torch.randn(1, generator=g).to(DEV)
     e = torch.empty(B, C, device=DEV)
-    _native.check(lib.siren_enc_pixfc_fwd(a.data_ptr(), w.data_ptr(), bias.data_ptr(), e.data_ptr(), B, P, C,
-                                          ws.data_ptr(), ws.numel(), st), "pixfc_fwd")
+    cb = torch.randn(C, generator=g).to(DEV).to(torch.bfloat16)
+    _native.check(lib.siren_enc_pixfc_fwd(a.data_ptr(), cb.data_ptr(), w.data_ptr(), bias.data_ptr(), e.data_ptr(), B,
+                                          P, C, ws.data_ptr(), ws.numel(), st), "pixfc_fwd")
+    a = a + cb  # the reference below sees the biased pre-activation
     r = torch.relu(a.float()).reshape(B, P, C)
     torch.testing.assert_close(e, torch.einsum("bpc,p->bc", r, w) + bias, rtol=1e-4, atol=1e-4)
     gin = torch.randn(B, C, generator=g).to(DEV)
     ga = torch.empty_like(a)
     db = torch.empty(C, device=DEV)
     gw = torch.empty(P, device=DEV)
-    _native.check(lib.siren_enc_pixfc_bwd(gin.data_ptr(), a.data_ptr(), w.data_ptr(), ga.data_ptr(), db.data_ptr(),
-                                          gw.data_ptr(), B, P, C, ws.data_ptr(), ws.numel(), st), "pixfc_bwd")
+    _native.check(lib.siren_enc_pixfc_bwd(gin.data_ptr(), a_raw.data_ptr(),
+                                          cb.data_ptr(), w.data_ptr(), ga.data_ptr(), db.data_ptr(), gw.data_ptr(), B, P,
+                                          C, ws.data_ptr(), ws.numel(), st), "pixfc_bwd")
     ga_ref = ((a.float() > 0) * gin[:, None, None, :] * w.reshape(1, H, H, 1)).to(torch.bfloat16)
     assert torch.equal(ga, ga_ref)
     torch.testing.assert_close(db, ga_ref.float().sum((0, 1, 2)), rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(gw, torch.einsum("bc,bpc->p", gin, r), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 128, 128), (3, 7, 64), (1, 1, 192)])
+def test_conv_weight_gradient_kernel_against_fp32(N, H, W):
+    """siren_conv_wrw_k5 (the residual blocks' 128 -> 128 5x5 weight gradient) against the fp32
+    weight gradient of the same bf16 operands (exact products; fp32 sums in another order)."""
+    from siren_mri_amd import _native
+    lib = _native.lib()
+    g = torch.Generator().manual_seed(N * 1000 + H + W)
+    x = torch.randn(N, 128, H, W, generator=g).to(torch.bfloat16)
+    dy = torch.randn(N, 128, H, W, generator=g).to(torch.bfloat16)
+    ref = torch.nn.grad.conv2d_weight(x.double(), (128, 128, 5, 5), dy.double(), padding=2).float()
+    xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
+    dyd = dy.to(DEV).contiguous(memory_format=torch.channels_last)
+    dw = torch.empty(128, 128, 5, 5, device=DEV).contiguous(memory_format=torch.channels_last)
+    ws = torch.empty(int(lib.siren_conv_wrw_workspace_bytes(N, H, W)), dtype=torch.uint8, device=DEV)
+    _native.check(lib.siren_conv_wrw_k5(xd.data_ptr(), dyd.data_ptr(), N, H, W, 128, dw.data_ptr(), ws.data_ptr(),
+                                        ws.numel(), _native.stream_handle(DEV)), "conv_wrw")
+    assert orc.norm_rel(dw.cpu(), ref) < 1e-6
+    dw2 = torch.empty_like(dw)
+    _native.check(lib.siren_conv_wrw_k5(xd.data_ptr(), dyd.data_ptr(), N, H, W, 128, dw2.data_ptr(), ws.data_ptr(),
+                                        ws.numel(), _native.stream_handle(DEV)), "conv_wrw")
+    assert torch.equal(dw, dw2)

@@ -132,3 +132,26 @@ def test_hypo256_batched_against_reference_fixture(precision, tol):
     norms = np.array([[params[f"net.net.{i}.0.weight"].grad.norm().item(),
                        params[f"net.net.{i}.0.bias"].grad.norm().item()] for i in range(5)])
     np.testing.assert_allclose(norms, d["grad_norms"], rtol=tg)
+
+
+def test_wide_output_linear_matches_matmul_chain():
+    """BatchLinear's wide-output form (the HyperNetwork heads emitting a 256x256 hypo-weight):
+    forward and all three gradients equal the matmul + add chain to fp32 rounding."""
+    from siren_mri_amd import modules
+    torch.manual_seed(0)
+    lin = modules.BatchLinear(128, 65536).to(DEV)
+    x = torch.randn(32, 128, device=DEV, requires_grad=True)
+    g = torch.randn(32, 65536, device=DEV)
+    y = lin(x)
+    y.backward(g)
+    gx, gw, gb = x.grad.clone(), lin.weight.grad.clone(), lin.bias.grad.clone()
+    x2 = x.detach().clone().requires_grad_(True)
+    w2 = lin.weight.detach().clone().requires_grad_(True)
+    b2 = lin.bias.detach().clone().requires_grad_(True)
+    y2 = x2.matmul(w2.t()) + b2.unsqueeze(-2)
+    y2.backward(g)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    assert orc.norm_rel(y.detach().cpu(), y2.detach().cpu()) < 1e-6
+    assert orc.norm_rel(gx.cpu(), x2.grad.cpu()) < 1e-5
+    assert orc.norm_rel(gw.cpu(), w2.grad.cpu()) < 1e-6
+    assert orc.norm_rel(gb.cpu(), b2.grad.cpu()) < 1e-6

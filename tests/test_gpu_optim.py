@@ -48,7 +48,7 @@ def test_adam_state_dict_round_trip_with_torch():
 def test_adam_graph_mode_replay_matches_eager(sizes):
     """enable_graph_mode(): bias corrections from a device step counter, so a hipGraph of the
     step replays with the right t each time (same values as eager steps). One launch per group:
-    the launch advances the counter itself (the last of its workgroups; (300000, ...) runs 293)."""
+    a single-thread launch per step advances the counter and looks the scalars up in a table."""
     from siren_mri_amd.optim import Adam
     g = torch.Generator().manual_seed(1)
     inits = [torch.randn(n, generator=g) for n in sizes]
