@@ -250,6 +250,13 @@ int64_t siren_enc_workspace_bytes(void);
  * (siren_conv_wrw_workspace_bytes) added in split order (deterministic). Replaces the convolution
  * weight-gradient of the encoder's autograd chain. */
 int64_t siren_conv_wrw_workspace_bytes(int N, int H, int W);
+/* Forward convolution of the same shape, bf16 NHWC x [N][H][128][128] (H even) and filter w
+ * [128 out][5][5][128 in] (channels-last) -> bf16 y, fp32 accumulation; with bias ([128] bf16)
+ * y = bf16(bf16(acc) + bias) (then ReLU if relu), the rounding of the conv + bias-add chain. The
+ * input gradient of such a convolution is this one on the flipped, transposed filter. Replaces
+ * the encoder's MIOpen forward / input-gradient convolutions for this shape. */
+int siren_conv_fwd_k5(const void* x, const void* w, const void* bias, int relu, void* y, int N, int H, int W, int C,
+                      void* stream);
 int siren_conv_wrw_k5(const void* x, const void* dy, int N, int H, int W, int C, float* dw, void* ws, int64_t ws_bytes,
                       void* stream);
 int siren_enc_relu_bwd(const void* g1, const void* g2, const void* y, void* out, float* db, int64_t P, int C, void* ws,

@@ -182,3 +182,202 @@ __global__ __launch_bounds__(256) void conv_wrw_reduce_kernel(ConvWArgs a) {
 }
 
 }  // namespace siren
+
+namespace siren {
+
+// ------------------------------------------------------------------------------------------
+// conv_fwd_k5: y = conv(x, W) for the same 128 -> 128, 5x5, stride-1, padding-2 shape, bf16 NHWC
+// in and out, fp32 accumulation (the residual blocks' forward convolutions, and their input
+// gradients as forward convolutions of the flipped, transposed filter W'[ci][kh][kw][co] =
+// W[co][4 - kh][4 - kw][ci] — the same layout, so one kernel serves both).
+//
+//   y[n][h][w][co] = sum_{kh, kw, ci} x[n][h + kh - 2][w + kw - 2][ci] W[co][kh][kw][ci]  (0 outside)
+//
+// Workgroup tile: two output image rows (256 pixels when W = 128) x all 128 output channels, as
+// D[co][px] = W . X^T on the bf16 MFMA (A = filter rows, B = pixel channel vectors: both operands
+// are 16-byte LDS reads of 8 consecutive input channels). Wave w holds co half w & 1 and pixel
+// quarter w >> 1: four 32 x 32 accumulator blocks. K loop: 20 stages (filter row kh x 32-channel
+// chunk cc); a stage holds the two input rows h0 + kh - 2, h0 + kh - 1 (132 px with the zero halo)
+// and the 5 x 128 filter rows of that chunk in LDS (rows padded to 80 bytes), and runs 5 taps x 2
+// K steps of MFMAs; the next stage's global loads are in flight meanwhile (two register sets,
+// compile-time selected, two LDS stages). Epilogue: bf16(acc) (optionally + bias, ReLU: the bias
+// add and the ReLU of the conv + bias + ReLU chain, same rounding) through LDS to coalesced
+// 16-byte stores.
+// ------------------------------------------------------------------------------------------
+constexpr int CF_W = 128;                    // image width (pixels per row), fixed
+constexpr int CF_HALO = CF_W + CW_K - 1;     // 132
+constexpr int CF_CC = 32;                    // input channels per stage
+constexpr int CF_ROWB = 80;                  // bytes per LDS row (32 bf16 + 16 pad)
+constexpr int CF_XB = 2 * CF_HALO * CF_ROWB;         // x part of a stage (21,120 B)
+constexpr int CF_WB = CW_K * CW_C * CF_ROWB;          // filter part (51,200 B)
+constexpr int CF_STAGE = CF_XB + CF_WB;               // 72,320 B
+constexpr int CF_XP = 2 * CF_HALO * 4;                // 16-byte x pieces per stage (1056)
+constexpr int CF_WP = CW_K * CW_C * 4;                // filter pieces (2560)
+constexpr int CF_NL = (CF_XP + CF_WP + 511) / 512;    // loads per thread per stage (8)
+
+struct ConvFArgs {
+  const bf16* x;     // [N][H][128][128]
+  const bf16* w;     // [128 out][5][5][128 in]
+  const bf16* bias;  // [128] or null
+  bf16* y;           // [N][H][128][128]
+  int N, H;
+  int relu;          // with bias: y = relu(bf16(bf16(acc) + bias))
+};
+
+__global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem_cf[2 * CF_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wc = wave & 1, wp = wave >> 1;
+  const int hp = a.H / 2;  // row pairs per image (H even)
+  const int n = blockIdx.x / hp, h0 = 2 * (blockIdx.x % hp);
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  // stage s = (kh = s / 4, cc = s % 4). Piece q < CF_XP: x row r = q / (4 * CF_HALO) of the pair,
+  // halo pixel j = (q / 4) % CF_HALO, 16-byte channel piece q % 4; else filter piece
+  // q' = q - CF_XP: tap kw = q' / 512, out channel (q' / 4) % 128, piece q' % 4.
+  u32x4_t lv[2][CF_NL];
+  const u32x4_t zero = {0u, 0u, 0u, 0u};
+  auto load = [&](int s, auto set_c) {
+    constexpr int set = decltype(set_c)::value;
+    const int kh = s >> 2, cc = s & 3;
+#pragma unroll
+    for (int i = 0; i < CF_NL; ++i) {
+      const int q = tid + 512 * i;
+      u32x4_t v = zero;
+      if (q < CF_XP) {
+        const int r = q / (4 * CF_HALO), j = (q >> 2) % CF_HALO, pc = q & 3;
+        const int xr = h0 + r + kh - CW_K / 2, w = j - CW_K / 2;
+        if (xr >= 0 && xr < a.H && w >= 0 && w < CF_W)
+          v = *(const u32x4_t*)(a.x + (((int64_t)n * a.H + xr) * CF_W + w) * CW_C + CF_CC * cc + 8 * pc);
+      } else if (q < CF_XP + CF_WP) {
+        const int q2 = q - CF_XP, kw = q2 >> 9, co = (q2 >> 2) & 127, pc = q2 & 3;
+        v = *(const u32x4_t*)(a.w + ((int64_t)(co * CW_K + kh) * CW_K + kw) * CW_C + CF_CC * cc + 8 * pc);
+      }
+      lv[set][i] = v;
+    }
+  };
+  auto stage = [&](auto set_c, int buf) {
+    constexpr int set = decltype(set_c)::value;
+    char* base = smem_cf + buf * CF_STAGE;
+#pragma unroll
+    for (int i = 0; i < CF_NL; ++i) {
+      const int q = tid + 512 * i;
+      if (q < CF_XP) {
+        const int r = q / (4 * CF_HALO), j = (q >> 2) % CF_HALO, pc = q & 3;
+        *(u32x4_t*)(base + (r * CF_HALO + j) * CF_ROWB + 16 * pc) = lv[set][i];
+      } else if (q < CF_XP + CF_WP) {
+        const int q2 = q - CF_XP, kw = q2 >> 9, co = (q2 >> 2) & 127, pc = q2 & 3;
+        *(u32x4_t*)(base + CF_XB + (kw * CW_C + co) * CF_ROWB + 16 * pc) = lv[set][i];
+      }
+    }
+  };
+
+  // operand reads: A (filter) lane -> out channel 64 wc + 32 i + (lane & 31), channels 8 (lane >> 5)
+  // (+16 for the second K step); B (pixels) lane -> pixel 64 wp + 32 j + (lane & 31) of the pair
+  // (row (pixel >> 7), column pixel & 127), the tap's halo column + kw
+  const int l32 = lane & 31, kh2 = lane >> 5;
+  uint32_t aoff[2], boff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) aoff[i] = CF_XB + (64 * wc + 32 * i + l32) * CF_ROWB + 16 * kh2;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int px = 64 * wp + 32 * j + l32;
+    boff[j] = ((px >> 7) * CF_HALO + (px & 127)) * CF_ROWB + 16 * kh2;
+  }
+  const uint32_t sbase = lds_addr(smem_cf);
+
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  constexpr int NS = CW_K * 4;
+  load(0, S0{});
+  stage(S0{}, 0);
+  load(1, S1{});
+  __syncthreads();
+  auto iter = [&](int s, auto par_c) {
+    constexpr int par = decltype(par_c)::value;
+    using SN = std::integral_constant<int, par ^ 1>;
+    using SC = std::integral_constant<int, par>;
+    if (s + 1 < NS) stage(SN{}, (s + 1) & 1);
+    if (s + 2 < NS) load(s + 2, SC{});
+    const uint32_t sb = sbase + (s & 1) * CF_STAGE;
+    static_for<0, CW_K>([&](auto kw_c) {
+      constexpr int kw = decltype(kw_c)::value;
+      static_for<0, 2>([&](auto ks_c) {
+        constexpr int ks = decltype(ks_c)::value;
+        bf16x8 af[2], bfr[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(af[i]) : "v"(sb + aoff[i]), "n"(kw * CW_C * CF_ROWB + 32 * ks));
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bfr[j]) : "v"(sb + boff[j]), "n"(kw * CF_ROWB + 32 * ks));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(bfr[0]), "+v"(bfr[1]));
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      });
+    });
+    __syncthreads();
+  };
+  for (int s = 0; s < NS; s += 2) {
+    iter(s, S0{});
+    iter(s + 1, S1{});
+  }
+
+  // epilogue: D[co][px] -> LDS tile [256 px][128 co] bf16 (rows of 256 + 16 bytes), then 16-byte
+  // stores of whole pixel rows
+  constexpr int OROW = CW_C * 2 + 16;
+  char* ot = smem_cf;
+  float bia[2][16];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int co = 64 * wc + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * kh2;
+      bia[i][e] = a.bias ? (float)a.bias[co] : 0.f;
+    }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int px = 64 * wp + 32 * j + l32;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float z = (float)(bf16)acc[i][j][4 * g + e];
+          if (a.bias) {
+            z = (float)(bf16)(z + bia[i][4 * g + e]);
+            if (a.relu) z = fmaxf(z, 0.f);
+          }
+          v[e] = (bf16)z;
+        }
+        const int co = 64 * wc + 32 * i + 8 * g + 4 * kh2;
+        *(bf16x4*)(ot + px * OROW + co * 2) = v;
+      }
+    }
+  __syncthreads();
+  // the pair's 64 KB as 16-byte buffer stores, each followed by its 2 wait states (siren_common.h
+  // store_b128_ws2)
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.y + ((int64_t)n * a.H + h0) * CF_W * CW_C, 2 * CF_W * CW_C * 2);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int q = tid + 512 * k;        // 16-byte piece: pixel q / 16, channels 8 (q % 16)
+    const int px = q >> 4, pc = q & 15;
+    store_b128_ws2(*(const u32x4_t*)(ot + px * OROW + 16 * pc), ry, (uint32_t)(q * 16), 0);
+  }
+}
+
+}  // namespace siren

@@ -1768,6 +1768,25 @@ int siren_conv_wrw_k5(const void* x, const void* dy, int N, int H, int W, int C,
   return check_launch("conv_wrw_reduce");
 }
 
+int siren_conv_fwd_k5(const void* x, const void* w, const void* bias, int relu, void* y, int N, int H, int W, int C,
+                      void* stream) {
+  if (C != CW_C || W != CF_W || N < 1 || H < 2 || H % 2 != 0)
+    return fail(SIREN_EINVAL, "conv_fwd_k5: needs C = %d, W = %d and H even (C = %d, N = %d, H = %d, W = %d)", CW_C,
+                CF_W, C, N, H, W);
+  if (!x || !w || !y) return fail(SIREN_EINVAL, "conv_fwd_k5: null pointer");
+  ConvFArgs a;
+  memset(&a, 0, sizeof(a));
+  a.x = (const bf16*)x;
+  a.w = (const bf16*)w;
+  a.bias = (const bf16*)bias;
+  a.y = (bf16*)y;
+  a.N = N;
+  a.H = H;
+  a.relu = relu ? 1 : 0;
+  hipLaunchKernelGGL(conv_fwd_k5_kernel, dim3((unsigned)(N * (H / 2))), dim3(512), 0, (hipStream_t)stream, a);
+  return check_launch("conv_fwd_k5");
+}
+
 int siren_enc_relu_bwd(const void* g1, const void* g2, const void* y, void* out, float* db, int64_t P, int C, void* ws,
                        int64_t ws_bytes, void* stream) {
   EncArgs a;

@@ -5,10 +5,12 @@ The reference's autograd chain runs, around each convolution, a ReLU, its mask i
 bias-gradient reduction and the residual adds as separate passes over 134 MB planes (C4: 32 x 128^2
 x 128 channels in bf16), and the final Linear over the 16,384 pixels as a cast copy + GEMV. Here:
 
-  forward   bias-free convolutions (MIOpen, bf16 NHWC; with a bias PyTorch adds it in a separate
-            pass) followed by one pass each: bias + ReLU in place (siren_enc_bias_relu), each
-            residual block's tail relu(relu(a + b) + x) (siren_enc_res_fwd), and the 1x1 conv's bias
-            + relu_2 + the pixel Linear as one reduction (siren_enc_pixfc_fwd, fp32 out).
+  forward   the residual blocks' 128 -> 128 5x5 convolutions on a native implicit-GEMM MFMA
+            kernel (siren_conv_fwd_k5: bias + ReLU in its epilogue), the other shapes on MIOpen
+            bias-free (PyTorch would add a bias in a separate pass) + one bias/ReLU pass
+            (siren_enc_bias_relu); each residual block's tail relu(relu(a + b) + x) in one pass
+            (siren_enc_res_fwd); the 1x1 conv's bias + relu_2 + the pixel Linear as one reduction
+            (siren_enc_pixfc_fwd, fp32 out).
   backward  the pixel Linear's three gradients and conv_1x1's ReLU mask + bias gradient in one pass
             (siren_enc_pixfc_bwd); each block's mask / skip / bias-gradient work in one pass
             (siren_enc_res_bwd, siren_enc_relu_bwd, the skip gradient added inside the next mask
@@ -63,10 +65,33 @@ def _w_flip(wb):
     return wb.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL)
 
 
-def _conv(x, wb, bb, pad):
-    # NHWC planes for the passes below (MIOpen returns channels-last for channels-last operands;
-    # the call is a no-op then)
-    return F.conv2d(x, wb, bb, padding=pad).contiguous(memory_format=_CL)
+_CONV_NATIVE = [True]
+
+
+def _native_conv(x, wb):
+    co, ci, k, _ = wb.shape
+    n, _, h, w = x.shape
+    return _CONV_NATIVE[0] and co == ci == 128 and k == 5 and w == 128 and h % 2 == 0
+
+
+def _conv(x, wb, bb, pad, relu=False):
+    """Stride-1 'same' convolution, bf16 NHWC out: the native MFMA kernel for the residual blocks'
+    128 -> 128 5x5 shape (siren_conv_fwd_k5, bias + ReLU in its epilogue), MIOpen otherwise
+    (relu=True needs a bias on that path and is applied by siren_enc_bias_relu)."""
+    if _native_conv(x, wb):
+        n, _, h, w = x.shape
+        y = torch.empty((n, wb.shape[0], h, w), dtype=torch.bfloat16, device=x.device, memory_format=_CL)
+        _native.check(_native.lib().siren_conv_fwd_k5(x.data_ptr(), wb.data_ptr(),
+                                                      bb.data_ptr() if bb is not None else None, 1 if relu else 0,
+                                                      y.data_ptr(), n, h, w, wb.shape[1],
+                                                      _native.stream_handle(x.device)), "siren_conv_fwd_k5")
+        return y
+    y = F.conv2d(x, wb, None if relu else bb, padding=pad).contiguous(memory_format=_CL)
+    if relu:
+        P, C = _plane(y)
+        _native.check(_native.lib().siren_enc_bias_relu(y.data_ptr(), bb.data_ptr() if bb is not None else None, P, C,
+                                                        _native.stream_handle(x.device)), "siren_enc_bias_relu")
+    return y
 
 
 _WGRAD_NATIVE = [True]
@@ -108,20 +133,15 @@ class _EncoderBF16(torch.autograd.Function):
         x0 = I.detach().to(torch.bfloat16).contiguous(memory_format=_CL)
         saved = [x0]
 
-        def bias_relu(y, k):
-            P, C = _plane(y)
-            _native.check(lib.siren_enc_bias_relu(y.data_ptr(), bbs[k].data_ptr(), P, C, stream), "siren_enc_bias_relu")
-            return y
-
-        # conv_theta + bias + relu, cnn[0] + bias + relu (bias-free convolutions, the bias added in
-        # the ReLU pass)
-        t = bias_relu(_conv(x0, wbs[0], None, convs[0].padding[0]), 0)
+        # each convolution bias-free, its bias (+ ReLU) in the native kernel's epilogue or in one
+        # pass after MIOpen's (PyTorch would add a bias in a separate pass)
+        t = _conv(x0, wbs[0], bbs[0], convs[0].padding[0], relu=True)
         saved.append(t)
-        t = bias_relu(_conv(t, wbs[1], None, convs[1].padding[0]), 1)
+        t = _conv(t, wbs[1], bbs[1], convs[1].padding[0], relu=True)
         saved.append(t)
         k = 2
         for _ in range(enc._enc_nblocks):
-            h = bias_relu(_conv(t, wbs[k], None, convs[k].padding[0]), k)
+            h = _conv(t, wbs[k], bbs[k], convs[k].padding[0], relu=True)
             a = _conv(h, wbs[k + 1], None, convs[k + 1].padding[0])  # bias added in the tail pass
             out = torch.empty_like(a)
             P, C = _plane(a)
