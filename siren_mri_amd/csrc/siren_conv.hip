@@ -130,25 +130,41 @@ __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
     if (t + 2 < T) load(t + 2, SC{});
     const int buf = (int)(t % CW_NB);
     const uint32_t db = dbase + buf * DSTAGE, xb = xbase + buf * XSTAGE;
+    // K step ks's 12 fragment reads are issued before step ks - 1's MFMAs (a wait for the older 12
+    // then covers step ks - 1 exactly: lgkmcnt(12))
+    TrFrag fa[2], fb[2][CW_K];
+#define SIREN_CW_RD(KS)                                                                  \
+  {                                                                                      \
+    constexpr int ks_ = (KS), b_ = (KS) & 1;                                             \
+    tr16_read<16 * ks_ * DROWB>(fa[b_].lo, db);                                          \
+    tr16_read<16 * ks_ * DROWB + 4 * DROWB>(fa[b_].hi, db);                              \
+    static_for<0, CW_K>([&](auto kw_c) {                                                 \
+      constexpr int kw = decltype(kw_c)::value;                                          \
+      tr16_read<(16 * ks_ + kw) * XROWB>(fb[b_][kw].lo, xb);                             \
+      tr16_read<(16 * ks_ + kw + 4) * XROWB>(fb[b_][kw].hi, xb);                         \
+    });                                                                                  \
+  }
+    SIREN_CW_RD(0)
     static_for<0, CW_PX / 16>([&](auto ks_c) {
-      constexpr int ks = decltype(ks_c)::value;
-      TrFrag fa, fb[CW_K];
-      tr16_read<16 * ks * DROWB>(fa.lo, db);
-      tr16_read<16 * ks * DROWB + 4 * DROWB>(fa.hi, db);
+      constexpr int ks = decltype(ks_c)::value, b = ks & 1;
+      if constexpr (ks + 1 < CW_PX / 16) {
+        SIREN_CW_RD(ks + 1)
+        asm volatile("s_waitcnt lgkmcnt(12)"
+                     : "+v"(fa[b].lo), "+v"(fa[b].hi), "+v"(fb[b][0].lo), "+v"(fb[b][0].hi), "+v"(fb[b][1].lo),
+                       "+v"(fb[b][1].hi), "+v"(fb[b][2].lo), "+v"(fb[b][2].hi), "+v"(fb[b][3].lo), "+v"(fb[b][3].hi),
+                       "+v"(fb[b][4].lo), "+v"(fb[b][4].hi));
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(fa[b].lo), "+v"(fa[b].hi), "+v"(fb[b][0].lo), "+v"(fb[b][0].hi), "+v"(fb[b][1].lo),
+                       "+v"(fb[b][1].hi), "+v"(fb[b][2].lo), "+v"(fb[b][2].hi), "+v"(fb[b][3].lo), "+v"(fb[b][3].hi),
+                       "+v"(fb[b][4].lo), "+v"(fb[b][4].hi));
+      }
       static_for<0, CW_K>([&](auto kw_c) {
         constexpr int kw = decltype(kw_c)::value;
-        tr16_read<(16 * ks + kw) * XROWB>(fb[kw].lo, xb);
-        tr16_read<(16 * ks + kw + 4) * XROWB>(fb[kw].hi, xb);
-      });
-      static_for<0, CW_K>([&](auto kw_c) {
-        constexpr int kw = decltype(kw_c)::value;
-        // A and B_0..B_kw landed: 2 + 2 (kw + 1) of the 12 reads
-        asm volatile("s_waitcnt lgkmcnt(%4)"
-                     : "+v"(fa.lo), "+v"(fa.hi), "+v"(fb[kw].lo), "+v"(fb[kw].hi)
-                     : "n"(8 - 2 * kw));
-        acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr16_value(fa), tr16_value(fb[kw]), acc[kw], 0, 0, 0);
+        acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr16_value(fa[b]), tr16_value(fb[b][kw]), acc[kw], 0, 0, 0);
       });
     });
+#undef SIREN_CW_RD
     __syncthreads();
   };
   for (int64_t t = 0; t < T; t += 2) {
@@ -307,27 +323,32 @@ __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
     if (s + 1 < NS) stage(SN{}, (s + 1) & 1);
     if (s + 2 < NS) load(s + 2, SC{});
     const uint32_t sb = sbase + (s & 1) * CF_STAGE;
-    static_for<0, CW_K>([&](auto kw_c) {
-      constexpr int kw = decltype(kw_c)::value;
-      static_for<0, 2>([&](auto ks_c) {
-        constexpr int ks = decltype(ks_c)::value;
-        bf16x8 af[2], bfr[2];
+    // 10 K steps (kw, ks); the fragments of step i + 1 are read while step i's MFMAs run
+    bf16x8 af[2][2], bfr[2][2];
+#define SIREN_CF_RD(I)                                                                                            \
+  {                                                                                                               \
+    constexpr int kw_ = (I) >> 1, ks_ = (I) & 1, b_ = (I) & 1;                                                    \
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(af[b_][0]) : "v"(sb + aoff[0]), "n"(kw_ * CW_C * CF_ROWB + 32 * ks_)); \
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(af[b_][1]) : "v"(sb + aoff[1]), "n"(kw_ * CW_C * CF_ROWB + 32 * ks_)); \
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bfr[b_][0]) : "v"(sb + boff[0]), "n"(kw_ * CF_ROWB + 32 * ks_));      \
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bfr[b_][1]) : "v"(sb + boff[1]), "n"(kw_ * CF_ROWB + 32 * ks_));      \
+  }
+    SIREN_CF_RD(0)
+    static_for<0, 2 * CW_K>([&](auto i_c) {
+      constexpr int i = decltype(i_c)::value, b = i & 1;
+      if constexpr (i + 1 < 2 * CW_K) {
+        SIREN_CF_RD(i + 1)
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(af[b][0]), "+v"(af[b][1]), "+v"(bfr[b][0]), "+v"(bfr[b][1]));
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[b][0]), "+v"(af[b][1]), "+v"(bfr[b][0]), "+v"(bfr[b][1]));
+      }
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(af[i]) : "v"(sb + aoff[i]), "n"(kw * CW_C * CF_ROWB + 32 * ks));
-        }
+      for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bfr[j]) : "v"(sb + boff[j]), "n"(kw * CF_ROWB + 32 * ks));
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(bfr[0]), "+v"(bfr[1]));
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      });
+        for (int j = 0; j < 2; ++j)
+          acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[b][ii], bfr[b][j], acc[ii][j], 0, 0, 0);
     });
+#undef SIREN_CF_RD
     __syncthreads();
   };
   for (int s = 0; s < NS; s += 2) {

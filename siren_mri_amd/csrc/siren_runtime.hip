@@ -442,7 +442,9 @@ int dispatch_first_bwd(const FirstBwdArgs& a, int64_t nsplit, int64_t nb, hipStr
     // weight gradient without dx; the input gradient (bf16 mode) as its own MFMA launch
     FirstBwdArgs aw = a;
     aw.dx = nullptr;
-    if (a.C == 16) hipLaunchKernelGGL((first_bwd_wide_kernel<PREC, 16>), grid, dim3(256), 0, st, aw);
+    if (PREC == kPrecBF16 && a.F == 256 && a.rows_per_split % 32 == 0)
+      hipLaunchKernelGGL(first_bwd_wide_mfma_kernel, grid, dim3(256), 0, st, aw);
+    else if (a.C == 16) hipLaunchKernelGGL((first_bwd_wide_kernel<PREC, 16>), grid, dim3(256), 0, st, aw);
     else hipLaunchKernelGGL((first_bwd_wide_kernel<PREC, 0>), grid, dim3(256), 0, st, aw);
     if (a.dx) {
       int rc = check_launch("first_bwd_wide");

@@ -532,6 +532,111 @@ __global__ __launch_bounds__(256) void first_bwd_wide_kernel(FirstBwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// first_bwd_wide_mfma (bf16 mode, F = 256, 5..16 inputs): dW_0 = dZ_0^T x and db_0 = sum dZ_0 on
+// the bf16 MFMA, rows as the K dimension. Per 32-row chunk the dZ_0 rows (32 x 256 bf16, rows of 576
+// bytes) and x as bf16 hi | lo columns (32 x 32, rows of 64 bytes) are staged in LDS and read with
+// transposing ds_read_b64_tr_b16 (tn_dw_kernel's lane roles); wave w owns features 64 w .. 64 w + 63:
+// D[f][c'] = dZ^T [x_hi | x_lo] (dW = D[:, c] + D[:, 16 + c], ~2^-16 of x) and db from a second
+// MFMA against a ones column. The next chunk's global loads are in flight during this chunk's
+// MFMAs. One partial slab per workgroup, first_bwd_wide_kernel's layout and split.
+// (first_bwd_wide_kernel, one thread per feature: 0.34 ms of the C4 step.)
+constexpr int FBM_DZROW = 576;   // bytes per staged dZ row (512 + 64: 4-row transposing reads conflict-free)
+constexpr int FBM_XROW = 64;     // bytes per staged x row (32 bf16)
+__global__ __launch_bounds__(256) void first_bwd_wide_mfma_kernel(FirstBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) char sdz[32 * FBM_DZROW];
+  __shared__ __attribute__((aligned(16))) char sx[32 * FBM_XROW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int split = blockIdx.x;
+  const int64_t batch = blockIdx.y;
+  const int64_t rows = a.rows_per_batch;
+  const int64_t r_begin = (int64_t)split * a.rows_per_split;
+  const int64_t r_end = r_begin + a.rows_per_split < rows ? r_begin + a.rows_per_split : rows;
+  const int C = a.C;
+  const bf16* dz = (const bf16*)a.dZ + batch * rows * 256;
+  const float* xb = a.x + batch * rows * C;
+  f32x16 acc[2], acd[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[i][e] = acd[i][e] = 0.f;
+  // ones column for db: B[k][0] = 1
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (lane & 31) == 0 ? (bf16)1.f : (bf16)0.f;
+
+  // loads of chunk r0: dZ pieces q = tid + 256 j (row q / 32, 16-byte piece q % 32), x: thread t < 128
+  // holds row t / 4, channels 4 (t % 4) .. + 4 (zeros past C and past the range)
+  u32x4_t zv[4];
+  f32x4 xv;
+  auto load = [&](int64_t r0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = tid + 256 * j, r = q >> 5, pc = q & 31;
+      const int64_t row = r0 + r < r_end ? r0 + r : r_end - 1;
+      const u32x4_t v = *(const u32x4_t*)(dz + row * 256 + 8 * pc);
+      const u32x4_t zero = {0u, 0u, 0u, 0u};
+      zv[j] = r0 + r < r_end ? v : zero;
+    }
+    if (tid < 128) {
+      const int r = tid >> 2, c0 = 4 * (tid & 3);
+      const int64_t row = r0 + r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) xv[e] = (row < r_end && c0 + e < C) ? xb[row * C + c0 + e] : 0.f;
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = tid + 256 * j, r = q >> 5, pc = q & 31;
+      *(u32x4_t*)(sdz + r * FBM_DZROW + 16 * pc) = zv[j];
+    }
+    if (tid < 128) {
+      const int r = tid >> 2, c0 = 4 * (tid & 3);
+      bf16x4 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        hi[e] = (bf16)xv[e];
+        lo[e] = (bf16)(xv[e] - (float)hi[e]);
+      }
+      *(bf16x4*)(sx + r * FBM_XROW + 2 * c0) = hi;
+      *(bf16x4*)(sx + r * FBM_XROW + 2 * (16 + c0)) = lo;
+    }
+  };
+  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  if (r_begin < r_end) load(r_begin);
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += 32) {
+    __syncthreads();  // the previous chunk's reads are done
+    stage();
+    __syncthreads();
+    if (r0 + 32 < r_end) load(r0 + 32);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int nb = 16 * ks + 8 * (g >> 1) + tq;
+      const int cx = 16 * (g & 1) + 4 * tp;
+      const bf16x8 bx = lds_read_tr16_pair(sx + nb * FBM_XROW + 2 * cx, sx + (nb + 4) * FBM_XROW + 2 * cx);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int cf = 64 * wave + 32 * i + 16 * (g & 1) + 4 * tp;
+        const bf16x8 af = lds_read_tr16_pair(sdz + nb * FBM_DZROW + 2 * cf, sdz + (nb + 4) * FBM_DZROW + 2 * cf);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bx, acc[i], 0, 0, 0);
+        acd[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, ones, acd[i], 0, 0, 0);
+      }
+    }
+  }
+  float* part = a.part + (int64_t)split * a.split_stride + batch * (int64_t)(256 * C + 256);
+  const int cn = lane & 31;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int f = 64 * wave + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+      const float lo = __shfl_xor(acc[i][e], 16, 32);
+      if (cn < C) part[f * C + cn] = acc[i][e] + lo;
+      if (cn == 0) part[256 * C + f] = acd[i][e];
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // first_dx_wide (bf16 mode, F = 256, 5..16 inputs): the wide first layer's input gradient
 // dx = dZ_0 W_0 ([rows, 256] x [256, C]) on the bf16 MFMA, beside first_bwd_wide_kernel (which has
 // no input gradient). Per wave, 32-row tiles: the A operand is the tile's dZ_0 rows straight from
