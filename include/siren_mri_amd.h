@@ -167,6 +167,18 @@ int siren_jvp_backward(const siren_mlp_desc* d, int order, const float* x, const
                        const void* saved, int64_t saved_bytes, void* workspace,
                        int64_t workspace_bytes, float* const* dweight, float* const* dbias,
                        float* dx, void* stream);
+/* The same two with `primal`: the saved buffer of a plain siren_mlp_forward of this stack on this x
+ * (fp32 mode, outermost_linear; primal_bytes >= siren_mlp_saved_bytes). Its per-layer phases are the
+ * primal stream, so only the tangent streams are computed (diff_operators.gradient of a model output
+ * reuses the model's forward instead of repeating it); the backward reads the same phases, so
+ * `primal` must stay unchanged between the two calls. NULL: as above. */
+int siren_jvp_forward_ex(const siren_mlp_desc* d, int order, const float* x, float* grad, float* lap,
+                         void* saved, int64_t saved_bytes, void* workspace, int64_t workspace_bytes,
+                         const void* primal, int64_t primal_bytes, void* stream);
+int siren_jvp_backward_ex(const siren_mlp_desc* d, int order, const float* x, const float* dgrad,
+                          const void* saved, int64_t saved_bytes, void* workspace, int64_t workspace_bytes,
+                          float* const* dweight, float* const* dbias, float* dx, const void* primal,
+                          int64_t primal_bytes, void* stream);
 
 /*
  * Optional per-kernel-class timing, for benchmarks and profiling (not thread-safe; not for use

@@ -37,6 +37,8 @@ EXPORTED_SYMBOLS = (
     "siren_jvp_workspace_bytes",
     "siren_jvp_forward",
     "siren_jvp_backward",
+    "siren_jvp_forward_ex",
+    "siren_jvp_backward_ex",
     "siren_timing_enable",
     "siren_timing_collect",
     "siren_timing_disable",
@@ -185,9 +187,14 @@ def _declare(lib):
     lib.siren_jvp_workspace_bytes.restype = i64
     lib.siren_jvp_forward.argtypes = [P, ci, vp, vp, vp, vp, i64, vp, i64, vp]
     lib.siren_jvp_forward.restype = ci
+    lib.siren_jvp_forward_ex.argtypes = [P, ci, vp, vp, vp, vp, i64, vp, i64, vp, i64, vp]
+    lib.siren_jvp_forward_ex.restype = ci
     lib.siren_jvp_backward.argtypes = [P, ci, vp, vp, vp, i64, vp, i64,
                                        ctypes.POINTER(vp), ctypes.POINTER(vp), vp, vp]
     lib.siren_jvp_backward.restype = ci
+    lib.siren_jvp_backward_ex.argtypes = [P, ci, vp, vp, vp, i64, vp, i64,
+                                          ctypes.POINTER(vp), ctypes.POINTER(vp), vp, vp, i64, vp]
+    lib.siren_jvp_backward_ex.restype = ci
     lib.siren_timing_enable.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.siren_timing_enable.restype = ctypes.c_int
     lib.siren_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64)]

@@ -39,6 +39,7 @@ struct JNTArgs {
   void* Pout;         // [B][N][Nout] phase_t (JFWD)
   float* Uout;        // JFWD: [B][S-1][N][Nout]; JBWD: raw [B][S][N][Nout]
   int64_t N;          // rows per stream
+  int64_t srow0;      // first stacked row processed (N: the primal stream is given, not computed)
   int S, C, lap;
   int64_t w_bstride, b_bstride;
   int K, Nout;
@@ -101,7 +102,7 @@ __global__ __launch_bounds__(256) void jvp_nt_kernel(JNTArgs a) {
   const int wm = wave >> 1, wn = wave & 1;
   const int64_t b = blockIdx.z;
   const int64_t rows = (int64_t)a.S * a.N;  // stacked rows of this weight set
-  const int64_t m0 = (int64_t)blockIdx.x * JNT_BM;
+  const int64_t m0 = a.srow0 + (int64_t)blockIdx.x * JNT_BM;
   const int n0 = blockIdx.y * JNT_BN;
   const int K = a.K;
   const op_t* W = (const op_t*)a.W + b * a.w_bstride;
@@ -510,7 +511,7 @@ struct JFirstArgs {
   const float* x;     // [B][N][C]
   const float* W;     // [nb_w][F][C]
   const float* bias;  // [nb_w][F]
-  void* P;            // [B][N][F]
+  void* P;            // [B][N][F], or null (the primal's phases are given)
   float* U;           // [B][Su][N][F]
   int64_t N;
   int C, F, Su;
@@ -532,7 +533,7 @@ __global__ __launch_bounds__(256) void jvp_first_kernel(JFirstArgs a) {
     const float* xr = a.x + (b * a.N + n) * a.C;
     float z = 0.f;
     for (int c = 0; c < a.C; ++c) z = fmaf(xr[c], W[f * a.C + c], z);
-    ((phase_t*)a.P)[(b * a.N + n) * a.F + f] = PT::encz(z, bias[f], a.w0);
+    if (a.P) ((phase_t*)a.P)[(b * a.N + n) * a.F + f] = PT::encz(z, bias[f], a.w0);
     for (int s = 0; s < a.Su; ++s)
       a.U[((b * a.Su + s) * a.N + n) * a.F + f] = (s < a.C) ? W[f * a.C + s] : 0.f;
   }

@@ -1242,7 +1242,7 @@ int jvp_check(const siren_mlp_desc* d, int order) {
 
 template <int PREC>
 int jvp_forward_impl(const siren_mlp_desc* d, int order, const float* x, float* grad, float* lap,
-                     char* saved, char* ws, hipStream_t st) {
+                     char* saved, char* ws, hipStream_t st, const char* primal = nullptr) {
   const Geo g = geo_of(d);
   const JLayout jl = jlayout_of(d, order);
   char* base = saved ? saved : ws;
@@ -1251,12 +1251,15 @@ int jvp_forward_impl(const siren_mlp_desc* d, int order, const float* x, float* 
   // without a saved buffer the per-layer tensors still need a home: use the saved layout inside
   // the workspace tail (jvp workspace queries include it in that case, see siren_jvp_workspace_bytes)
   char* store = saved ? saved : ws + jl.ws_bytes;
+  // primal given: layer l's phases are the plain forward's saved P_l (siren_mlp_forward's layout),
+  // and only the tangent streams run (stacked rows N .. S N)
+  auto pptr = [&](int l) -> char* { return primal ? (char*)primal + jl.base.saved_off[l] : store + jl.p_off[l]; };
   {
     JFirstArgs a;
     a.x = x;
     a.W = d->weight[0];
     a.bias = d->bias[0];
-    a.P = store + jl.p_off[0];
+    a.P = primal ? nullptr : store + jl.p_off[0];
     a.U = (float*)(store + jl.u_off[0]);
     a.N = g.rows;
     a.C = d->dims[0];
@@ -1271,14 +1274,15 @@ int jvp_forward_impl(const siren_mlp_desc* d, int order, const float* x, float* 
   }
   for (int l = 1; l + 1 < g.L; ++l) {
     JNTArgs a;
-    a.P = store + jl.p_off[l - 1];
+    a.P = pptr(l - 1);
     a.U = (const float*)(store + jl.u_off[l - 1]);
     a.D = nullptr;
     a.W = PREC == kPrecBF16 ? (const void*)(base + jl.base.w_op_off[l]) : (const void*)d->weight[l];
     a.bias = d->bias[l];
-    a.Pout = store + jl.p_off[l];
+    a.Pout = pptr(l);
     a.Uout = (float*)(store + jl.u_off[l]);
     a.N = g.rows;
+    a.srow0 = primal ? g.rows : 0;
     a.S = jl.S;
     a.C = jl.C;
     a.lap = order == SIREN_JVP_LAPLACE;
@@ -1287,7 +1291,7 @@ int jvp_forward_impl(const siren_mlp_desc* d, int order, const float* x, float* 
     a.K = d->dims[l];
     a.Nout = d->dims[l + 1];
     a.w0 = d->w0;
-    dim3 grid((unsigned)cdiv((int64_t)jl.S * g.rows, JNT_BM), (unsigned)cdiv(a.Nout, JNT_BN), (unsigned)g.nb);
+    dim3 grid((unsigned)cdiv((int64_t)jl.S * g.rows - a.srow0, JNT_BM), (unsigned)cdiv(a.Nout, JNT_BN), (unsigned)g.nb);
     if (a.lap) hipLaunchKernelGGL((jvp_nt_kernel<PREC, JMODE_FWD, true>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((jvp_nt_kernel<PREC, JMODE_FWD>), grid, dim3(256), 0, st, a);
     if ((rc = check_launch("jvp_nt fwd"))) return rc;
@@ -1295,7 +1299,7 @@ int jvp_forward_impl(const siren_mlp_desc* d, int order, const float* x, float* 
   {
     const int l = g.L - 1;
     JLastArgs a;
-    a.P = store + jl.p_off[l - 1];
+    a.P = pptr(l - 1);
     a.U = (const float*)(store + jl.u_off[l - 1]);
     a.W = d->weight[l];
     a.grad = grad;
@@ -1317,9 +1321,11 @@ int jvp_forward_impl(const siren_mlp_desc* d, int order, const float* x, float* 
 
 template <int PREC>
 int jvp_backward_impl(const siren_mlp_desc* d, int order, const float* x, const float* dout,
-                      const char* saved, char* ws, float* const* dW, float* const* db, float* dx, hipStream_t st) {
+                      const char* saved, char* ws, float* const* dW, float* const* db, float* dx, hipStream_t st,
+                      const char* primal = nullptr) {
   const Geo g = geo_of(d);
   const JLayout jl = jlayout_of(d, order);
+  auto pptr = [&](int l) -> const char* { return primal ? primal + jl.base.saved_off[l] : saved + jl.p_off[l]; };
   const int lapmode = order == SIREN_JVP_LAPLACE;
   float* part = (float*)(ws + jl.part_off);
   int rc = SIREN_OK;
@@ -1328,7 +1334,7 @@ int jvp_backward_impl(const siren_mlp_desc* d, int order, const float* x, const 
     const int l = g.L - 1;
     const Split s = jcol_split(g);
     JCombArgs a;
-    a.P = saved + jl.p_off[l - 1];
+    a.P = pptr(l - 1);
     a.U = (const float*)(saved + jl.u_off[l - 1]);
     a.raw = nullptr;
     a.gbar = lapmode ? nullptr : dout;
@@ -1364,7 +1370,7 @@ int jvp_backward_impl(const siren_mlp_desc* d, int order, const float* x, const 
       const Split s = jtn_split(g, (int64_t)jl.Sb * g.rows, M, N);
       JTNArgs a;
       a.D = ws + jl.d_off[cur];
-      a.P = saved + jl.p_off[l - 1];
+      a.P = pptr(l - 1);
       a.U = (const float*)(saved + jl.u_off[l - 1]);
       a.part = part;
       a.N = g.rows;
@@ -1405,7 +1411,7 @@ int jvp_backward_impl(const siren_mlp_desc* d, int order, const float* x, const 
       const Split s = jcol_split(g);
       JCombArgs a;
       memset(&a, 0, sizeof(a));
-      a.P = saved + jl.p_off[l - 1];
+      a.P = pptr(l - 1);
       a.U = (const float*)(saved + jl.u_off[l - 1]);
       a.raw = (const float*)(ws + jl.raw_off);
       a.D = ws + jl.d_off[cur ^ 1];
@@ -1614,11 +1620,29 @@ int64_t siren_jvp_workspace_bytes(const siren_mlp_desc* d, int order) {
   return jl.ws_bytes + jl.saved_bytes;  // room for the per-layer tensors when no saved buffer is given
 }
 
-int siren_jvp_forward(const siren_mlp_desc* d, int order, const float* x, float* grad, float* lap,
-                      void* saved, int64_t saved_bytes, void* workspace, int64_t workspace_bytes,
-                      void* stream) {
+namespace {
+// the plain forward's saved buffer as the primal stream of a jvp (fp32 mode: its phases are the
+// jvp's fp32 phases; siren_mlp_forward's layout)
+int jvp_primal_check(const siren_mlp_desc* d, const void* primal, int64_t primal_bytes) {
+  if (!primal) return SIREN_OK;
+  if (d->prec != SIREN_PREC_F32) return fail(SIREN_EINVAL, "jvp primal: fp32 mode only");
+  if (!d->outermost_linear) return fail(SIREN_EINVAL, "jvp primal: needs outermost_linear");
+  const Layout lo = layout_of(d);
+  if (primal_bytes < lo.saved_bytes)
+    return fail(SIREN_ENOSPACE, "jvp primal: saved buffer %lld < %lld bytes", (long long)primal_bytes,
+                (long long)lo.saved_bytes);
+  for (int l = 0; l + 1 < d->num_layers; ++l)
+    if (lo.saved_off[l] < 0) return fail(SIREN_EINVAL, "jvp primal: layer %d phases not kept", l);
+  return SIREN_OK;
+}
+}  // namespace
+
+int siren_jvp_forward_ex(const siren_mlp_desc* d, int order, const float* x, float* grad, float* lap,
+                         void* saved, int64_t saved_bytes, void* workspace, int64_t workspace_bytes,
+                         const void* primal, int64_t primal_bytes, void* stream) {
   int rc = jvp_check(d, order);
   if (rc) return rc;
+  if ((rc = jvp_primal_check(d, primal, primal_bytes))) return rc;
   const JLayout jl = jlayout_of(d, order);
   if (saved && saved_bytes < jl.saved_bytes)
     return fail(SIREN_ENOSPACE, "saved buffer %lld < %lld bytes", (long long)saved_bytes, (long long)jl.saved_bytes);
@@ -1630,14 +1654,23 @@ int siren_jvp_forward(const siren_mlp_desc* d, int order, const float* x, float*
   hipStream_t st = (hipStream_t)stream;
   if (d->prec == SIREN_PREC_BF16)
     return jvp_forward_impl<kPrecBF16>(d, order, x, grad, lap, (char*)saved, (char*)workspace, st);
-  return jvp_forward_impl<kPrecF32>(d, order, x, grad, lap, (char*)saved, (char*)workspace, st);
+  return jvp_forward_impl<kPrecF32>(d, order, x, grad, lap, (char*)saved, (char*)workspace, st, (const char*)primal);
 }
 
-int siren_jvp_backward(const siren_mlp_desc* d, int order, const float* x, const float* dgrad,
-                       const void* saved, int64_t saved_bytes, void* workspace, int64_t workspace_bytes,
-                       float* const* dweight, float* const* dbias, float* dx, void* stream) {
+int siren_jvp_forward(const siren_mlp_desc* d, int order, const float* x, float* grad, float* lap,
+                      void* saved, int64_t saved_bytes, void* workspace, int64_t workspace_bytes,
+                      void* stream) {
+  return siren_jvp_forward_ex(d, order, x, grad, lap, saved, saved_bytes, workspace, workspace_bytes, nullptr, 0,
+                              stream);
+}
+
+int siren_jvp_backward_ex(const siren_mlp_desc* d, int order, const float* x, const float* dgrad,
+                          const void* saved, int64_t saved_bytes, void* workspace, int64_t workspace_bytes,
+                          float* const* dweight, float* const* dbias, float* dx, const void* primal,
+                          int64_t primal_bytes, void* stream) {
   int rc = jvp_check(d, order);
   if (rc) return rc;
+  if ((rc = jvp_primal_check(d, primal, primal_bytes))) return rc;
   const JLayout jl = jlayout_of(d, order);
   if (!saved || saved_bytes < jl.saved_bytes)
     return fail(SIREN_ENOSPACE, "saved buffer %lld < %lld bytes", (long long)saved_bytes, (long long)jl.saved_bytes);
@@ -1650,7 +1683,15 @@ int siren_jvp_backward(const siren_mlp_desc* d, int order, const float* x, const
   hipStream_t st = (hipStream_t)stream;
   if (d->prec == SIREN_PREC_BF16)
     return jvp_backward_impl<kPrecBF16>(d, order, x, dgrad, (const char*)saved, (char*)workspace, dweight, dbias, dx, st);
-  return jvp_backward_impl<kPrecF32>(d, order, x, dgrad, (const char*)saved, (char*)workspace, dweight, dbias, dx, st);
+  return jvp_backward_impl<kPrecF32>(d, order, x, dgrad, (const char*)saved, (char*)workspace, dweight, dbias, dx, st,
+                                     (const char*)primal);
+}
+
+int siren_jvp_backward(const siren_mlp_desc* d, int order, const float* x, const float* dgrad,
+                       const void* saved, int64_t saved_bytes, void* workspace, int64_t workspace_bytes,
+                       float* const* dweight, float* const* dbias, float* dx, void* stream) {
+  return siren_jvp_backward_ex(d, order, x, dgrad, saved, saved_bytes, workspace, workspace_bytes, dweight, dbias, dx,
+                               nullptr, 0, stream);
 }
 
 const char* siren_last_error(void) { return g_err.c_str(); }

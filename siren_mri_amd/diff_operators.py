@@ -48,6 +48,12 @@ def siren_source(y, x):
     return _lookup(y, x)
 
 
+def _primal(y):
+    """The saved buffer of the forward that produced y (ops.siren_mlp, fp32 mode), or None: the
+    tangent-stream op then takes its primal phases from it instead of recomputing the forward."""
+    return getattr(y, "_siren_primal", None)
+
+
 _ANALYTIC = True
 
 
@@ -68,12 +74,12 @@ def gradient(y, x, grad_outputs=None):
         if src is not None:
             from .jvp import siren_gradient, siren_jacobian
             if grad_outputs is None:
-                return siren_gradient(x, *src)
+                return siren_gradient(x, *src, primal=_primal(y))
             g = grad_outputs
             if g.shape == y.shape:
                 if y.shape[-1] == 1:
-                    return siren_gradient(x, *src) * g
-                return (siren_jacobian(x, *src) * g.unsqueeze(-1)).sum(-2)
+                    return siren_gradient(x, *src, primal=_primal(y)) * g
+                return (siren_jacobian(x, *src, primal=_primal(y)) * g.unsqueeze(-1)).sum(-2)
     if grad_outputs is None:
         grad_outputs = torch.ones_like(y)
     return torch.autograd.grad(y, [x], grad_outputs=grad_outputs, create_graph=True)[0]
@@ -91,7 +97,7 @@ def laplace(y, x):
         src = _lookup(y, x)
         if src is not None:
             from .jvp import siren_laplace
-            return siren_laplace(x, *src)
+            return siren_laplace(x, *src, primal=_primal(y))
     return divergence(gradient(y, x), x)
 
 
@@ -102,7 +108,7 @@ def jacobian(y, x):
         src = _lookup(y, x)
         if src is not None:
             from .jvp import siren_jacobian
-            jac = siren_jacobian(x, *src)
+            jac = siren_jacobian(x, *src, primal=_primal(y))
             return jac, (-1 if torch.any(torch.isnan(jac)) else 0)
     b, n = y.shape[:2]
     jac = torch.zeros(b, n, y.shape[-1], x.shape[-1], device=y.device)

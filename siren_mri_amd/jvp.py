@@ -48,15 +48,16 @@ def _jvp_sizes(geo, prec, order):
 GRADIENT, LAPLACE, JACOBIAN = 1, 2, 3  # SIREN_JVP_* of include/siren_mri_amd.h
 
 _LIB.define("sine_mlp_jvp(Tensor x, Tensor[] weights, Tensor[] biases, float w0, int prec, bool batched, int order, "
-            "bool keep) -> (Tensor, Tensor)")
+            "bool keep, Tensor? primal=None) -> (Tensor, Tensor)")
 _LIB.define("sine_mlp_jvp_bwd(Tensor dout, Tensor x, Tensor[] weights, Tensor[] biases, Tensor saved, float w0, "
-            "int prec, bool batched, int order, bool need_dx) -> (Tensor, Tensor[], Tensor[])")
+            "int prec, bool batched, int order, bool need_dx, Tensor? primal=None) -> (Tensor, Tensor[], Tensor[])")
 
 
 def sine_mlp_jvp(x: Tensor, weights: List[Tensor], biases: List[Tensor], w0: float, prec: int, batched: bool,
-                 order: int, keep: bool) -> Tuple[Tensor, Tensor]:
-    """siren_jvp_forward: order 1 -> sum_c dy_c/dx (shape of x); order 2 -> the Laplacian [.., 1];
-    order 3 -> the per-channel Jacobian dy_c/dx_k [.., out, in]."""
+                 order: int, keep: bool, primal: Tensor | None = None) -> Tuple[Tensor, Tensor]:
+    """siren_jvp_forward_ex: order 1 -> sum_c dy_c/dx (shape of x); order 2 -> the Laplacian [.., 1];
+    order 3 -> the per-channel Jacobian dy_c/dx_k [.., out, in]. primal: the saved buffer of the
+    plain forward of this stack on this x (fp32): its phases are the primal stream."""
     _require_device(x)
     geo = _geo_of(x, weights, batched)
     ws = [w.contiguous() for w in weights]
@@ -70,15 +71,17 @@ def sine_mlp_jvp(x: Tensor, weights: List[Tensor], biases: List[Tensor], w0: flo
     gshape = xc.shape[:-1] + (geo.dims[-1], xc.shape[-1]) if order == JACOBIAN else xc.shape
     grad = torch.empty(gshape, dtype=torch.float32, device=dev)
     lap = torch.empty(xc.shape[:-1] + (1,), dtype=torch.float32, device=dev) if order == LAPLACE else None
-    rc = _native.lib().siren_jvp_forward(ctypes.byref(desc), order, xc.data_ptr(), grad.data_ptr(),
-                                         lap.data_ptr() if lap is not None else None,
-                                         saved.data_ptr() if keep else None, saved_bytes if keep else 0,
-                                         work.data_ptr(), ws_bytes, _native.stream_handle(dev))
-    _native.check(rc, "siren_jvp_forward")
+    rc = _native.lib().siren_jvp_forward_ex(ctypes.byref(desc), order, xc.data_ptr(), grad.data_ptr(),
+                                            lap.data_ptr() if lap is not None else None,
+                                            saved.data_ptr() if keep else None, saved_bytes if keep else 0,
+                                            work.data_ptr(), ws_bytes,
+                                            primal.data_ptr() if primal is not None else None,
+                                            primal.numel() if primal is not None else 0, _native.stream_handle(dev))
+    _native.check(rc, "siren_jvp_forward_ex")
     return (lap if order == LAPLACE else grad), saved
 
 
-def _sine_mlp_jvp_fake(x, weights, biases, w0, prec, batched, order, keep):
+def _sine_mlp_jvp_fake(x, weights, biases, w0, prec, batched, order, keep, primal=None):
     geo = _geo_of(x, weights, batched)
     saved_bytes, _ = _jvp_sizes(geo, prec, order)
     if order == JACOBIAN:
@@ -89,8 +92,8 @@ def _sine_mlp_jvp_fake(x, weights, biases, w0, prec, batched, order, keep):
 
 
 def sine_mlp_jvp_bwd(dout: Tensor, x: Tensor, weights: List[Tensor], biases: List[Tensor], saved: Tensor, w0: float,
-                     prec: int, batched: bool, order: int,
-                     need_dx: bool) -> Tuple[Tensor, List[Tensor], List[Tensor]]:
+                     prec: int, batched: bool, order: int, need_dx: bool,
+                     primal: Tensor | None = None) -> Tuple[Tensor, List[Tensor], List[Tensor]]:
     """siren_jvp_backward: the adjoint of the tangent streams -> (dx or empty, dW, db)."""
     if saved.numel() == 0:
         raise RuntimeError("siren_mri_amd: sine_mlp_jvp_bwd needs the saved buffer of a forward with keep=True")
@@ -106,16 +109,17 @@ def sine_mlp_jvp_bwd(dout: Tensor, x: Tensor, weights: List[Tensor], biases: Lis
     db = [torch.empty_like(b) for b in bs]
     dx = torch.empty_like(xc) if need_dx else xc.new_empty((0,))
     VP = ctypes.c_void_p * len(ws)
-    rc = _native.lib().siren_jvp_backward(ctypes.byref(desc), order, xc.data_ptr(),
-                                          dout.contiguous().float().data_ptr(), saved.data_ptr(), saved_bytes,
-                                          work.data_ptr(), ws_bytes, VP(*[g.data_ptr() for g in dW]),
-                                          VP(*[g.data_ptr() for g in db]), dx.data_ptr() if need_dx else None,
-                                          _native.stream_handle(dev))
-    _native.check(rc, "siren_jvp_backward")
+    rc = _native.lib().siren_jvp_backward_ex(ctypes.byref(desc), order, xc.data_ptr(),
+                                             dout.contiguous().float().data_ptr(), saved.data_ptr(), saved_bytes,
+                                             work.data_ptr(), ws_bytes, VP(*[g.data_ptr() for g in dW]),
+                                             VP(*[g.data_ptr() for g in db]), dx.data_ptr() if need_dx else None,
+                                             primal.data_ptr() if primal is not None else None,
+                                             primal.numel() if primal is not None else 0, _native.stream_handle(dev))
+    _native.check(rc, "siren_jvp_backward_ex")
     return dx, dW, db
 
 
-def _sine_mlp_jvp_bwd_fake(dout, x, weights, biases, saved, w0, prec, batched, order, need_dx):
+def _sine_mlp_jvp_bwd_fake(dout, x, weights, biases, saved, w0, prec, batched, order, need_dx, primal=None):
     return (torch.empty_like(x) if need_dx else x.new_empty((0,)),
             [torch.empty_like(w) for w in weights], [torch.empty_like(b) for b in biases])
 
@@ -124,12 +128,14 @@ class _SineMLPJVPAutograd(torch.autograd.Function):
     """Autograd formula of sine_mlp_jvp: its backward is sine_mlp_jvp_bwd (lists passed flattened)."""
 
     @staticmethod
-    def forward(ctx, meta, x, *params):
+    def forward(ctx, meta, x, primal, *params):
         w0, prec, batched, order, n, keep = meta
         with torch._C._AutoDispatchBelowAutograd():
             out, saved = torch.ops.siren_mri_amd.sine_mlp_jvp(x, list(params[:n]), list(params[n:]), w0, prec,
-                                                              batched, order, keep)
+                                                              batched, order, keep, primal)
         ctx.meta = meta
+        # the primal buffer is read again by the backward: kept alive here
+        ctx.primal = primal
         ctx.save_for_backward(x, saved, *params)
         ctx.mark_non_differentiable(saved)
         ctx.set_materialize_grads(False)
@@ -139,7 +145,7 @@ class _SineMLPJVPAutograd(torch.autograd.Function):
     def backward(ctx, dout, _dsaved):
         w0, prec, batched, order, n, keep = ctx.meta
         if dout is None:
-            return (None,) * (2 + 2 * n)
+            return (None,) * (3 + 2 * n)
         if not keep:
             raise RuntimeError("siren_mri_amd: the tangent-stream forward ran without keeping its streams "
                                "(grad mode was off); it cannot be differentiated")
@@ -148,7 +154,7 @@ class _SineMLPJVPAutograd(torch.autograd.Function):
         need_dx = ctx.needs_input_grad[1]
         with torch.no_grad():
             dx, dW, db = torch.ops.siren_mri_amd.sine_mlp_jvp_bwd(dout, x, ws, bs, saved, w0, prec, batched, order,
-                                                                  need_dx)
+                                                                  need_dx, ctx.primal)
         db = list(db)
         # the output bias does not reach dy/dx or the Laplacian: autograd leaves its .grad None in the reference
         db[-1] = None
@@ -159,11 +165,11 @@ class _SineMLPJVPAutograd(torch.autograd.Function):
             outs = guard_higher_order(outs, [x, *ws, *bs],
                                       "siren_mri_amd: derivatives of the tangent-stream backward (a third "
                                       "derivative of the SIREN) are not provided")
-        return (None, *outs)
+        return (None, outs[0], None, *outs[1:])
 
 
-def _sine_mlp_jvp_autograd(x, weights, biases, w0, prec, batched, order, keep):
-    return _SineMLPJVPAutograd.apply((w0, prec, batched, order, len(weights), keep), x, *weights, *biases)
+def _sine_mlp_jvp_autograd(x, weights, biases, w0, prec, batched, order, keep, primal=None):
+    return _SineMLPJVPAutograd.apply((w0, prec, batched, order, len(weights), keep), x, primal, *weights, *biases)
 
 
 _LIB.impl("sine_mlp_jvp", sine_mlp_jvp, "CUDA")
@@ -173,7 +179,7 @@ torch.library.register_fake("siren_mri_amd::sine_mlp_jvp", _sine_mlp_jvp_fake, l
 torch.library.register_fake("siren_mri_amd::sine_mlp_jvp_bwd", _sine_mlp_jvp_bwd_fake, lib=_LIB)
 
 
-def _apply(x, fcblock, params, order):
+def _apply(x, fcblock, params, order, primal=None):
     from .meta import get_subdict
     ws, bs = fcblock.layer_params(get_subdict(params, "net") if params is not None else None)
     prec = _native.precision_code(fcblock.precision or get_default_precision())
@@ -182,22 +188,24 @@ def _apply(x, fcblock, params, order):
     if geo.squeeze_w:
         ws, bs = [w[0] for w in ws], [b[0] for b in bs]
     keep = torch.is_grad_enabled() and (x.requires_grad or any(t.requires_grad for t in list(ws) + list(bs)))
+    if primal is not None and (prec != _native.PREC_F32 or not fcblock.outermost_linear):
+        primal = None
     out, _ = torch.ops.siren_mri_amd.sine_mlp_jvp(x, list(ws), list(bs), float(fcblock.w0), prec, geo.batched,
-                                                  order, keep)
+                                                  order, keep, primal)
     return out
 
 
-def siren_gradient(x, fcblock, params=None):
-    return _apply(x, fcblock, params, GRADIENT)
+def siren_gradient(x, fcblock, params=None, primal=None):
+    return _apply(x, fcblock, params, GRADIENT, primal)
 
 
-def siren_laplace(x, fcblock, params=None):
-    return _apply(x, fcblock, params, LAPLACE)
+def siren_laplace(x, fcblock, params=None, primal=None):
+    return _apply(x, fcblock, params, LAPLACE, primal)
 
 
-def siren_jacobian(x, fcblock, params=None):
+def siren_jacobian(x, fcblock, params=None, primal=None):
     """dy_c/dx_k per output channel, [..., out_features, in_features] (diff_operators.jacobian)."""
-    return _apply(x, fcblock, params, JACOBIAN)
+    return _apply(x, fcblock, params, JACOBIAN, primal)
 
 
 def jacobian_of(x, weights, biases, w0, prec, batched):

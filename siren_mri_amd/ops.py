@@ -476,4 +476,9 @@ def siren_mlp(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence
             return y
     y, saved = torch.ops.siren_mri_amd.sine_mlp_fwd(x, ws, bs, float(w0), prec, bool(outermost_linear),
                                                     geo.batched, keep)
-    return (y, saved) if return_saved else y
+    if return_saved:
+        return y, saved
+    if keep and outermost_linear and prec == _native.PREC_F32:
+        # diff_operators hands this to the tangent-stream op on (y, x): its primal stream is these phases
+        y._siren_primal = saved
+    return y

@@ -294,3 +294,47 @@ def test_unprovided_higher_orders_raise():
     gw = torch.autograd.grad(g.square().sum(), list(m.parameters())[:2], create_graph=True)
     with pytest.raises(RuntimeError, match="not provided"):
         gw[0].sum().backward()
+
+
+@pytest.mark.parametrize("order", ["gradient", "laplace", "jacobian"])
+@pytest.mark.parametrize("batched", [False, True])
+def test_primal_reuse_matches_recomputed_primal(order, batched):
+    """The fp32 forward's saved phases as the tangent op's primal stream (y._siren_primal) give the
+    same values and parameter / input gradients as the op recomputing its own primal stream."""
+    from siren_mri_amd import jvp
+    from siren_mri_amd.meta import get_subdict
+    out = 2 if order == "jacobian" else 1
+    m = _model(128, 2, 21, "fp32", out=out)
+    B = 2 if batched else 1
+    coords = orc.get_mgrid(20)[None].repeat(B, 1, 1).to(DEV)
+    params = None
+    if batched:
+        params = {k: torch.stack([v * (1 + 0.03 * i) for i in range(B)]).requires_grad_(True)
+                  for k, v in m.state_dict().items()}
+    fn = {"gradient": jvp.siren_gradient, "laplace": jvp.siren_laplace, "jacobian": jvp.siren_jacobian}[order]
+    res = []
+    for use_primal in (True, False):
+        m.zero_grad(set_to_none=True)
+        if params is not None:
+            for p in params.values():
+                p.grad = None
+        x = coords.clone().requires_grad_(True)
+        o = m({"coords": x}, params=params)
+        y = o["model_out"]
+        primal = getattr(y, "_siren_primal", None)
+        assert primal is not None
+        sub = get_subdict(params, "net") if params is not None else None
+        val = fn(o["model_in"], m.net, sub, primal=primal if use_primal else None)
+        torch.manual_seed(5)
+        w = torch.randn_like(val)
+        (val * w).sum().backward()
+        grads = [p.grad.clone() for p in (params.values() if params is not None else m.parameters())
+                 if p.grad is not None]
+        res.append((val.detach(), grads, o["model_in"].grad))
+    (v1, g1, dx1), (v0, g0, dx0) = res
+    assert orc.norm_rel(v1.cpu(), v0.cpu()) < 1e-6
+    assert len(g1) == len(g0)
+    for a, b in zip(g1, g0):
+        assert orc.norm_rel(a.cpu(), b.cpu()) < 1e-5
+    if dx0 is not None:
+        assert orc.norm_rel(dx1.cpu(), dx0.cpu()) < 1e-5

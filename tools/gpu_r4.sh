@@ -31,7 +31,7 @@ for st in "$@"; do
     c3)
       timeout -k 10 300 python -u bench.py --config c3 --no-cpu-baseline --no-psnr --no-other-configs > $out/c3.json 2> $out/c3.err || exit $? ;;
     c3prof)
-      (cd /tmp && export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$out/c3prof -o c3 -- python3 $GRAFT_REPO_ROOT/bench.py --config c3 --no-cpu-baseline --no-psnr --no-other-configs --steps 5 --warmup 2 > $GRAFT_REPO_ROOT/$out/c3prof.log 2>&1) || exit $? ;;
+      (cd /tmp && export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$out/c3prof -o c3 -- python3 $GRAFT_REPO_ROOT/bench.py --config c3 --no-cpu-baseline --no-psnr --no-other-configs --steps 5 --warmup 2 > $GRAFT_REPO_ROOT/$out/c3prof.log 2>&1) || exit $? ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$out/prof -o m -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-psnr --no-other-configs --steps 20 --warmup 5 > $GRAFT_REPO_ROOT/$out/prof.log 2>&1) || exit $? ;;
     probe)
