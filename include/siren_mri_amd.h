@@ -228,8 +228,17 @@ typedef struct siren_adam_desc {
   float* exp_avg_sq[SIREN_ADAM_MAX_TENSORS];
   const float* dev_scalars;      /* NULL, or device {step_size, bias_correction2_sqrt} read by the
                                     kernel (written by siren_adam_scalars: hipGraph replays) */
+  double* dev_steps;             /* NULL, or siren_adam_num_blocks(d) device step counters, all equal:
+                                    each workgroup advances its own (t += 1) and reads its scalars
+                                    from dev_table[t - 1] (hipGraph replays without the separate
+                                    scalars launch); takes precedence over dev_scalars */
+  const float* dev_table;        /* [table_n][2] {step_size, bias_correction2_sqrt} of t = 1 .. table_n,
+                                    the last entry repeated past the end (as siren_adam_scalars_table) */
+  int64_t table_n;
 } siren_adam_desc;
 int siren_adam_step(const siren_adam_desc* d, void* stream);
+/* Workgroups of siren_adam_step's launch for this descriptor (the length of dev_steps). */
+int64_t siren_adam_num_blocks(const siren_adam_desc* d);
 /* Device-side bias corrections for graph-captured steps: *t += 1, then
  * out[0] = -(lr / (1 - beta1^t)), out[1] = sqrt(1 - beta2^t), computed in double and rounded to
  * float as the host path does (t, out: device pointers). One single-thread launch. */

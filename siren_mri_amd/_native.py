@@ -45,6 +45,7 @@ EXPORTED_SYMBOLS = (
     "siren_config_set",
     "siren_config_get",
     "siren_adam_step",
+    "siren_adam_num_blocks",
     "siren_adam_scalars",
     "siren_adam_scalars_table",
     "siren_sse_workspace_bytes",
@@ -146,6 +147,9 @@ class SirenAdamDesc(ctypes.Structure):
         ("exp_avg", ctypes.c_void_p * ADAM_MAX_TENSORS),
         ("exp_avg_sq", ctypes.c_void_p * ADAM_MAX_TENSORS),
         ("dev_scalars", ctypes.c_void_p),
+        ("dev_steps", ctypes.c_void_p),
+        ("dev_table", ctypes.c_void_p),
+        ("table_n", ctypes.c_int64),
 
     ]
 
@@ -207,6 +211,8 @@ def _declare(lib):
     lib.siren_config_get.restype = i64
     lib.siren_adam_step.argtypes = [ctypes.POINTER(SirenAdamDesc), vp]
     lib.siren_adam_step.restype = ctypes.c_int
+    lib.siren_adam_num_blocks.argtypes = [ctypes.POINTER(SirenAdamDesc)]
+    lib.siren_adam_num_blocks.restype = ctypes.c_int64
     f32 = ctypes.c_float
     f64 = ctypes.c_double
     lib.siren_adam_scalars.argtypes = [vp, f64, f64, f64, vp, vp]

@@ -17,6 +17,9 @@ struct AdamArgs {
   int64_t numel[SIREN_ADAM_MAX_TENSORS];
   float one_minus_beta1, beta2, one_minus_beta2, eps, weight_decay, step, bc2_sqrt;
   const float* dev;  // null, or device {step, bc2_sqrt} (graph-captured steps)
+  double* steps;     // null, or one step counter per workgroup (graph-captured steps, table form)
+  const float* table;
+  int64_t table_n;
   int maximize;
 };
 
@@ -49,8 +52,19 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   const float* gr = a.grad[t];
   float* m = a.exp_avg[t];
   float* v = a.exp_avg_sq[t];
-  const float step = a.dev ? a.dev[0] : a.step;
-  const float bc2_sqrt = a.dev ? a.dev[1] : a.bc2_sqrt;
+  float step = a.dev ? a.dev[0] : a.step;
+  float bc2_sqrt = a.dev ? a.dev[1] : a.bc2_sqrt;
+  // table form: this workgroup's own counter (no other workgroup touches it, so the read-advance-
+  // write needs no ordering between workgroups; the scalars kernel's launch is folded in here)
+  const int64_t blk = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  double tnew = 0.0;
+  if (a.steps) {
+    tnew = a.steps[blk] + 1.0;
+    int64_t k = (int64_t)tnew - 1;
+    k = k < 0 ? 0 : k >= a.table_n ? a.table_n - 1 : k;
+    step = a.table[2 * k];
+    bc2_sqrt = a.table[2 * k + 1];
+  }
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     float g = gr[i];
     if (a.maximize) g = -g;
@@ -64,6 +78,10 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
     m[i] = mv;
     v[i] = vv;
     p[i] = pv + step * (mv / d);
+  }
+  if (a.steps) {
+    __syncthreads();  // every thread has read the counter
+    if (threadIdx.x == 0) a.steps[blk] = tnew;
   }
 }
 

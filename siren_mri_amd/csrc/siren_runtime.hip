@@ -2046,6 +2046,13 @@ int siren_sincos_f32(const float* x, float* s, float* c, int64_t n, int impl, vo
   return check_launch("sincos_f32");
 }
 
+int64_t siren_adam_num_blocks(const siren_adam_desc* d) {
+  if (!d || d->num_tensors <= 0 || d->num_tensors > SIREN_ADAM_MAX_TENSORS) return 0;
+  int64_t maxn = 0;
+  for (int t = 0; t < d->num_tensors; ++t) maxn = std::max(maxn, d->numel[t]);
+  return maxn > 0 ? (int64_t)grid1d(maxn, 1024) * d->num_tensors : 0;
+}
+
 int siren_adam_step(const siren_adam_desc* d, void* stream) {
   if (!d || d->num_tensors < 0 || d->num_tensors > SIREN_ADAM_MAX_TENSORS)
     return fail(SIREN_EINVAL, "adam: num_tensors outside [0, %d]", SIREN_ADAM_MAX_TENSORS);
@@ -2071,8 +2078,15 @@ int siren_adam_step(const siren_adam_desc* d, void* stream) {
   a.step = d->step_size;
   a.bc2_sqrt = d->bias_correction2_sqrt;
   a.dev = d->dev_scalars;
+  a.steps = d->dev_steps;
+  a.table = d->dev_table;
+  a.table_n = d->table_n;
+  if (a.steps && (!a.table || a.table_n < 1)) return fail(SIREN_EINVAL, "adam: dev_steps without a table");
   a.maximize = d->maximize;
-  if (maxn == 0) return SIREN_OK;
+  if (maxn == 0) {
+    if (a.steps) return fail(SIREN_EINVAL, "adam: dev_steps with no elements (the counters would not advance)");
+    return SIREN_OK;
+  }
   hipLaunchKernelGGL(adam_kernel, dim3(grid1d(maxn, 1024), (unsigned)d->num_tensors), dim3(256), 0,
                      (hipStream_t)stream, a);
   return check_launch("adam");

@@ -28,10 +28,12 @@ class Adam(torch.optim.Adam):
     """torch.optim.Adam whose step is one native launch (see the module docstring).
 
     ``enable_graph_mode()`` makes the step hipGraph-capturable: the bias corrections come from a
-    device-side step counter instead of host floats baked into the captured launch — one
-    single-thread launch per group advances it and looks the step's scalars up in a table the host
-    computed once (siren_adam_scalars_table), or computes them (siren_adam_scalars). The host-side ``state['step']`` keeps counting
-    eager calls only; ``sync_graph_steps()`` copies the device counters back into it."""
+    device-side step count instead of host floats baked into the captured launch: each workgroup
+    of the update launch advances its own counter and looks the step's scalars up in a table the
+    host computed once (siren_adam_desc.dev_steps; no extra launch), or, for betas whose table
+    would be too long, a single-thread launch per group advances one counter and computes them
+    (siren_adam_scalars). The host-side ``state['step']`` keeps counting eager calls only;
+    ``sync_graph_steps()`` copies the device counters back into it."""
 
     _graph_mode = False
     # graph mode: {step_size, bias_correction2_sqrt} of steps 1, 2, ... up to the step where both
@@ -65,7 +67,12 @@ class Adam(torch.optim.Adam):
             dev = getattr(self, "_dev_step", {}).get(id(group))
             if dev is None:
                 continue
-            t = float(dev[0].item())
+            if "t" in dev:
+                t = float(dev["t"].item())
+            elif dev["steps"]:
+                t = float(dev["steps"][0][0].item())
+            else:
+                continue
             for p in group["params"]:
                 if p in self.state and "step" in self.state[p]:
                     self.state[p]["step"].fill_(t)
@@ -138,14 +145,16 @@ class Adam(torch.optim.Adam):
                 continue
             stream = ctypes.c_void_p(_native.stream_handle(params[0].device))
             dev_scalars = None
+            tab = None
+            dev = None
             if self._graph_mode:
                 if len(by_step) != 1:
                     raise RuntimeError("siren_mri_amd.optim.Adam: graph mode needs one step count per group")
                 dev = self._dev_step.get(id(group))
                 if dev is None:
-                    t0 = next(iter(by_step)) - 1
-                    dev = (torch.full((1,), t0, dtype=torch.float64, device=params[0].device),
-                           torch.zeros(2, dtype=torch.float32, device=params[0].device))
+                    # {"t0": count before this step, "steps": per-launch workgroup counters (table form),
+                    #  "t": the group counter and "scalars" (computed form)}
+                    dev = {"t0": next(iter(by_step)) - 1, "steps": {}}
                     self._dev_step[id(group)] = dev
                 key = (float(group["lr"]), float(beta1), float(beta2))
                 tables = self.__dict__.setdefault("_tables", {})
@@ -153,15 +162,16 @@ class Adam(torch.optim.Adam):
                 if tab is None or tab[0] != key:
                     tab = (key, self._scalar_table(*key, params[0].device))
                     tables[id(group)] = tab
-                if tab[1] is not None:
-                    rc = lib.siren_adam_scalars_table(dev[0].data_ptr(), tab[1].data_ptr(), tab[1].shape[0],
-                                                      dev[1].data_ptr(), stream)
-                else:
-                    rc = lib.siren_adam_scalars(dev[0].data_ptr(), float(group["lr"]), float(beta1), float(beta2),
-                                                dev[1].data_ptr(), stream)
-                if rc != 0:
-                    raise _native.NativeError(_native.last_error())
-                dev_scalars = dev[1].data_ptr()
+                tab = tab[1]
+                if tab is None:
+                    if "t" not in dev:
+                        dev["t"] = torch.full((1,), dev["t0"], dtype=torch.float64, device=params[0].device)
+                        dev["scalars"] = torch.zeros(2, dtype=torch.float32, device=params[0].device)
+                    rc = lib.siren_adam_scalars(dev["t"].data_ptr(), float(group["lr"]), float(beta1), float(beta2),
+                                                dev["scalars"].data_ptr(), stream)
+                    if rc != 0:
+                        raise _native.NativeError(_native.last_error())
+                    dev_scalars = dev["scalars"].data_ptr()
             for t, plist in by_step.items():
                 bc1 = 1 - beta1 ** t
                 bc2 = 1 - beta2 ** t
@@ -183,6 +193,16 @@ class Adam(torch.optim.Adam):
                         d.grad[k] = p.grad.data_ptr()
                         d.exp_avg[k] = st["exp_avg"].data_ptr()
                         d.exp_avg_sq[k] = st["exp_avg_sq"].data_ptr()
+                    if tab is not None:
+                        # table form: the launch's workgroups each advance their own counter
+                        nblk = lib.siren_adam_num_blocks(ctypes.byref(d))
+                        cnt = dev["steps"].get(i0)
+                        if cnt is None or cnt.numel() != nblk:
+                            cnt = torch.full((max(nblk, 1),), dev["t0"], dtype=torch.float64, device=p.device)
+                            dev["steps"][i0] = cnt
+                        d.dev_steps = cnt.data_ptr()
+                        d.dev_table = tab.data_ptr()
+                        d.table_n = tab.shape[0]
                     if lib.siren_adam_step(ctypes.byref(d), stream) != 0:
                         raise _native.NativeError(_native.last_error())
         return loss

@@ -44,12 +44,17 @@ def test_adam_state_dict_round_trip_with_torch():
     assert torch.equal(o2.state[p]["exp_avg"], o1.state[p]["exp_avg"])
 
 
-@pytest.mark.parametrize("sizes", [(300,), (300000, 77, 256 * 256)])
-def test_adam_graph_mode_replay_matches_eager(sizes):
-    """enable_graph_mode(): bias corrections from a device step counter, so a hipGraph of the
-    step replays with the right t each time (same values as eager steps). One launch per group:
-    a single-thread launch per step advances the counter and looks the scalars up in a table."""
+@pytest.mark.parametrize("form", ["table", "computed"])
+@pytest.mark.parametrize("sizes", [(300,), (300000, 77, 256 * 256), tuple(range(1, 60))])
+def test_adam_graph_mode_replay_matches_eager(sizes, form, monkeypatch):
+    """enable_graph_mode(): bias corrections from device step counters, so a hipGraph of the
+    step replays with the right t each time (same values as eager steps). Table form: one launch
+    per chunk of tensors, its workgroups advancing their own counters (59 tensors: two
+    chunks); computed form (a table too long for the betas): a single-thread launch per step
+    advances the group counter and computes the scalars."""
     from siren_mri_amd.optim import Adam
+    if form == "computed":
+        monkeypatch.setattr(Adam, "_TABLE_MAX", 4)
     g = torch.Generator().manual_seed(1)
     inits = [torch.randn(n, generator=g) for n in sizes]
     grads = [[torch.randn(n, generator=g).to(DEV) for n in sizes] for _ in range(6)]

@@ -33,7 +33,7 @@ for st in "$@"; do
     c3prof)
       (cd /tmp && export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$out/c3prof -o c3 -- python3 $GRAFT_REPO_ROOT/bench.py --config c3 --no-cpu-baseline --no-psnr --no-other-configs --steps 5 --warmup 2 > $GRAFT_REPO_ROOT/$out/c3prof.log 2>&1) || exit $? ;;
     prof)
-      (cd /tmp && export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$out/prof -o m -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-psnr --no-other-configs --steps 20 --warmup 5 > $GRAFT_REPO_ROOT/$out/prof.log 2>&1) || exit $? ;;
+      (cd /tmp && export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$out/prof -o m -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-psnr --no-other-configs --steps 20 --warmup 5 > $GRAFT_REPO_ROOT/$out/prof.log 2>&1) || exit $? ;;
     probe)
       timeout -k 10 300 build/probe_store_hazard > $out/probe_store_hazard.txt 2>&1 || exit $? ;;
   esac
