@@ -38,6 +38,10 @@ struct TopArgs {
   float* partL;        // tn_dw only: dW_L / db_L partial slabs [split][nb][O*F_top + O]
   int64_t partL_stride;
   int O;
+  // pair_ring only: the output layer's dW_L / db_L sums are shared between the roles — the input-
+  // gradient role takes rows 0..15 of every 32-row tile (its dZ_top pass reads the same phases and
+  // dy) into slab npair + pair, the weight-gradient role rows 16..31 into slab pair
+  int dx_share;
 };
 // First-layer fusion into the bottom hidden layer's input-gradient kernel (C <= 4, no dx): the
 // epilogue accumulates dW_0 = dZ_0^T x and db_0 = sum dZ_0 (first_bwd_kernel's sums) instead of
@@ -1238,7 +1242,8 @@ DEV void dx_ring_body_v1(const NTArgs& a, char* smem, const int64_t t0, const in
 // through buffer resources bounded by the tile's valid rows (rows past the end arrive as zeros),
 // stores are buffer stores bounded the same way. One barrier per tile (two with TOPO).
 template <int TOPO>
-DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const int64_t G, const int64_t niter) {
+DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const int64_t G, const int64_t niter,
+                         const int64_t slab) {
   using PT = Prec<kPrecBF16>;
   constexpr int K = 256, N = 256, BM = RING_BM, S = RING_S;
   constexpr int G_BYTES = TOPO > 0 ? BM * TOPO * 4 : 0;
@@ -1278,6 +1283,17 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
     for (int o = 0; o < TOPO; ++o)
 #pragma unroll
       for (int e = 0; e < 8; ++e) twl[o][e] = a.top.WL[batch * a.top.wl_bstride + (int64_t)o * K + 8 * (tid & 31) + e] * a.w0;
+  }
+  // TOPO with dx_share: this thread's dW_L / db_L sums over rows tid / 32 of every tile (the
+  // weight-gradient role's arithmetic for those rows)
+  constexpr int TO = TOPO > 0 ? TOPO : 1;
+  const bool share = TOPO > 0 && a.top.dx_share;
+  float tdw[TO][8], tdb[TO];
+#pragma unroll
+  for (int o = 0; o < TO; ++o) {
+    tdb[o] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tdw[o][e] = 0.f;
   }
 
   // both images: row r (512 B), 16-byte chunk c stored at chunk c ^ (r & 15)
@@ -1387,6 +1403,18 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
           v[e] = (bf16)(dh * PT::cosp(ph[e]));
         }
         *(bf16x8*)pp = v;
+        if (q == 0 && share) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float sv = PT::sinp(ph[e]);
+#pragma unroll
+            for (int o = 0; o < TOPO; ++o) tdw[o][e] = fmaf(gg[o], sv, tdw[o][e]);
+          }
+          if (c == 0) {
+#pragma unroll
+            for (int o = 0; o < TOPO; ++o) tdb[o] += gg[o];
+          }
+        }
       }
     }
   };
@@ -1478,6 +1506,31 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
   };
   if (a.stagger && wave >= 4) loop(std::true_type{});
   else loop(std::false_type{});
+  if constexpr (TOPO > 0) {
+    if (share) {
+      // dW_L [O][K] and db_L [O] over the 16 row slots (dw_ring_body's slab form), slab `slab`
+      __syncthreads();
+      float* red = (float*)smem;
+      constexpr int RS = TOPO * 256 + TOPO;
+      const int cth = tid & 31, rth = tid >> 5;
+#pragma unroll
+      for (int o = 0; o < TOPO; ++o)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[rth * RS + o * 256 + 8 * cth + e] = tdw[o][e];
+      if (cth == 0) {
+#pragma unroll
+        for (int o = 0; o < TOPO; ++o) red[rth * RS + TOPO * 256 + o] = tdb[o];
+      }
+      __syncthreads();
+      float* pl = a.top.partL + slab * a.top.partL_stride + batch * (int64_t)RS;
+      for (int idx = tid; idx < RS; idx += 512) {
+        float sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sum += red[k * RS + idx];
+        pl[idx] = sum;
+      }
+    }
+  }
 }
 
 // dx_ring body of the bottom hidden layer with the first layer folded in and P_0 rebuilt from x
@@ -1733,7 +1786,7 @@ DEV void dx_ring_body_v2bot(const NTArgs& a, char* smem, const int64_t t0, const
 template <int BOTC, bool DXOUT, bool REC = false, int TOPO = 0>
 DEV void dx_ring_body(const NTArgs& a, char* smem, const int64_t t0, const int64_t G, const int64_t niter,
                       const int64_t slab) {
-  if constexpr (BOTC == 0) dx_ring_body_v2<TOPO>(a, smem, t0, G, niter);
+  if constexpr (BOTC == 0) dx_ring_body_v2<TOPO>(a, smem, t0, G, niter, slab);
   else if constexpr (REC) dx_ring_body_v2bot<BOTC, DXOUT>(a, smem, t0, G, niter, slab);
   else dx_ring_body_v1<BOTC, DXOUT, REC, TOPO>(a, smem, t0, G, niter, slab);
 }
@@ -1873,6 +1926,8 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
   constexpr int TO = TOPO > 0 ? TOPO : 1;
   float twl[TO][8], tdw[TO][8], tdb[TO];
   const float dys = (TOPO > 0 && a.top.dy_scale) ? *a.top.dy_scale : 1.f;
+  // pair_ring with dx_share: the input-gradient role sums rows 0..15 of each chunk
+  const bool share = TOPO > 0 && a.top.dx_share;
 #pragma unroll
   for (int o = 0; o < TO; ++o) {
     tdb[o] = 0.f;
@@ -1933,12 +1988,14 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
 #pragma unroll
         for (int o = 1; o < TO; ++o) dh = fmaf(gg[o], twl[o][e], dh);
         dz[e] = (bf16)(dh * PT::cosp(pt[e]));
-        const float sv = PT::sinp(pt[e]);
+        if (!share || qq == 1) {
+          const float sv = PT::sinp(pt[e]);
 #pragma unroll
-        for (int o = 0; o < TO; ++o) tdw[o][e] = fmaf(gg[o], sv, tdw[o][e]);
+          for (int o = 0; o < TO; ++o) tdw[o][e] = fmaf(gg[o], sv, tdw[o][e]);
+        }
       }
       *(bf16x8*)(Db + off) = dz;
-      if (cth == 0) {
+      if (cth == 0 && (!share || qq == 1)) {
 #pragma unroll
         for (int o = 0; o < TO; ++o) tdb[o] += gg[o];
       }
@@ -2123,7 +2180,7 @@ __global__ __launch_bounds__(512) void pair_ring_bf16_kernel(NTArgs ax, TNArgs a
   const int64_t tb = ntiles * pair / npair, te = ntiles * (pair + 1) / npair;
   if (((b >> 3) & 1) == 0) {
     if (!(aw.pair_roles & 1)) return;
-    dx_ring_body<BOTC, DXOUT, REC, TOPO>(ax, smem, tb, 1, te - tb, pair);
+    dx_ring_body<BOTC, DXOUT, REC, TOPO>(ax, smem, tb, 1, te - tb, TOPO > 0 ? npair + pair : pair);
   } else {
     const int64_t r_end = te * RING_BM < rows ? te * RING_BM : rows;
     if (aw.pair_roles & 2) dw_ring_body<RECC, TOPO>(aw, smem, tb * RING_BM, r_end, pair);

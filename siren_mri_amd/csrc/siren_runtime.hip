@@ -98,6 +98,7 @@ bool g_pair_ring = true;   // both gradients of a ring layer in one launch (pair
 int g_pair_roles = 3;      // debug timing: which pair_ring roles run (results are wrong unless 3)
 bool g_dx_stagger = false;  // middle/top input-gradient ring: staggered wave halves (measured slower: +5-9 us/step)
 bool g_tail_reduce = true;  // a pair launch reduces the previous pair launch's slabs (no reduce launch)
+bool g_top_share = false;   // top pair: the dx role takes half the rows of the output layer's dW_L / db_L sums (measured: no gain, +1 % step)
 long long* g_ring_prof = nullptr;   // debug: pair_ring segment cycle counters, one block per launch
 int g_ring_prof_n = 0;
 long long* g_fused_prof = nullptr;
@@ -286,7 +287,7 @@ Layout layout_of(const siren_mlp_desc* d) {
   if (g.L >= 3) {
     const int F = d->dims[g.L - 1], O = d->dims[g.L];
     const int64_t ns = std::max(std::max(tn_split(g, F, d->dims[g.L - 2]).nsplit, dw_ring_split(g).nsplit),
-                                pair_count(g));
+                                2 * pair_count(g));  // (top pair with the shared dW_L sums: 2 slabs a pair)
     off = align_up(off + ns * split_stride(g, (int64_t)O * F + O) * 4, 256);
   }
   lo.partB_off = off;
@@ -819,6 +820,9 @@ int launch_pair(const siren_mlp_desc* d, const Geo& g, const Layout& lo, int kin
     a.bot.split_stride = bot_stride;
     a.bot.C = C;
   }
+  // top pair: dW_L / db_L sums split between the roles (slabs pair and npair + pair)
+  const bool share = kind == 2 && g_top_share;
+  a.top.dx_share = w.top.dx_share = share ? 1 : 0;
   const dim3 grid((unsigned)(2 * npair), (unsigned)g.nb);
   const int kcls = kind == 1 ? SIREN_KCLASS_PAIR_RING : kind == 2 ? SIREN_KCLASS_PAIR_RING_TOP : SIREN_KCLASS_PAIR_RING_BOT;
   tmark_begin(kcls, st);
@@ -846,7 +850,7 @@ int launch_pair(const siren_mlp_desc* d, const Geo& g, const Layout& lo, int kin
   // this launch's slabs: reduced by the next pair launch, or by a reduce_multi launch (flush)
   ReduceList red;
   red.add(part, npair, w.split_stride, g.nb, (int64_t)M * N + M, (int64_t)M * N, dW[l], db[l]);
-  if (kind == 2) red.add(ta.partL, npair, ta.partL_stride, g.nb, (int64_t)O * M + O, (int64_t)O * M, dW[g.L - 1], db[g.L - 1]);
+  if (kind == 2) red.add(ta.partL, share ? 2 * npair : npair, ta.partL_stride, g.nb, (int64_t)O * M + O, (int64_t)O * M, dW[g.L - 1], db[g.L - 1]);
   if (kind == 3) red.add(a.bot.part, npair, bot_stride, g.nb, (int64_t)F0 * C + F0, (int64_t)F0 * C, dW[0], db[0]);
   pend = red;
   return SIREN_OK;
@@ -2145,6 +2149,10 @@ int siren_config_set(const char* key, int64_t value) {
     g_tail_reduce = value != 0;
     return SIREN_OK;
   }
+  if (key && strcmp(key, "top_share") == 0 && (value == 0 || value == 1)) {
+    g_top_share = value != 0;
+    return SIREN_OK;
+  }
   if (key && strcmp(key, "pair_ring") == 0 && (value == 0 || value == 1)) {
     g_pair_ring = value != 0;
     return SIREN_OK;
@@ -2178,6 +2186,7 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "dw_ring") == 0) return g_dw_ring ? 1 : 0;
   if (key && strcmp(key, "bwd_ring") == 0) return g_bwd_ring ? 1 : 0;
   if (key && strcmp(key, "pair_tail_reduce") == 0) return g_tail_reduce ? 1 : 0;
+  if (key && strcmp(key, "top_share") == 0) return g_top_share ? 1 : 0;
   if (key && strcmp(key, "dx_stagger") == 0) return g_dx_stagger ? 1 : 0;
   if (key && strcmp(key, "pair_ring") == 0) return g_pair_ring ? 1 : 0;
   if (key && strcmp(key, "debug_keep_p0") == 0) return g_keep_p0 ? 1 : 0;
