@@ -99,6 +99,9 @@ struct TNArgs {
   int64_t rec_b0_bstride;
   TopArgs top;         // TOP: D = dZ_top formed from P_top, dy and W_L; also dW_L / db_L partials
   int pair_roles;      // pair_ring (debug timing only): bit 0 runs the dx role, bit 1 the dw role
+  int pair_nx;         // pair_ring: 0 = paired mapping (npair + npair); else the first pair_nx workgroups
+                       // take the input-gradient role and the rest the weight-gradient role, each
+                       // role's workgroups splitting the tiles evenly among themselves
   long long* prof;     // debug: [grid.x][8 waves][RING_NPROF] segment cycle counters (null: off)
 };
 
@@ -2173,17 +2176,33 @@ __global__ __launch_bounds__(512) void pair_ring_bf16_kernel(NTArgs ax, TNArgs a
   constexpr int LX = dx_ring_lds_bytes<BOTC, TOPO>(), LW = dw_ring_lds_bytes<RECC, TOPO>();
   __shared__ __attribute__((aligned(16))) char smem[LX > LW ? LX : LW];
   const int b = blockIdx.x;
-  const int64_t pair = (b & 7) | ((b >> 4) << 3);
-  const int64_t npair = gridDim.x >> 1;
+  const int64_t G = gridDim.x;
   const int64_t rows = ax.rows_per_batch;
   const int64_t ntiles = (rows + RING_BM - 1) / RING_BM;
-  const int64_t tb = ntiles * pair / npair, te = ntiles * (pair + 1) / npair;
-  if (((b >> 3) & 1) == 0) {
+  // role, index within the role, workgroups of the role; nw = weight-gradient workgroups (slabs)
+  bool dxrole;
+  int64_t idx, nrole, nw;
+  if (aw.pair_nx <= 0) {
+    idx = (b & 7) | ((b >> 4) << 3);
+    nrole = nw = G >> 1;
+    dxrole = ((b >> 3) & 1) == 0;
+  } else {
+    // uneven split (the input-gradient role is the slower one): the roles no longer walk the same
+    // tiles on one XCD, but both sweep the rows front to back at the same pace
+    const int64_t nx = aw.pair_nx;
+    nw = G - nx;
+    dxrole = b < nx;
+    idx = dxrole ? b : b - nx;
+    nrole = dxrole ? nx : nw;
+  }
+  const int64_t tb = ntiles * idx / nrole, te = ntiles * (idx + 1) / nrole;
+  if (dxrole) {
     if (!(aw.pair_roles & 1)) return;
-    dx_ring_body<BOTC, DXOUT, REC, TOPO>(ax, smem, tb, 1, te - tb, TOPO > 0 ? npair + pair : pair);
+    // slab: the first-layer slab (BOTC), or the shared output-layer slab after the nw of the other role
+    dx_ring_body<BOTC, DXOUT, REC, TOPO>(ax, smem, tb, 1, te - tb, TOPO > 0 ? nw + idx : idx);
   } else {
     const int64_t r_end = te * RING_BM < rows ? te * RING_BM : rows;
-    if (aw.pair_roles & 2) dw_ring_body<RECC, TOPO>(aw, smem, tb * RING_BM, r_end, pair);
+    if (aw.pair_roles & 2) dw_ring_body<RECC, TOPO>(aw, smem, tb * RING_BM, r_end, idx);
     // tail: the previous pair launch's slab reduction (this role finishes ahead of the
     // input-gradient role), 128-float blocks dealt over the weight-gradient workgroups, two
     // 256-thread groups each; reduce_multi_kernel's block body and summation order
@@ -2191,7 +2210,7 @@ __global__ __launch_bounds__(512) void pair_ring_bf16_kernel(NTArgs ax, TNArgs a
       __syncthreads();
       f32x4(*red)[32] = (f32x4(*)[32])(smem + (threadIdx.x >> 8) * (8 * 32 * 16));
       const int nblk = reduce_total_blocks(prev);
-      const int wg = (int)(pair + npair * blockIdx.y), per = (int)(2 * npair * gridDim.y);
+      const int wg = (int)(idx + nw * blockIdx.y), per = (int)(2 * nw * gridDim.y);
       for (int k = 0; k * per < nblk; ++k) reduce_block(prev, k * per + 2 * wg + (threadIdx.x >> 8), threadIdx.x & 255, red);
     }
   }

@@ -98,6 +98,9 @@ bool g_pair_ring = true;   // both gradients of a ring layer in one launch (pair
 int g_pair_roles = 3;      // debug timing: which pair_ring roles run (results are wrong unless 3)
 bool g_dx_stagger = false;  // middle/top input-gradient ring: staggered wave halves (measured slower: +5-9 us/step)
 bool g_tail_reduce = true;  // a pair launch reduces the previous pair launch's slabs (no reduce launch)
+// pair_ring role split, input-gradient workgroups per 32 of the grid, per pair kind (middle, top,
+// bottom); 16 = the paired mapping (npair + npair, same tiles on one XCD)
+int g_pair_split[3] = {16, 16, 16};
 bool g_top_share = false;   // top pair: the dx role takes half the rows of the output layer's dW_L / db_L sums (measured: no gain, +1 % step)
 long long* g_ring_prof = nullptr;   // debug: pair_ring segment cycle counters, one block per launch
 int g_ring_prof_n = 0;
@@ -291,7 +294,8 @@ Layout layout_of(const siren_mlp_desc* d) {
     off = align_up(off + ns * split_stride(g, (int64_t)O * F + O) * 4, 256);
   }
   lo.partB_off = off;
-  if (lo.p0_rec) off = align_up(off + kMaxPairs * split_stride(g, (int64_t)d->dims[1] * d->dims[0] + d->dims[1]) * 4, 256);
+  // (the bottom pair's input-gradient role: up to 2 npair - 8 first-layer slabs, pair_split)
+  if (lo.p0_rec) off = align_up(off + 2 * kMaxPairs * split_stride(g, (int64_t)d->dims[1] * d->dims[0] + d->dims[1]) * 4, 256);
   lo.xcopy_off = off;
   if (lo.p0_rec) off = align_up(off + g.total * d->dims[0] * 4, 256);
   // paired 256x256 layers alternate between part and part2: a pair launch reduces the previous
@@ -823,6 +827,15 @@ int launch_pair(const siren_mlp_desc* d, const Geo& g, const Layout& lo, int kin
   // top pair: dW_L / db_L sums split between the roles (slabs pair and npair + pair)
   const bool share = kind == 2 && g_top_share;
   a.top.dx_share = w.top.dx_share = share ? 1 : 0;
+  // role split: nx input-gradient + nw weight-gradient workgroups (nw <= npair: the slab buffers)
+  int64_t nx = npair, nw = npair;
+  w.pair_nx = 0;
+  const int split = g_pair_split[kind - 1];
+  if (split != 16) {
+    nx = std::min<int64_t>(2 * npair - 8, std::max<int64_t>(npair, (2 * npair * split / 32) / 8 * 8));
+    nw = 2 * npair - nx;
+    if (nx != npair) w.pair_nx = (int)nx;
+  }
   const dim3 grid((unsigned)(2 * npair), (unsigned)g.nb);
   const int kcls = kind == 1 ? SIREN_KCLASS_PAIR_RING : kind == 2 ? SIREN_KCLASS_PAIR_RING_TOP : SIREN_KCLASS_PAIR_RING_BOT;
   tmark_begin(kcls, st);
@@ -849,9 +862,9 @@ int launch_pair(const siren_mlp_desc* d, const Geo& g, const Layout& lo, int kin
   if (rc) return rc;
   // this launch's slabs: reduced by the next pair launch, or by a reduce_multi launch (flush)
   ReduceList red;
-  red.add(part, npair, w.split_stride, g.nb, (int64_t)M * N + M, (int64_t)M * N, dW[l], db[l]);
-  if (kind == 2) red.add(ta.partL, share ? 2 * npair : npair, ta.partL_stride, g.nb, (int64_t)O * M + O, (int64_t)O * M, dW[g.L - 1], db[g.L - 1]);
-  if (kind == 3) red.add(a.bot.part, npair, bot_stride, g.nb, (int64_t)F0 * C + F0, (int64_t)F0 * C, dW[0], db[0]);
+  red.add(part, nw, w.split_stride, g.nb, (int64_t)M * N + M, (int64_t)M * N, dW[l], db[l]);
+  if (kind == 2) red.add(ta.partL, share ? nw + nx : nw, ta.partL_stride, g.nb, (int64_t)O * M + O, (int64_t)O * M, dW[g.L - 1], db[g.L - 1]);
+  if (kind == 3) red.add(a.bot.part, nx, bot_stride, g.nb, (int64_t)F0 * C + F0, (int64_t)F0 * C, dW[0], db[0]);
   pend = red;
   return SIREN_OK;
 }
@@ -2149,6 +2162,14 @@ int siren_config_set(const char* key, int64_t value) {
     g_tail_reduce = value != 0;
     return SIREN_OK;
   }
+  if (key && strncmp(key, "pair_split_", 11) == 0 && value >= 16 && value <= 31) {
+    const char* k = key + 11;
+    const int i = strcmp(k, "mid") == 0 ? 0 : strcmp(k, "top") == 0 ? 1 : strcmp(k, "bot") == 0 ? 2 : -1;
+    if (i >= 0) {
+      g_pair_split[i] = (int)value;
+      return SIREN_OK;
+    }
+  }
   if (key && strcmp(key, "top_share") == 0 && (value == 0 || value == 1)) {
     g_top_share = value != 0;
     return SIREN_OK;
@@ -2187,6 +2208,9 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "bwd_ring") == 0) return g_bwd_ring ? 1 : 0;
   if (key && strcmp(key, "pair_tail_reduce") == 0) return g_tail_reduce ? 1 : 0;
   if (key && strcmp(key, "top_share") == 0) return g_top_share ? 1 : 0;
+  if (key && strcmp(key, "pair_split_mid") == 0) return g_pair_split[0];
+  if (key && strcmp(key, "pair_split_top") == 0) return g_pair_split[1];
+  if (key && strcmp(key, "pair_split_bot") == 0) return g_pair_split[2];
   if (key && strcmp(key, "dx_stagger") == 0) return g_dx_stagger ? 1 : 0;
   if (key && strcmp(key, "pair_ring") == 0) return g_pair_ring ? 1 : 0;
   if (key && strcmp(key, "debug_keep_p0") == 0) return g_keep_p0 ? 1 : 0;
