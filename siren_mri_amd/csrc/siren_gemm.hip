@@ -1290,7 +1290,7 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
   // TOPO with dx_share: this thread's dW_L / db_L sums over rows tid / 32 of every tile (the
   // weight-gradient role's arithmetic for those rows)
   constexpr int TO = TOPO > 0 ? TOPO : 1;
-  const bool share = TOPO > 0 && a.top.dx_share;
+  const bool share = TOPO > 0 && (a.top.dx_share & 1);
   float tdw[TO][8], tdb[TO];
 #pragma unroll
   for (int o = 0; o < TO; ++o) {
@@ -1386,6 +1386,7 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
   // separates it from the MFMAs that read it (the next iteration's barrier publishes it)
   auto top_pass = [&](int st) {
     if constexpr (TOPO > 0) {
+      if (a.top.dx_share & 2) return;  // debug timing only (results wrong): no dZ_top pass
       char* base = smem + st * STAGE;
       const float* gt = (const float*)(base + A_BYTES + C_BYTES);
 #pragma unroll
@@ -1467,7 +1468,7 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
       // this stage's DMA (this wave's part) landed; then every wave's part, and every wave is done
       // with the stage the next DMA overwrites (tile i - 1: MFMA reads and its store pass)
       if (io) {
-        if constexpr (TOPO > 0) {
+        if (TOPO > 0 && !(a.top.dx_share & 4)) {  // (4: debug timing only, the plain ring's wait)
           if (i + 1 < niter) {
             if (i >= S - 2 && i + S - 2 < niter) vm_wait<STEADY_T>();
             else vm_drain();
@@ -1930,7 +1931,7 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
   float twl[TO][8], tdw[TO][8], tdb[TO];
   const float dys = (TOPO > 0 && a.top.dy_scale) ? *a.top.dy_scale : 1.f;
   // pair_ring with dx_share: the input-gradient role sums rows 0..15 of each chunk
-  const bool share = TOPO > 0 && a.top.dx_share;
+  const bool share = TOPO > 0 && (a.top.dx_share & 1);
 #pragma unroll
   for (int o = 0; o < TO; ++o) {
     tdb[o] = 0.f;

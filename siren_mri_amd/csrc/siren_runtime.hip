@@ -101,7 +101,8 @@ bool g_tail_reduce = true;  // a pair launch reduces the previous pair launch's 
 // pair_ring role split, input-gradient workgroups per 32 of the grid, per pair kind (middle, top,
 // bottom); 16 = the paired mapping (npair + npair, same tiles on one XCD)
 int g_pair_split[3] = {16, 16, 16};
-bool g_top_share = false;   // top pair: the dx role takes half the rows of the output layer's dW_L / db_L sums (measured: no gain, +1 % step)
+bool g_top_share = false;
+int g_top_debug = 0;  // debug timing only (results wrong unless 0): top pair dx role, 2 = no dZ_top pass, 4 = plain ring wait   // top pair: the dx role takes half the rows of the output layer's dW_L / db_L sums (measured: no gain, +1 % step)
 long long* g_ring_prof = nullptr;   // debug: pair_ring segment cycle counters, one block per launch
 int g_ring_prof_n = 0;
 long long* g_fused_prof = nullptr;
@@ -826,7 +827,7 @@ int launch_pair(const siren_mlp_desc* d, const Geo& g, const Layout& lo, int kin
   }
   // top pair: dW_L / db_L sums split between the roles (slabs pair and npair + pair)
   const bool share = kind == 2 && g_top_share;
-  a.top.dx_share = w.top.dx_share = share ? 1 : 0;
+  a.top.dx_share = w.top.dx_share = (share ? 1 : 0) | (kind == 2 ? g_top_debug : 0);
   // role split: nx input-gradient + nw weight-gradient workgroups (nw <= npair: the slab buffers)
   int64_t nx = npair, nw = npair;
   w.pair_nx = 0;
@@ -2170,6 +2171,10 @@ int siren_config_set(const char* key, int64_t value) {
       return SIREN_OK;
     }
   }
+  if (key && strcmp(key, "debug_top_pass") == 0 && (value == 0 || value == 2 || value == 4 || value == 6)) {
+    g_top_debug = (int)value;
+    return SIREN_OK;
+  }
   if (key && strcmp(key, "top_share") == 0 && (value == 0 || value == 1)) {
     g_top_share = value != 0;
     return SIREN_OK;
@@ -2208,6 +2213,7 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "bwd_ring") == 0) return g_bwd_ring ? 1 : 0;
   if (key && strcmp(key, "pair_tail_reduce") == 0) return g_tail_reduce ? 1 : 0;
   if (key && strcmp(key, "top_share") == 0) return g_top_share ? 1 : 0;
+  if (key && strcmp(key, "debug_top_pass") == 0) return g_top_debug;
   if (key && strcmp(key, "pair_split_mid") == 0) return g_pair_split[0];
   if (key && strcmp(key, "pair_split_top") == 0) return g_pair_split[1];
   if (key && strcmp(key, "pair_split_bot") == 0) return g_pair_split[2];
