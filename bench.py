@@ -294,8 +294,9 @@ def build_c4(args, dev, rank, world, precision, encoder_precision="bf16"):
     params = [p for p in model.parameters() if p.requires_grad]
 
     def step():
-        mi = dict(inp)
-        mi["coords"] = ff(inp["coords"])
+        # training.train's transform step: raw coordinates + B for the hypernetwork, whose SIREN forms
+        # the Fourier features in its first layer (features.py model_input)
+        mi = ff.model_input(model, dict(inp))
         fusion.stage_image_loss(gt["img"])  # as training.train: the fused DC + loss epilogue
         out = model(mi)
         losses = loss_fn(out, gt)

@@ -64,6 +64,13 @@ typedef struct siren_mlp_desc {
   int64_t rows_per_batch;
   const float* weight[SIREN_MAX_LAYERS];
   const float* bias[SIREN_MAX_LAYERS];
+  /* Fourier-feature input (features.py:21-41, applied by training.py:61-64 before the model)
+   * computed in the first layer instead of materialised: when ff_B is non-NULL, x holds ff_in raw
+   * coordinates per row and the first layer's dims[0] = 2m inputs are
+   * cat(sin(2 pi x B), cos(2 pi x B)) with B = ff_B [ff_in][m]. bf16 mode, the register-resident
+   * forward's wide first layer (dims[0] even, 6..16), ff_in 1..4; no input gradient (dx NULL). */
+  const float* ff_B;
+  int32_t ff_in;
 } siren_mlp_desc;
 
 /* Validates a descriptor; returns SIREN_OK or SIREN_EINVAL (message in siren_last_error). */

@@ -101,6 +101,8 @@ class SirenMLPDesc(ctypes.Structure):
         ("rows_per_batch", ctypes.c_int64),
         ("weight", ctypes.c_void_p * MAX_LAYERS),
         ("bias", ctypes.c_void_p * MAX_LAYERS),
+        ("ff_B", ctypes.c_void_p),
+        ("ff_in", ctypes.c_int32),
     ]
 
 
@@ -361,7 +363,7 @@ def enc_workspace(device) -> torch.Tensor:
 
 
 def make_desc(dims, weights, biases, *, w0: float, prec: int, outermost_linear: bool,
-              weights_batched: bool, batch: int, rows_per_batch: int) -> SirenMLPDesc:
+              weights_batched: bool, batch: int, rows_per_batch: int, ff_B=None) -> SirenMLPDesc:
     L = len(dims) - 1
     if not 2 <= L <= MAX_LAYERS:
         raise ValueError(f"siren_mri_amd: {L} linear layers outside [2, {MAX_LAYERS}]")
@@ -378,11 +380,14 @@ def make_desc(dims, weights, biases, *, w0: float, prec: int, outermost_linear: 
     for l in range(L):
         d.weight[l] = weights[l].data_ptr()
         d.bias[l] = biases[l].data_ptr()
+    if ff_B is not None:  # Fourier-feature input: x holds the raw coordinates
+        d.ff_B = ff_B.data_ptr()
+        d.ff_in = int(ff_B.shape[0])
     return d
 
 
 def describe_only(dims, *, prec: int, outermost_linear: bool = True, weights_batched: bool = False,
-                  batch: int = 1, rows_per_batch: int = 1, w0: float = 30.0):
+                  batch: int = 1, rows_per_batch: int = 1, w0: float = 30.0, ff_in: int = 0):
     """Descriptor with fake (aligned, non-null) pointers — for size queries and validation."""
     L = len(dims) - 1
     d = SirenMLPDesc()
@@ -398,6 +403,9 @@ def describe_only(dims, *, prec: int, outermost_linear: bool = True, weights_bat
     for l in range(L):
         d.weight[l] = 256 * (l + 1)
         d.bias[l] = 256 * (l + 1) + 64
+    if ff_in:
+        d.ff_B = 256 * (L + 2)
+        d.ff_in = int(ff_in)
     return d
 
 

@@ -86,6 +86,26 @@ DEV float cos_f32(float x) {
   return ((q + 1) & 2) ? -v : v;
 }
 
+// Fourier feature f of a row (features.py:21-41 as siren_kspace.hip fourier_kernel computes it,
+// with sin_f32 / cos_f32 for sincosf): z = sum_c x[c] B[c][k] (fma chain from 0), k = f mod m,
+// sin(2 pi z) for f < m, cos(2 pi z) for m <= f < 2m, 0 past 2m. Arguments stay inside the
+// Cody-Waite range for any |x| <= 1 coordinates and |B| entries below ~4000 (no far path here).
+DEV float ff_feature(const float* xr, const float* B, int cin, int m, int f) {
+  if (f >= 2 * m) return 0.f;
+  const bool cosine = f >= m;
+  const int k = cosine ? f - m : f;
+  float z = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)  // (compile-time indices into the caller's register array; cin <= 4)
+    if (c < cin) z = fmaf(xr[c], B[c * m + k], z);
+  float sn, cs;
+  int q;
+  sincos_poly(__fmul_rn(6.2831854820251465f, z), sn, cs, q);
+  q += cosine ? 1 : 0;  // cos x = sin(x + pi / 2): one quadrant on
+  const float v = (q & 1) ? cs : sn;
+  return (q & 2) ? -v : v;
+}
+
 template <> struct Prec<kPrecF32> {
   using phase_t = float;
   using grad_t = float;

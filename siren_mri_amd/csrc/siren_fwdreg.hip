@@ -116,6 +116,10 @@ struct FwdRegArgs {
   int O, nh, sine_out;
   int cin;                    // inputs of layer 0 (= C, or 5..16 for the wide form C = 16)
   float w0;
+  // wide form: Fourier-feature input (siren_mlp_desc.ff_B): x holds ffin raw coordinates per row and
+  // layer 0's cin = 2m inputs are computed from them and ffB [ffin][m] (ff_feature)
+  const float* ffB;
+  int ffin;
   // LOSS instantiations: image_mse's (masked k-space) SSE of the output,
   // with the data consistency of DataConsistencyInKspace applied first, in the output layer's
   // epilogue. Layouts as siren_kspace.hip: rows [B*N, O]; k0 / mask NCHW planes [B, O, N].
@@ -238,7 +242,9 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   constexpr bool WIDE = C > 4;
   constexpr int NKK = WIDE ? 1 : (C + 1) / 2;  // K pairs of the f32 layer-0 MFMA (narrow form)
   constexpr int MAXH_ = WIDE ? FREG_WIDE_MAXH : FUSED_MAXH;
-  static_assert((C >= 1 && C <= 4) || C == 16, "1..4 inputs, or the wide form (C = 16: 5..16 inputs)");
+  static_assert((C >= 1 && C <= 4) || C == 16 || C == 17,
+                "1..4 inputs, or the wide form (C = 16: 5..16 inputs; C = 17: the same from the Fourier-feature input)");
+  constexpr bool FFI = C == 17;  // wide form, layer 0's inputs formed from raw coordinates (ff_feature)
   // the ring's 8 slots as separate objects: the compiler's wait-count pass then knows that a read
   // of slot fb cannot alias the LDS-DMA just issued into slot fb - 1 (one array would put an
   // s_waitcnt vmcnt(0) in front of every fragment read after a refill)
@@ -262,6 +268,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   __shared__ __attribute__((aligned(16))) char w0f[WIDE ? FREG_W0F_BYTES : 16];  // wide layer-0 fragments
   __shared__ __attribute__((aligned(16))) float sbl[8];
   __shared__ __attribute__((aligned(16))) float w0s[WIDE ? 4 : NB * NKK * 64];  // narrow layer-0 A operands
+  __shared__ float sffB[FFI ? 32 : 1];  // C = 17: the Fourier-feature input's B [ffin][m]
 
 #ifdef SIREN_FREG_DBG
   // timing builds only (compile-time, so the schedule of the rest is unchanged): 1: no hidden-
@@ -314,6 +321,8 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
       sbias[(l + 1) * F + i] = unsafe ? bk : __builtin_amdgcn_fractf(bk) + FREG_MAGIC;
     }
   if (tid < 8) sbl[tid] = tid < O ? a.bL[wb * O + tid] : 0.f;
+  constexpr bool ffin_on = FFI;
+  if (FFI && tid < 32) sffB[tid] = tid < a.ffin * (a.cin / 2) ? a.ffB[tid] : 0.f;
   if (tid < FREG_WL_BYTES / 16)
     *(u32x4_t*)(wlf + 16 * tid) = *(const u32x4_t*)((const char*)(a.WLreg + wb * (FREG_WL_BYTES / 2)) + 16 * tid);
   if (tid == FREG_WL_BYTES / 16) *(u32x4_t*)(wlf + FREG_WL_BYTES) = u32x4_t{0u, 0u, 0u, 0u};
@@ -360,11 +369,20 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   };
   // wide: the lane's 8 inputs 8 hh .. 8 hh + 7 of its row of tile t, straight from global memory
   // into registers (rows past the end and inputs past cin read as 0); issued a layer ahead
-  float xw[WIDE ? 8 : 1];
+  float xw[WIDE ? (FFI ? 4 : 8) : 1];  // (C = 17: the row's raw coordinates)
   auto load_xw = [&](int64_t t) {
     if constexpr (!WIDE) return;
     const int64_t r0 = t * FREG_WG_ROWS;
     const int64_t nv = rows - r0 < 0 ? 0 : (rows - r0 < FREG_WG_ROWS ? rows - r0 : FREG_WG_ROWS);
+    if constexpr (ffin_on) {
+      // the row's raw coordinates (the features are formed at layer 0 from these)
+      const int fin = a.ffin;
+      const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.x + (batch * rows + r0) * fin, nv * fin * 4);
+      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rr, (uint32_t)((wave * FREG_WROWS + j) * fin) * 4, 0, 0);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) xw[m] = m < fin ? __builtin_bit_cast(float, v[m]) : 0.f;
+      return;
+    }
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x + (batch * rows + r0) * cin, nv * cin * 4);
     // two 16-byte loads from the lane's first input (dword-aligned; inputs past cin belong to the
     // next row and are zeroed, rows past the end read as 0 through the resource)
@@ -739,10 +757,22 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
 #pragma unroll
         for (int kk = 0; kk < NKK; ++kk) xr[kk] = (2 * kk + hh) < C ? xt[2 * kk + hh] : 0.f;
       } else {
+        if constexpr (ffin_on) {
+          // Fourier features 8 hh .. 8 hh + 7 of the lane's row from its raw coordinates, one at a
+          // time, each split into its f16 hi / lo parts at once (eight fp32 features in flight spilled)
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-          xh[m] = (_Float16)xw[m];
-          xl[m] = (_Float16)(xw[m] - (float)xh[m]);
+          for (int m = 0; m < 8; ++m) {
+            const float f = ff_feature(xw, sffB, a.ffin, cin / 2, 8 * hh + m);
+            xh[m] = (_Float16)f;
+            xl[m] = (_Float16)(f - (float)xh[m]);
+            asm volatile("" : "+v"(xh), "+v"(xl));
+          }
+        } else {
+#pragma unroll
+          for (int m = 0; m < 8; ++m) {
+            xh[m] = (_Float16)xw[m];
+            xl[m] = (_Float16)(xw[m] - (float)xh[m]);
+          }
         }
       }
       // block fb + 1's MFMAs are issued before block fb's epilogue (its result latency and the

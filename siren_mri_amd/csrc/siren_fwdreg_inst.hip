@@ -19,6 +19,8 @@ SIREN_FREG_INST(2, 1)
 SIREN_FREG_INST(3, 1)
 SIREN_FREG_INST(4, 1)
 SIREN_FREG_INST(16, 1)
+SIREN_FREG_INST(17, 0)
+SIREN_FREG_INST(17, 1)
 // the fused-loss forms (fract epilogue only): the coordinate fits (1..4 inputs, one output) and the
 // hypernetwork's wide form (Fourier features, one or more outputs)
 template __global__ void fused_fwd_reg_kernel<1, 1, 0, true>(FwdRegArgs);
@@ -27,6 +29,8 @@ template __global__ void fused_fwd_reg_kernel<3, 1, 0, true>(FwdRegArgs);
 template __global__ void fused_fwd_reg_kernel<4, 1, 0, true>(FwdRegArgs);
 template __global__ void fused_fwd_reg_kernel<16, 0, 0, true>(FwdRegArgs);
 template __global__ void fused_fwd_reg_kernel<16, 1, 0, true>(FwdRegArgs);
+template __global__ void fused_fwd_reg_kernel<17, 0, 0, true>(FwdRegArgs);
+template __global__ void fused_fwd_reg_kernel<17, 1, 0, true>(FwdRegArgs);
 #endif
 #undef SIREN_FREG_INST
 

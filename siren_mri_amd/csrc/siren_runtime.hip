@@ -440,6 +440,12 @@ template <int PREC>
 int dispatch_first_bwd(const FirstBwdArgs& a, int64_t nsplit, int64_t nb, hipStream_t st) {
   const int it = (int)cdiv(a.F, 256);
   dim3 grid((unsigned)nsplit, (unsigned)nb);
+  if (a.ffB) {  // Fourier-feature input: the MFMA weight-gradient kernel forms the features itself
+    if (!(PREC == kPrecBF16 && a.F == 256 && a.C > 4 && a.rows_per_split % 32 == 0 && !a.dx))
+      return fail(SIREN_EINVAL, "fourier input: first-layer backward needs the bf16 wide MFMA path and no dx");
+    hipLaunchKernelGGL(first_bwd_wide_mfma_kernel, grid, dim3(256), 0, st, a);
+    return check_launch("first_bwd_wide_mfma (fourier input)");
+  }
   if (a.C <= 4) {
     if (it == 1) hipLaunchKernelGGL((first_bwd_kernel<PREC, 1, 4>), grid, dim3(256), 0, st, a);
     else if (it == 2) hipLaunchKernelGGL((first_bwd_kernel<PREC, 2, 4>), grid, dim3(256), 0, st, a);
@@ -579,6 +585,8 @@ int fused_forward_reg(const siren_mlp_desc* d, const Geo& g, const Layout& lo, c
   a.sine_out = d->outermost_linear ? 0 : 1;
   a.cin = d->dims[0];
   a.w0 = d->w0;
+  a.ffB = d->ff_B;
+  a.ffin = d->ff_B ? d->ff_in : 0;
   if (L) {
     a.ltgt = L->target;
     a.lk0 = L->k0;
@@ -600,14 +608,17 @@ int fused_forward_reg(const siren_mlp_desc* d, const Geo& g, const Layout& lo, c
   static const KernelFn table[2][FUSED_MAXC][2] = {
       {SIREN_FREG_FORMS(1, 0), SIREN_FREG_FORMS(2, 0), SIREN_FREG_FORMS(3, 0), SIREN_FREG_FORMS(4, 0)},
       {SIREN_FREG_FORMS(1, 1), SIREN_FREG_FORMS(2, 1), SIREN_FREG_FORMS(3, 1), SIREN_FREG_FORMS(4, 1)}};
-  static const KernelFn wide[2][2] = {SIREN_FREG_FORMS(16, 0), SIREN_FREG_FORMS(16, 1)};
+  static const KernelFn wide[2][2][2] = {{SIREN_FREG_FORMS(16, 0), SIREN_FREG_FORMS(16, 1)},
+                                         {SIREN_FREG_FORMS(17, 0), SIREN_FREG_FORMS(17, 1)}};
 #undef SIREN_FREG_FORMS
-  const KernelFn* k = fused_wide(d) ? wide[a.O == 1 ? 1 : 0] : table[a.O == 1 ? 1 : 0][d->dims[0] - 1];
+  const int ffi = d->ff_B ? 1 : 0;  // C = 17: the Fourier-feature input (siren_mlp_check: wide shapes only)
+  const KernelFn* k = fused_wide(d) ? wide[ffi][a.O == 1 ? 1 : 0] : table[a.O == 1 ? 1 : 0][d->dims[0] - 1];
   if (L) {  // the fused-loss forms (siren_mlp_loss_check admitted this shape)
     static const KernelFn lnarrow[FUSED_MAXC] = {fused_fwd_reg_kernel<1, 1, 0, true>, fused_fwd_reg_kernel<2, 1, 0, true>,
                                                  fused_fwd_reg_kernel<3, 1, 0, true>, fused_fwd_reg_kernel<4, 1, 0, true>};
-    static const KernelFn lwide[2] = {fused_fwd_reg_kernel<16, 0, 0, true>, fused_fwd_reg_kernel<16, 1, 0, true>};
-    const KernelFn kl = fused_wide(d) ? lwide[a.O == 1 ? 1 : 0] : lnarrow[d->dims[0] - 1];
+    static const KernelFn lwide[2][2] = {{fused_fwd_reg_kernel<16, 0, 0, true>, fused_fwd_reg_kernel<16, 1, 0, true>},
+                                         {fused_fwd_reg_kernel<17, 0, 0, true>, fused_fwd_reg_kernel<17, 1, 0, true>}};
+    const KernelFn kl = fused_wide(d) ? lwide[ffi][a.O == 1 ? 1 : 0] : lnarrow[d->dims[0] - 1];
     a.wbound = nullptr;  // the fract form alone (no magic-form exit test on an unwritten bound)
     tmark_begin(SIREN_KCLASS_FWD_FUSED, st);
     hipLaunchKernelGGL(kl, grid, dim3(512), 0, st, a);
@@ -1165,8 +1176,11 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
   } else {
     const Split s = valu_split(g);
     FirstBwdArgs a;
+    memset(&a, 0, sizeof(a));
     a.dZ = ws + lo.dz_off[cur];
     a.x = x;
+    a.ffB = d->ff_B;
+    a.ffin = d->ff_B ? d->ff_in : 0;
     a.W = d->weight[0];
     a.dx = dx;
     a.part = part;
@@ -1509,6 +1523,15 @@ int siren_mlp_check(const siren_mlp_desc* d) {
     if (!d->weight[l] || !d->bias[l]) return fail(SIREN_EINVAL, "layer %d: null weight/bias", l);
   for (int l = 1; l + 1 < L; ++l)
     if (!aligned16(d->weight[l])) return fail(SIREN_EINVAL, "layer %d weight not 16-B aligned", l);
+  if (d->ff_B) {
+    if (d->ff_in < 1 || d->ff_in > 4 || d->dims[0] % 2 || d->ff_in * (d->dims[0] / 2) > 32)
+      return fail(SIREN_EINVAL, "fourier input: ff_in=%d raw coordinates (1..4) for %d features (even)", d->ff_in,
+                  d->dims[0]);
+    if (d->prec != SIREN_PREC_BF16 || !g_fused_forward || !g_fwd_reg || !fused_shape(d) || !fused_wide(d) || L < 3 ||
+        d->dims[1] != 256)
+      return fail(SIREN_EINVAL, "fourier input: needs the bf16 register-resident forward's wide first layer "
+                                "(6..16 features, hidden 256)");
+  }
   return SIREN_OK;
 }
 
@@ -1556,6 +1579,7 @@ int siren_mlp_backward(const siren_mlp_desc* d, const float* x, const float* dy,
   if (!x || !dy || !dweight || !dbias) return fail(SIREN_EINVAL, "null argument");
   for (int l = 0; l < d->num_layers; ++l)
     if (!dweight[l] || !dbias[l]) return fail(SIREN_EINVAL, "layer %d: null gradient output", l);
+  if (d->ff_B && dx) return fail(SIREN_EINVAL, "fourier input: no input gradient (dx must be NULL)");
   hipStream_t st = (hipStream_t)stream;
   g_err.clear();
   if (d->prec == SIREN_PREC_BF16)
@@ -1620,6 +1644,7 @@ int siren_mlp_backward_ex(const siren_mlp_desc* d, const float* x, const float* 
   if (!x || !dy || !dweight || !dbias) return fail(SIREN_EINVAL, "null argument");
   for (int l = 0; l < d->num_layers; ++l)
     if (!dweight[l] || !dbias[l]) return fail(SIREN_EINVAL, "layer %d: null gradient output", l);
+  if (d->ff_B && dx) return fail(SIREN_EINVAL, "fourier input: no input gradient (dx must be NULL)");
   hipStream_t st = (hipStream_t)stream;
   g_err.clear();
   if (d->prec == SIREN_PREC_BF16)

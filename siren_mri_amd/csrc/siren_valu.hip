@@ -67,6 +67,8 @@ struct FirstBwdArgs {
   int64_t split_stride;
   int64_t w_bstride;
   int F, C;
+  const float* ffB;    // first_bwd_wide_mfma: Fourier-feature input (x = ffin raw coordinates per row), or null
+  int ffin;
 };
 
 // 8-element row chunk loads/stores (16 B for 2-byte types, 32 B for fp32).
@@ -554,6 +556,10 @@ __global__ __launch_bounds__(256) void first_bwd_wide_mfma_kernel(FirstBwdArgs a
   const int C = a.C;
   const bf16* dz = (const bf16*)a.dZ + batch * rows * 256;
   const float* xb = a.x + batch * rows * C;
+  const float* xraw = a.x + batch * rows * (a.ffB ? a.ffin : 0);
+  __shared__ float sB[32];  // Fourier-feature input: B [ffin][C / 2]
+  if (a.ffB && tid < 32) sB[tid] = tid < a.ffin * (C / 2) ? a.ffB[tid] : 0.f;
+  __syncthreads();
   f32x16 acc[2], acd[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -580,8 +586,17 @@ __global__ __launch_bounds__(256) void first_bwd_wide_mfma_kernel(FirstBwdArgs a
     if (tid < 128) {
       const int r = tid >> 2, c0 = 4 * (tid & 3);
       const int64_t row = r0 + r;
+      if (a.ffB) {
+        // features c0 .. c0 + 3 of the row from its raw coordinates (the forward's ff_feature)
+        float xr[4] = {0.f, 0.f, 0.f, 0.f};
+        if (row < r_end)
+          for (int c = 0; c < a.ffin; ++c) xr[c] = xraw[row * a.ffin + c];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) xv[e] = (row < r_end && c0 + e < C) ? xb[row * C + c0 + e] : 0.f;
+        for (int e = 0; e < 4; ++e) xv[e] = row < r_end ? ff_feature(xr, sB, a.ffin, C / 2, c0 + e) : 0.f;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xv[e] = (row < r_end && c0 + e < C) ? xb[row * C + c0 + e] : 0.f;
+      }
     }
   };
   auto stage = [&]() {

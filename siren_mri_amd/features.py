@@ -8,6 +8,8 @@ reference's file format (a bare tensor saved with torch.save).
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -54,6 +56,20 @@ torch.library.register_fake("siren_mri_amd::fourier_features",
                             lambda x, B: x.new_empty(x.shape[:-1] + (2 * B.shape[1],)), lib=_LIB)
 
 
+# GaussianFourierFeatureTransform.model_input: hand raw coordinates + B to models that form the
+# features in their first layer (False: always materialise them, the reference's data flow)
+FUSED_INPUT = os.environ.get("SIREN_MRI_AMD_FUSED_FOURIER", "1") != "0"
+
+
+def fourier_features(x, B):
+    """cat(sin(2 pi x B), cos(2 pi x B)) (features.py:21-41) for a given B."""
+    B = B.to(x.device, x.dtype)
+    if x.is_cuda and x.dtype == torch.float32:
+        return torch.ops.siren_mri_amd.fourier_features(x, B)
+    z = 2 * np.pi * (x @ B)
+    return torch.cat([torch.sin(z), torch.cos(z)], dim=-1)
+
+
 class GaussianFourierFeatureTransform(torch.nn.Module):
     def __init__(self, num_input_channels, mapping_size_spatial=256, scale=10, loaded_B=None, device=None):
         super().__init__()
@@ -70,6 +86,22 @@ class GaussianFourierFeatureTransform(torch.nn.Module):
         z = x @ self._B_spatial.to(x.device, x.dtype)
         z = 2 * np.pi * z
         return torch.cat([torch.sin(z), torch.cos(z)], dim=-1)
+
+    def model_input(self, model, model_input):
+        """Apply the transform to model_input["coords"] for `model` (training.py:61-64). A model that
+        takes the Fourier-feature input in its SIREN's first layer (attribute fourier_input, e.g.
+        the conv hypernetwork; the kernel forms the features) gets the raw
+        coordinates and model_input["fourier_B"] when fusion is on and the coordinates need no
+        gradient; every other model gets the materialised features, as in the reference."""
+        from . import fusion
+        x = model_input["coords"]
+        inner = getattr(model, "module", model)  # (a DistributedDataParallel wrapper)
+        if (FUSED_INPUT and getattr(inner, "fourier_input", False) and fusion.enabled() and x.is_cuda
+                and x.dtype == torch.float32 and not x.requires_grad):
+            model_input["fourier_B"] = self._B_spatial.to(x.device, x.dtype)
+        else:
+            model_input["coords"] = self(x)
+        return model_input
 
     def save_B(self, filename):
         torch.save(self._B_spatial.detach().cpu(), filename)

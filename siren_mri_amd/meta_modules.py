@@ -74,6 +74,10 @@ class ConvolutionalNeuralProcessImplicit2DHypernetFourierFeatures(nn.Module):
     precision: the SIREN stack's arithmetic (native kernels); encoder_precision: the conv
     encoder's ('fp32' = reference, 'bf16' = MIOpen bf16 channels-last, see ConvImgEncoder)."""
 
+    # takes model_input["fourier_B"] with raw coordinates (features.py model_input): the hypo net's
+    # first layer forms the Fourier features (SURVEY.md §8(f) row 1)
+    fourier_input = True
+
     def __init__(self, in_features, out_features, image_resolution=None, partial_conv=False,
                  fourier_features_size=512, latent_dim=256, hidden_features=256, num_hidden_layers=5,
                  hyper_hidden_features=512, hyper_hidden_layers=1, conv_kernel_size=3,

@@ -206,13 +206,18 @@ class FCBlock(MetaModule):
             bs = [params[f"{i}.0.bias"] for i in range(self.num_linear)]
         return ws, bs
 
-    def forward(self, coords, params=None, **kwargs):
+    def forward(self, coords, params=None, ff_B=None, **kwargs):
+        """ff_B: coords are raw coordinates whose Gaussian Fourier features (features.py:21-41) are
+        the block's input (ops.siren_mlp forms them in the first layer where it can)."""
         sub = get_subdict(params, "net") if params is not None else None
         if self.nonlinearity == "sine":
             ws, bs = self.layer_params(sub)
             return siren_mlp(coords, ws, bs, w0=self.w0,
                              precision=self.precision or get_default_precision(),
-                             outermost_linear=self.outermost_linear)
+                             outermost_linear=self.outermost_linear, ff_B=ff_B)
+        if ff_B is not None:
+            from .features import fourier_features
+            coords = fourier_features(coords, ff_B)
         return self.net(coords, params=sub)
 
     def forward_with_activations(self, coords, params=None, retain_grad=False):
@@ -288,6 +293,16 @@ class SingleBVPNet(MetaModule):
     def forward(self, model_input, params=None):
         # grad leaf for derivatives w.r.t. coordinates (modules.py:151). The reference clones first;
         # a detached alias is the same leaf without a copy (nothing writes coordinates in place).
+        ff_B = model_input.get("fourier_B")
+        if ff_B is not None and not self.image_downsampling.downsample:
+            # raw coordinates + B (features.py GaussianFourierFeatureTransform.model_input): the
+            # SIREN's first layer forms the features; model_in is then the raw coordinates, and
+            # derivatives w.r.t. the features need the materialised path (fusion off)
+            coords = model_input["coords"]
+            return {"model_in": coords, "model_out": self.net(coords, get_subdict(params, "net"), ff_B=ff_B)}
+        if ff_B is not None:
+            from .features import fourier_features
+            model_input = dict(model_input, coords=fourier_features(model_input["coords"], ff_B))
         coords_org = model_input["coords"].detach().requires_grad_(True)
         coords = coords_org
         if self.image_downsampling.downsample:

@@ -61,7 +61,9 @@ class _Geometry:
     batched weights ([B, out, in]) need x of shape [B, N, in]."""
     __slots__ = ("dims", "batch", "rows", "batched", "lead_shape", "squeeze_w")
 
-    def __init__(self, x: torch.Tensor, weights: Sequence[torch.Tensor]):
+    def __init__(self, x: torch.Tensor, weights: Sequence[torch.Tensor], in_features: int | None = None):
+        # in_features: layer 0's inputs when x holds something else per row (the raw coordinates
+        # of a Fourier-feature input, siren_mlp_desc.ff_B)
         w_first = weights[0]
         if w_first.dim() not in (2, 3):
             raise RuntimeError(f"siren_mri_amd: weight of shape {tuple(w_first.shape)} unsupported")
@@ -77,7 +79,7 @@ class _Geometry:
             B, N = x.shape[0], x.shape[1]
         else:
             B, N = 1, x.numel() // max(1, x.shape[-1])
-        dims = [int(x.shape[-1])] + [int(w.shape[-2]) for w in weights]
+        dims = [int(in_features or x.shape[-1])] + [int(w.shape[-2]) for w in weights]
         for l, w in enumerate(weights):
             if int(w.shape[-1]) != dims[l]:
                 raise RuntimeError(f"siren_mri_amd: layer {l} weight {tuple(w.shape)} does not "
@@ -107,17 +109,18 @@ def _flat_params(weights, biases, geo: _Geometry):
 _SIZES = {}
 
 
-def _sizes(geo: _Geometry, prec: int, outermost_linear: bool):
+def _sizes(geo: _Geometry, prec: int, outermost_linear: bool, ff_in: int = 0):
     """(saved, workspace) bytes of a geometry after siren_mlp_check. They depend only on the
     geometry and options (not on the pointers), so they are asked once per geometry, with a
     pointer-free descriptor (also what the fake kernels use)."""
-    key = (tuple(geo.dims), geo.batch, geo.rows, geo.batched, prec, outermost_linear,
+    key = (tuple(geo.dims), geo.batch, geo.rows, geo.batched, prec, outermost_linear, ff_in,
            _native.options_epoch())
     hit = _SIZES.get(key)
     if hit is None:
         L = _native.lib()
         desc = _native.describe_only(geo.dims, prec=prec, outermost_linear=outermost_linear,
-                                     weights_batched=geo.batched, batch=geo.batch, rows_per_batch=geo.rows)
+                                     weights_batched=geo.batched, batch=geo.batch, rows_per_batch=geo.rows,
+                                     ff_in=ff_in)
         _native.check(L.siren_mlp_check(ctypes.byref(desc)), "siren_mlp_check")
         hit = (L.siren_mlp_saved_bytes(ctypes.byref(desc)), L.siren_mlp_workspace_bytes(ctypes.byref(desc)))
         if len(_SIZES) > 256:
@@ -126,8 +129,8 @@ def _sizes(geo: _Geometry, prec: int, outermost_linear: bool):
     return hit
 
 
-def _geo_of(x, weights, batched):
-    geo = _Geometry(x, weights)
+def _geo_of(x, weights, batched, ff_B=None):
+    geo = _Geometry(x, weights, 2 * int(ff_B.shape[1]) if ff_B is not None else None)
     if geo.batched != batched:
         raise RuntimeError("siren_mri_amd: weight batching does not match the op's `batched` flag")
     return geo
@@ -141,9 +144,10 @@ _LIB = torch.library.Library("siren_mri_amd", "DEF")
 _LIB.define("sine_mlp_fwd(Tensor x, Tensor[] weights, Tensor[] biases, float w0, int prec, bool outermost_linear, "
             "bool batched, bool keep) -> (Tensor, Tensor)")
 _LIB.define("sine_mlp_bwd(Tensor dy, Tensor x, Tensor[] weights, Tensor[] biases, Tensor saved, float w0, int prec, "
-            "bool outermost_linear, bool batched, bool need_dx, Tensor? dy_scale=None) -> (Tensor, Tensor[], Tensor[])")
+            "bool outermost_linear, bool batched, bool need_dx, Tensor? dy_scale=None, Tensor? ff_B=None) "
+            "-> (Tensor, Tensor[], Tensor[])")
 _LIB.define("sine_mlp_fwd_loss(Tensor x, Tensor[] weights, Tensor[] biases, float w0, int prec, bool batched, "
-            "Tensor tgt, Tensor? k0, Tensor? mask, Tensor? hf, float noise, float weight) "
+            "Tensor tgt, Tensor? k0, Tensor? mask, Tensor? hf, float noise, float weight, Tensor? ff_B=None) "
             "-> (Tensor, Tensor, Tensor, Tensor, Tensor)")
 
 
@@ -178,20 +182,24 @@ def _sine_mlp_fwd_fake(x, weights, biases, w0, prec, outermost_linear, batched, 
 
 def sine_mlp_bwd(dy: Tensor, x: Tensor, weights: List[Tensor], biases: List[Tensor], saved: Tensor, w0: float,
                  prec: int, outermost_linear: bool, batched: bool,
-                 need_dx: bool, dy_scale: Tensor | None = None) -> Tuple[Tensor, List[Tensor], List[Tensor]]:
+                 need_dx: bool, dy_scale: Tensor | None = None,
+                 ff_B: Tensor | None = None) -> Tuple[Tensor, List[Tensor], List[Tensor]]:
     """siren_mlp_backward_ex: (dx or an empty tensor, dW per layer, db per layer); dL/dy = dy times
-    the device scalar dy_scale when given (a fused loss's upstream gradient)."""
+    the device scalar dy_scale when given (a fused loss's upstream gradient). ff_B: x holds the raw
+    coordinates of a Fourier-feature input (no input gradient)."""
     if saved.numel() == 0:
         raise RuntimeError("siren_mri_amd: sine_mlp_bwd needs the saved buffer of a forward run with keep=True")
-    geo = _geo_of(x, weights, batched)
+    if ff_B is not None and need_dx:
+        raise RuntimeError("siren_mri_amd: no input gradient through a fused Fourier-feature input")
+    geo = _geo_of(x, weights, batched, ff_B)
     ws = [w.contiguous() for w in weights]
     bs = [b.contiguous() for b in biases]
     xc = x.contiguous()
     dev = x.device
     dyc = dy.contiguous().to(torch.float32)
     desc = _native.make_desc(geo.dims, ws, bs, w0=w0, prec=prec, outermost_linear=outermost_linear,
-                             weights_batched=geo.batched, batch=geo.batch, rows_per_batch=geo.rows)
-    saved_bytes, ws_bytes = _sizes(geo, prec, outermost_linear)
+                             weights_batched=geo.batched, batch=geo.batch, rows_per_batch=geo.rows, ff_B=ff_B)
+    saved_bytes, ws_bytes = _sizes(geo, prec, outermost_linear, int(ff_B.shape[0]) if ff_B is not None else 0)
     work = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     dW = [torch.empty_like(w) for w in ws]
     db = [torch.empty_like(b) for b in bs]
@@ -210,7 +218,8 @@ def sine_mlp_bwd(dy: Tensor, x: Tensor, weights: List[Tensor], biases: List[Tens
     return dx, dW, db
 
 
-def _sine_mlp_bwd_fake(dy, x, weights, biases, saved, w0, prec, outermost_linear, batched, need_dx, dy_scale=None):
+def _sine_mlp_bwd_fake(dy, x, weights, biases, saved, w0, prec, outermost_linear, batched, need_dx, dy_scale=None,
+                       ff_B=None):
     return (torch.empty_like(x) if need_dx else x.new_empty((0,)),
             [torch.empty_like(w) for w in weights], [torch.empty_like(b) for b in biases])
 
@@ -314,13 +323,13 @@ def _loss_desc(tgt, k0, mask, hf, noise, weight, y_dc, dy, loss, lws):
 _LOSS_OK = {}
 
 
-def fused_loss_supported(geo: _Geometry, prec: int, has_dc: bool, hf_len: int) -> bool:
+def fused_loss_supported(geo: _Geometry, prec: int, has_dc: bool, hf_len: int, ff_in: int = 0) -> bool:
     """siren_mlp_loss_check for a geometry (cached; pointer-free descriptors)."""
-    key = (tuple(geo.dims), geo.batch, geo.rows, geo.batched, prec, has_dc, hf_len, _native.options_epoch())
+    key = (tuple(geo.dims), geo.batch, geo.rows, geo.batched, prec, has_dc, hf_len, ff_in, _native.options_epoch())
     hit = _LOSS_OK.get(key)
     if hit is None:
         d = _native.describe_only(geo.dims, prec=prec, weights_batched=geo.batched, batch=geo.batch,
-                                  rows_per_batch=geo.rows)
+                                  rows_per_batch=geo.rows, ff_in=ff_in)
         ld = _native.SirenLossDesc()
         ld.target = ld.dy = ld.loss = ld.loss_workspace = 256
         if has_dc:
@@ -337,18 +346,20 @@ def fused_loss_supported(geo: _Geometry, prec: int, has_dc: bool, hf_len: int) -
 
 def sine_mlp_fwd_loss(x: Tensor, weights: List[Tensor], biases: List[Tensor], w0: float, prec: int, batched: bool,
                       tgt: Tensor, k0: Tensor | None, mask: Tensor | None, hf: Tensor | None, noise: float,
-                      weight: float):
+                      weight: float, ff_B: Tensor | None = None):
     """siren_mlp_forward_loss: (y, DC(y) or an empty tensor, loss, dL/dy for a unit upstream
-    gradient, saved)."""
+    gradient, saved). ff_B: x holds raw coordinates, layer 0's inputs are their Fourier features
+    cat(sin(2 pi x B), cos(2 pi x B)) formed in the kernel (features.py:21-41)."""
     _require_device(x)
-    geo = _geo_of(x, weights, batched)
+    geo = _geo_of(x, weights, batched, ff_B)
+    ff_in = int(ff_B.shape[0]) if ff_B is not None else 0
     ws = [w.contiguous() for w in weights]
     bs = [b.contiguous() for b in biases]
     xc = x.contiguous()
     dev = x.device
     desc = _native.make_desc(geo.dims, ws, bs, w0=w0, prec=prec, outermost_linear=True,
-                             weights_batched=geo.batched, batch=geo.batch, rows_per_batch=geo.rows)
-    saved_bytes, ws_bytes = _sizes(geo, prec, True)
+                             weights_batched=geo.batched, batch=geo.batch, rows_per_batch=geo.rows, ff_B=ff_B)
+    saved_bytes, ws_bytes = _sizes(geo, prec, True, ff_in)
     saved = torch.empty(saved_bytes, dtype=torch.uint8, device=dev)
     work = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     shape = geo.lead_shape + (geo.dims[-1],)
@@ -368,9 +379,9 @@ def sine_mlp_fwd_loss(x: Tensor, weights: List[Tensor], biases: List[Tensor], w0
     return y, y_dc, loss, dy, saved
 
 
-def _sine_mlp_fwd_loss_fake(x, weights, biases, w0, prec, batched, tgt, k0, mask, hf, noise, weight):
-    geo = _geo_of(x, weights, batched)
-    saved_bytes, _ = _sizes(geo, prec, True)
+def _sine_mlp_fwd_loss_fake(x, weights, biases, w0, prec, batched, tgt, k0, mask, hf, noise, weight, ff_B=None):
+    geo = _geo_of(x, weights, batched, ff_B)
+    saved_bytes, _ = _sizes(geo, prec, True, int(ff_B.shape[0]) if ff_B is not None else 0)
     shape = geo.lead_shape + (geo.dims[-1],)
     y = x.new_empty(shape, dtype=torch.float32)
     return (y, x.new_empty(shape if k0 is not None else (0,), dtype=torch.float32), x.new_empty((), dtype=torch.float32),
@@ -384,13 +395,14 @@ class _SineMLPLossAutograd(torch.autograd.Function):
     kernels as a device scalar (no dL/dy tensor, no extra launch)."""
 
     @staticmethod
-    def forward(ctx, meta, x, tgt, k0, mask, hf, *params):
+    def forward(ctx, meta, x, tgt, k0, mask, hf, ff_B, *params):
         w0, prec, batched, n, noise, weight = meta
         with torch._C._AutoDispatchBelowAutograd():
             y, y_dc, loss, dyu, saved = torch.ops.siren_mri_amd.sine_mlp_fwd_loss(
-                x, list(params[:n]), list(params[n:]), w0, prec, batched, tgt, k0, mask, hf, noise, weight)
+                x, list(params[:n]), list(params[n:]), w0, prec, batched, tgt, k0, mask, hf, noise, weight, ff_B)
         ctx.meta = meta
         ctx.has_dc = k0 is not None
+        ctx.ff_B = ff_B
         ctx.save_for_backward(x, saved, dyu, mask, *params)
         ctx.set_materialize_grads(False)
         return y, y_dc, loss
@@ -416,15 +428,16 @@ class _SineMLPLossAutograd(torch.autograd.Function):
             if gloss is not None:
                 dy = dy + dyu * gloss
         else:
-            return (None,) * (6 + 2 * n)
+            return (None,) * (7 + 2 * n)
         need_dx = ctx.needs_input_grad[1]
         dx, dW, db = torch.ops.siren_mri_amd.sine_mlp_bwd(dy, x, ws, bs, saved, w0, prec, True, batched, need_dx,
-                                                          scale)
-        return (None, dx if need_dx else None, None, None, None, None, *dW, *db)
+                                                          scale, ctx.ff_B)
+        return (None, dx if need_dx else None, None, None, None, None, None, *dW, *db)
 
 
-def _fused_loss_forward(st, x, ws, bs, w0, prec, geo):
-    """The staged image loss (fusion.py) on this SIREN forward, or None when it does not apply."""
+def _fused_loss_forward(st, x, ws, bs, w0, prec, geo, ff_B=None):
+    """The staged image loss (fusion.py) on this SIREN forward, or None when it does not apply.
+    ff_B: x holds raw coordinates of a Fourier-feature input (formed in the kernel)."""
     from . import loss_functions
     O = geo.dims[-1]
     shape = geo.lead_shape + (O,)
@@ -442,10 +455,11 @@ def _fused_loss_forward(st, x, ws, bs, w0, prec, geo):
                 and k0.shape[0] == geo.batch and k0.shape[1] == O and k0[0, 0].numel() == geo.rows
                 and not k0.requires_grad and not mask.requires_grad):
             k0 = mask = None
-    if not fused_loss_supported(geo, prec, k0 is not None, hf.numel() if hf is not None else 0):
+    if not fused_loss_supported(geo, prec, k0 is not None, hf.numel() if hf is not None else 0,
+                                int(ff_B.shape[0]) if ff_B is not None else 0):
         return None
     meta = (float(w0), prec, geo.batched, len(ws), float(noise), float(st.weight))
-    y, y_dc, loss = _SineMLPLossAutograd.apply(meta, x, tgt, k0, mask, hf, *ws, *bs)
+    y, y_dc, loss = _SineMLPLossAutograd.apply(meta, x, tgt, k0, mask, hf, ff_B, *ws, *bs)
     st.result = (y, y_dc if k0 is not None else None, loss, hf is not None, (k0, mask, noise) if k0 is not None else None)
     return y
 
@@ -454,16 +468,44 @@ _LIB.impl("sine_mlp_fwd_loss", sine_mlp_fwd_loss, "CUDA")
 torch.library.register_fake("siren_mri_amd::sine_mlp_fwd_loss", _sine_mlp_fwd_loss_fake, lib=_LIB)
 
 
+def _fourier_input_forward(x, weights, biases, w0, prec, outermost_linear, return_saved, ff_B):
+    """siren_mlp with a Fourier-feature input formed in the kernel, or None
+    when that path does not apply (then the caller materialises the features)."""
+    st = fusion.pending()
+    if (st is None or prec != _native.PREC_BF16 or not outermost_linear or return_saved or x.requires_grad
+            or not torch.is_grad_enabled() or not x.is_cuda or x.dtype != torch.float32
+            or not ff_B.is_cuda or ff_B.dtype != torch.float32 or ff_B.dim() != 2
+            or not 1 <= ff_B.shape[0] <= 4 or x.shape[-1] != ff_B.shape[0]
+            or 2 * ff_B.shape[1] != weights[0].shape[-1]):
+        return None
+    geo = _Geometry(x, weights, 2 * int(ff_B.shape[1]))
+    ws, bs = list(weights), list(biases)
+    if geo.squeeze_w:
+        ws, bs = [w[0] for w in ws], [b[0] for b in bs]
+    if not any(t.requires_grad for t in ws + bs):
+        return None
+    return _fused_loss_forward(st, x, ws, bs, w0, prec, geo, ff_B.contiguous())
+
+
 def siren_mlp(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[torch.Tensor], *,
               w0: float = 30.0, precision: str | None = None, outermost_linear: bool = True,
-              return_saved: bool = False):
+              return_saved: bool = False, ff_B: torch.Tensor | None = None):
     """Fused SIREN stack: y = Linear_L(sin(w0 Linear_{L-1}(... sin(w0 Linear_0(x))))).
-    return_saved=True also returns the op's saved buffer (diagnostics)."""
+    return_saved=True also returns the op's saved buffer (diagnostics). ff_B: x holds raw
+    coordinates and the stack's input is their Gaussian Fourier features (features.py:21-41):
+    formed inside the forward's first layer with a staged image loss (bf16 wide form, no input
+    gradient), else materialised by the fourier_features op first."""
     prec = _native.precision_code(precision or _DEFAULT_PRECISION)
     n = len(weights)
     if len(biases) != n:
         raise ValueError("siren_mlp: weights and biases differ in length")
     _require_device(x)
+    if ff_B is not None:
+        y = _fourier_input_forward(x, weights, biases, w0, prec, outermost_linear, return_saved, ff_B)
+        if y is not None:
+            return y
+        from . import features  # noqa: F401  (registers the fourier_features op)
+        x = torch.ops.siren_mri_amd.fourier_features(x, ff_B.to(x.device, x.dtype))
     geo = _Geometry(x, weights)
     ws, bs = list(weights), list(biases)
     if geo.squeeze_w:

@@ -137,7 +137,7 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
                 model_input = {k: v.double() for k, v in model_input.items()}
                 gt = {k: v.double() for k, v in gt.items()}
             if fourier_feat_transformer is not None:
-                model_input["coords"] = fourier_feat_transformer(model_input["coords"])
+                model_input = _fourier_input(model, model_input, fourier_feat_transformer)
 
             # image_mse's target, staged for the SIREN forward's fused loss epilogue (fusion.py:
             # one launch for forward + data consistency + loss; the losses pick its result up)
@@ -204,6 +204,15 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
 
 
 @torch.no_grad()
+def _fourier_input(model, model_input, transform):
+    """training.py:61-64: coords -> Fourier features; a GaussianFourierFeatureTransform may hand the
+    raw coordinates and B to a model that forms the features in its first layer (features.py)."""
+    if hasattr(transform, "model_input"):
+        return transform.model_input(model, model_input)
+    model_input["coords"] = transform(model_input["coords"])
+    return model_input
+
+
 def validate(model, val_dataloader, loss_fn, fourier_feat_transformer, dev):
     """training.py:111-136: mean of the 'img_loss' term over the validation loader."""
     model.eval()
@@ -212,7 +221,7 @@ def validate(model, val_dataloader, loss_fn, fourier_feat_transformer, dev):
         model_input = to_device(model_input, dev)
         gt = to_device(gt, dev)
         if fourier_feat_transformer is not None:
-            model_input["coords"] = fourier_feat_transformer(model_input["coords"])
+            model_input = _fourier_input(model, model_input, fourier_feat_transformer)
         out = model(model_input)
         vals.append(loss_fn(out, gt)["img_loss"])
     model.train()

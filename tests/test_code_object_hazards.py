@@ -72,4 +72,4 @@ def test_forward_stores_carry_their_wait_states(disassembly):
             for i, ln in enumerate(lines):
                 if ln.startswith("buffer_store"):
                     assert lines[i + 1].startswith("s_nop 1"), (m.group(1), ln, lines[i + 1])
-    assert forms == 26  # 5 input forms x 2 output classes x 2 epilogue forms + 6 fused-loss forms
+    assert forms == 32  # 6 input forms (1..4, wide, wide with the Fourier input) x 2 output classes x 2 epilogue forms + 8 fused-loss forms
