@@ -471,8 +471,10 @@ torch.library.register_fake("siren_mri_amd::sine_mlp_fwd_loss", _sine_mlp_fwd_lo
 def _fourier_input_forward(x, weights, biases, w0, prec, outermost_linear, return_saved, ff_B):
     """siren_mlp with a Fourier-feature input formed in the kernel, or None
     when that path does not apply (then the caller materialises the features)."""
+    from . import features
     st = fusion.pending()
-    if (st is None or prec != _native.PREC_BF16 or not outermost_linear or return_saved or x.requires_grad
+    if (not features.FUSED_INPUT or st is None or prec != _native.PREC_BF16 or not outermost_linear or return_saved
+            or x.requires_grad
             or not torch.is_grad_enabled() or not x.is_cuda or x.dtype != torch.float32
             or not ff_B.is_cuda or ff_B.dtype != torch.float32 or ff_B.dim() != 2
             or not 1 <= ff_B.shape[0] <= 4 or x.shape[-1] != ff_B.shape[0]
