@@ -201,10 +201,10 @@ def build_fit(cfg, args, dev, rank, world, precision, shard_of=None):
         # (siren_mri_amd/fusion.py), then model -> image_mse's reduction (sum / 128^2 over this
         # rank's coordinates: in a strong-scaling shard the partial sums over the ranks add up to
         # the whole image's loss) -> backward
-        fusion.stage_image_loss(tgt, weight=loss_functions.KSPACE_WEIGHT)
+        st = fusion.stage_image_loss(tgt, weight=loss_functions.KSPACE_WEIGHT)
         out = model(model_input)
         loss = loss_functions.weighted_sse(out["model_out"], tgt)
-        fusion.clear()
+        fusion.clear(st)
         loss.backward(one)
         if reducer is not None:
             reducer()
@@ -297,10 +297,10 @@ def build_c4(args, dev, rank, world, precision, encoder_precision="bf16"):
         # training.train's transform step: raw coordinates + B for the hypernetwork, whose SIREN forms
         # the Fourier features in its first layer (features.py model_input)
         mi = ff.model_input(model, dict(inp))
-        fusion.stage_image_loss(gt["img"])  # as training.train: the fused DC + loss epilogue
+        st = fusion.stage_image_loss(gt["img"])  # as training.train: the fused DC + loss epilogue
         out = model(mi)
         losses = loss_fn(out, gt)
-        fusion.clear()
+        fusion.clear(st)
         loss = sum(v.mean() for v in losses.values())
         if reducer is not None:
             reducer.begin()

@@ -376,23 +376,34 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
     const int64_t nv = rows - r0 < 0 ? 0 : (rows - r0 < FREG_WG_ROWS ? rows - r0 : FREG_WG_ROWS);
     if constexpr (ffin_on) {
       // the row's raw coordinates (the features are formed at layer 0 from these)
+      // Exactly fin dword loads: a 16-byte load of the tile's last row (fin = 2) would reach 8
+      // bytes past the resource, and a partly out-of-range multi-dword buffer load returns zeros
+      // for all of it — that row's coordinates became (0, 0) (round 4's fused-input loss error).
       const int fin = a.ffin;
       const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.x + (batch * rows + r0) * fin, nv * fin * 4);
-      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rr, (uint32_t)((wave * FREG_WROWS + j) * fin) * 4, 0, 0);
+      const uint32_t xo = (uint32_t)((wave * FREG_WROWS + j) * fin) * 4;
 #pragma unroll
-      for (int m = 0; m < 4; ++m) xw[m] = m < fin ? __builtin_bit_cast(float, v[m]) : 0.f;
+      for (int m = 0; m < 4; ++m)
+        xw[m] = m < fin ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, xo, 4 * m, 0)) : 0.f;
       return;
     }
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x + (batch * rows + r0) * cin, nv * cin * 4);
-    // two 16-byte loads from the lane's first input (dword-aligned; inputs past cin belong to the
-    // next row and are zeroed, rows past the end read as 0 through the resource)
+    // from the lane's first input: two 16-byte loads when a row is exactly 16 inputs (64-byte rows,
+    // no load crosses the resource's end), else eight dword loads — a 16-byte load that ends past
+    // the resource reads as zeros entirely, which would drop the tile's last row's valid inputs.
+    // Inputs past cin belong to the next row and are zeroed, rows past the end read as 0.
     const uint32_t xv = (uint32_t)((wave * FREG_WROWS + j) * cin + 8 * hh) * 4;
-    const u32x4_t v0 = __builtin_amdgcn_raw_buffer_load_b128(rx, xv, 0, 0);
-    const u32x4_t v1 = __builtin_amdgcn_raw_buffer_load_b128(rx, xv, 16, 0);
+    if (cin == 16) {
+      const u32x4_t v0 = __builtin_amdgcn_raw_buffer_load_b128(rx, xv, 0, 0);
+      const u32x4_t v1 = __builtin_amdgcn_raw_buffer_load_b128(rx, xv, 16, 0);
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      const uint32_t v = m < 4 ? v0[m] : v1[m - 4];
-      xw[m] = 8 * hh + m < cin ? __builtin_bit_cast(float, v) : 0.f;
+      for (int m = 0; m < 8; ++m) xw[m] = __builtin_bit_cast(float, m < 4 ? v0[m] : v1[m - 4]);
+    } else {
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rx, xv, 4 * m, 0);
+        xw[m] = 8 * hh + m < cin ? __builtin_bit_cast(float, v) : 0.f;
+      }
     }
   };
   // x rows of workgroup tile t (C KB; rows past the end arrive as zeros): waves 0..C-1, 1 KB each

@@ -97,7 +97,7 @@ class DataConsistencyInKspace(nn.Module):
     def forward(self, prediction, k0, mask):
         if _native_ok(prediction, k0, mask):
             noise = float(self.noise_lvl) if self.noise_lvl else 0.0
-            st = fusion.staged()
+            st = fusion.staged(prediction.device)
             if st is not None and st.result is not None and st.result[0] is prediction and st.result[1] is not None:
                 sk0, smask, snoise = st.result[4]
                 if sk0 is k0 and smask is mask and snoise == noise:

@@ -169,7 +169,7 @@ def high_freq_flat(device):
 def _staged_loss(out, tgt, hf_applied, weight):
     """The forward's fused loss (fusion.py) when `out` is its output (DC(y) with data consistency),
     `tgt` the staged target and the reduction the same; None otherwise."""
-    st = fusion.staged()
+    st = fusion.staged(out.device)
     if st is None or st.result is None:
         return None
     y, y_dc, loss, st_hf, _dc = st.result

@@ -472,7 +472,7 @@ def _fourier_input_forward(x, weights, biases, w0, prec, outermost_linear, retur
     """siren_mlp with a Fourier-feature input formed in the kernel, or None
     when that path does not apply (then the caller materialises the features)."""
     from . import features
-    st = fusion.pending()
+    st = fusion.pending(x.device)
     if (not features.FUSED_INPUT or st is None or prec != _native.PREC_BF16 or not outermost_linear or return_saved
             or x.requires_grad
             or not torch.is_grad_enabled() or not x.is_cuda or x.dtype != torch.float32
@@ -513,7 +513,7 @@ def siren_mlp(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence
     if geo.squeeze_w:
         ws, bs = [w[0] for w in ws], [b[0] for b in bs]
     keep = torch.is_grad_enabled() and (x.requires_grad or any(t.requires_grad for t in ws + bs))
-    st = fusion.pending()
+    st = fusion.pending(x.device)
     if st is not None and keep and outermost_linear and not return_saved and prec == _native.PREC_BF16:
         y = _fused_loss_forward(st, x, ws, bs, w0, prec, geo)
         if y is not None:

@@ -141,13 +141,12 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
 
             # image_mse's target, staged for the SIREN forward's fused loss epilogue (fusion.py:
             # one launch for forward + data consistency + loss; the losses pick its result up)
-            if "img" in gt:
-                fusion.stage_image_loss(gt["img"])
+            staged = fusion.stage_image_loss(gt["img"]) if "img" in gt else None
             try:
                 model_output = model(model_input)
                 losses = loss_fn(model_output, gt)
             finally:
-                fusion.clear()
+                fusion.clear(staged)
             train_loss = compute_loss(losses, loss_schedules, total_steps, writer)
             train_losses_dev.append(train_loss.detach().reshape(()))
             summary_step = not total_steps % steps_til_summary
@@ -203,18 +202,21 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
 #     with delta=True), so 'sum' and 'mean' both give sum/average over ranks of every micro-step.
 
 
-@torch.no_grad()
 def _fourier_input(model, model_input, transform):
-    """training.py:61-64: coords -> Fourier features; a GaussianFourierFeatureTransform may hand the
-    raw coordinates and B to a model that forms the features in its first layer (features.py)."""
+    """training.py:61-64: coords -> Fourier features, under the caller's grad mode (the reference
+    transforms with autograd on in training and under no_grad in validation); a
+    GaussianFourierFeatureTransform may hand the raw coordinates and B to a model that forms the
+    features in its first layer (features.py)."""
     if hasattr(transform, "model_input"):
         return transform.model_input(model, model_input)
     model_input["coords"] = transform(model_input["coords"])
     return model_input
 
 
+@torch.no_grad()
 def validate(model, val_dataloader, loss_fn, fourier_feat_transformer, dev):
-    """training.py:111-136: mean of the 'img_loss' term over the validation loader."""
+    """training.py:111-136: mean of the 'img_loss' term over the validation loader, under
+    torch.no_grad() as in the reference (training.py:114)."""
     model.eval()
     vals = []
     for model_input, gt in val_dataloader:

@@ -145,6 +145,37 @@ def test_training_loop_reproduces_reference_trajectory(tmp_path):
     assert (tmp_path / "run" / "checkpoints" / "model_final.pth").exists()
 
 
+def test_validate_runs_under_no_grad(tmp_path):
+    """training.py:114: validation runs under torch.no_grad(), while the
+    training step's Fourier transform keeps the caller's grad mode (training.py:61-64)."""
+    model = orc.OracleSiren(hidden_features=16, num_hidden_layers=1)
+    seen = []
+
+    class Probe(torch.nn.Module):
+        def forward(self, x):
+            seen.append(torch.is_grad_enabled())
+            return x
+
+    loader = [({"coords": dataio.get_mgrid(8)[None]}, {"img": torch.zeros(1, 64, 1)})]
+    loss_fn = lambda o, g: loss_functions.image_mse(None, o, g, high_freq=False)  # noqa: E731
+    ret = training.validate(model, loader, loss_fn, Probe(), torch.device("cpu"))
+    assert seen == [False] and isinstance(ret, float)
+    seen.clear()
+    training.train(model, loader, epochs=1, lr=1e-4, steps_til_summary=1, epochs_til_checkpoint=1000,
+                   model_dir=str(tmp_path / "run"), loss_fn=loss_fn, summary_fn=lambda *a, **k: None,
+                   val_dataloader=loader, fourier_feat_transformer=Probe())
+    assert seen == [True, False]  # the training step's transform, then validation's
+    out = model({"coords": dataio.get_mgrid(8)[None]})
+    vals = []
+
+    def spy(o, g):
+        r = loss_fn(o, g)
+        vals.append(r["img_loss"])
+        return r
+    training.validate(model, loader, spy, None, torch.device("cpu"))
+    assert vals and vals[0].grad_fn is None and out["model_out"].grad_fn is not None
+
+
 def test_hypernet_architecture_matches_reference_state_dict():
     d = load("hypernet.npz")
     model = meta_modules.ConvolutionalNeuralProcessImplicit2DHypernetFourierFeatures(
@@ -208,24 +239,44 @@ def test_checkpoint_compat_ddp_prefix_and_b_files(tmp_path):
 
 def test_fusion_staging_rules():
     """fusion.py: only a CUDA fp32 target without grad is staged; set_enabled(False) clears and
-    refuses; pending() is the record until the forward stores its result; clear() ends the step."""
+    refuses; pending() is the record until the forward stores its result; clear(record) ends the
+    step; records are per thread and per (device, stream) key (no process-global slot)."""
+    import threading
+
     from siren_mri_amd import fusion
     fusion.clear()
-    assert fusion.stage_image_loss(torch.zeros(1, 4, 1)) is None and fusion.staged() is None
+    cpu = torch.device("cpu")
+    assert fusion.stage_image_loss(torch.zeros(1, 4, 1)) is None and fusion.staged(cpu) is None
     # a CUDA-looking record is built by hand on CPU (the rules, not the kernel)
-    st = fusion.Staged(torch.zeros(1), True, 0.5)
-    fusion._STAGED[0] = st
-    assert fusion.pending() is st
-    fusion.stage_dc("k0", "mask", 0.25)
+    key = fusion.stream_key(cpu)
+    st = fusion.Staged(torch.zeros(1), True, 0.5, key)
+    fusion._slots()[key] = st
+    assert fusion.pending(cpu) is st
+    fusion.stage_dc("k0", "mask", 0.25, device=cpu)
     assert st.dc == ("k0", "mask", 0.25)
     st.result = ("y", None, "loss", False, None)
-    assert fusion.pending() is None and fusion.staged() is st
-    fusion.stage_dc("k1", "m1", 0.0)  # after the forward: no effect
+    assert fusion.pending(cpu) is None and fusion.staged(cpu) is st
+    fusion.stage_dc("k1", "m1", 0.0, device=cpu)  # after the forward: no effect
     assert st.dc == ("k0", "mask", 0.25)
+    # another thread sees none of this thread's records, and its own clear() leaves them alone
+    seen = []
+
+    def other():
+        seen.append(fusion.staged(cpu))
+        fusion.clear()
+    th = threading.Thread(target=other)
+    th.start()
+    th.join()
+    assert seen == [None] and fusion.staged(cpu) is st
+    fusion.clear(None)  # an unstaged step's record: nothing to clear
+    assert fusion.staged(cpu) is st
+    fusion.clear(st)
+    assert fusion.staged(cpu) is None
+    fusion._slots()[key] = st
     fusion.set_enabled(False)
     try:
-        assert fusion.staged() is None and not fusion.enabled()
+        assert fusion.staged(cpu) is None and not fusion.enabled()
     finally:
         fusion.set_enabled(True)
     fusion.clear()
-    assert fusion.staged() is None
+    assert fusion.staged(cpu) is None

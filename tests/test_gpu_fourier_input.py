@@ -54,6 +54,40 @@ def _hyper_case(seed=0, B=2, N=4096):
     return Bm.to(DEV), x.to(DEV), [w.to(DEV) for w in ws], [b.to(DEV) for b in bs], tgt.to(DEV)
 
 
+@pytest.mark.parametrize("B,N,scale", [(2, 4096, 3.0), (2, 4096, 21.0), (32, 16384, 3.0), (32, 16384, 21.0)])
+def test_fused_input_forward_rows_match_materialised(B, N, scale):
+    """y alone (no loss gradient, no backward): the forward with the features formed in layer 0's
+    prologue against the forward on the materialised features, row by row. A row that differs is
+    reported with its position in the 256-row workgroup tile, its 32-row wave tile and its lane
+    half (the round-4 fault: the tile's last row read its coordinates as (0, 0))."""
+    from siren_mri_amd import _native, features
+    import siren_mri_amd.ops  # noqa: F401
+    g = torch.Generator().manual_seed(7)
+    Bm = (torch.randn(2, 8, generator=g) * scale).to(DEV)
+    x = (torch.rand(B, N, 2, generator=g) * 2 - 1).to(DEV)
+    shapes = [(256, 16), (256, 256), (256, 256), (256, 256), (2, 256)]
+    # SIREN init ranges (modules.py:641-654): first layer U(-1/in, 1/in), then U(-sqrt(6/in)/w0, ..)
+    ws = [((torch.rand(B, o, i, generator=g) * 2 - 1) * (1 / i if k == 0 else (6 / i) ** 0.5 / 30)).to(DEV)
+          for k, (o, i) in enumerate(shapes)]
+    bs = [(torch.randn(B, o, generator=g) * 0.1).to(DEV) for o, _ in shapes]
+    tgt = torch.zeros(B, N, 2, device=DEV)
+    bf = _native.PREC_BF16
+    y1 = torch.ops.siren_mri_amd.sine_mlp_fwd_loss(x, ws, bs, 30.0, bf, True, tgt, None, None, None, 0.0, 1.0, Bm)[0]
+    feats = features.fourier_features(x, Bm)
+    y0, _ = torch.ops.siren_mri_amd.sine_mlp_fwd(feats, ws, bs, 30.0, bf, True, True, False)
+    torch.cuda.synchronize()
+    err = (y1 - y0).abs().amax(-1).reshape(-1).cpu()
+    scale_y = y0.abs().amax().item()
+    bad = torch.nonzero(err > 2e-2 * scale_y).flatten()
+    if bad.numel():
+        r = bad % N
+        report = {"rows": bad.numel(), "of": B * N, "first": bad[:8].tolist(),
+                  "row%256==255": int((r % 256 == 255).sum()), "row%32": torch.bincount(r % 32, minlength=32).tolist()}
+        pytest.fail(f"fused-input forward differs on {report}")
+    from oracle import siren_oracle as orc
+    assert orc.norm_rel(y1.cpu(), y0.cpu()) < 2e-3
+
+
 def _fit_grads(fused, monkeypatch):
     from siren_mri_amd import features, fusion, loss_functions
     monkeypatch.setattr(features, "FUSED_INPUT", True)

@@ -51,7 +51,7 @@ def test_image_mse_fused_matches_unfused(side, high_freq):
         model.zero_grad(set_to_none=True)
         fusion.stage_image_loss(tgt, high_freq=high_freq)
         out = model({"coords": coords})
-        st = fusion.staged()
+        st = fusion.staged(DEV)
         ran.append(st is not None and st.result is not None)
         loss = loss_functions.image_mse(None, out, {"img": tgt}, high_freq=high_freq)["img_loss"]
         fusion.clear()
@@ -82,7 +82,7 @@ def test_weighted_sse_fused_matches_unfused():
         fusion.stage_image_loss(tgt, weight=loss_functions.KSPACE_WEIGHT)
         out = model({"coords": coords})
         loss = loss_functions.weighted_sse(out["model_out"], tgt)
-        st = fusion.staged()
+        st = fusion.staged(DEV)
         ran.append(st is not None and st.result is not None and st.result[2] is loss)
         fusion.clear()
         loss.backward()
@@ -128,7 +128,7 @@ def test_unmatched_consumers_compute_their_own_loss():
     tgt = torch.randn(1, 64 * 64, 1, generator=torch.Generator().manual_seed(6)).to(DEV)
     fusion.stage_image_loss(tgt, high_freq=False)
     out = model({"coords": coords})
-    assert fusion.staged().result is not None
+    assert fusion.staged(DEV).result is not None
     other = tgt.clone()
     l_other = loss_functions.image_mse(None, out, {"img": other}, high_freq=False)["img_loss"]
     l_w = loss_functions.weighted_sse(out["model_out"], tgt, weight=0.5)
@@ -171,7 +171,7 @@ def test_hypernetwork_dc_loss_fused_matches_unfused(noise):
         model.zero_grad(set_to_none=True)
         fusion.stage_image_loss(gt["img"])
         out = model(mi)
-        st = fusion.staged()
+        st = fusion.staged(DEV)
         ran.append(st is not None and st.result is not None and st.result[1] is out["model_out"])
         hl = loss_functions.image_hypernetwork_loss(None, 2.78e-8, 6.4e-6, out, gt)
         fusion.clear()
@@ -233,3 +233,54 @@ def test_fused_loss_rejects_double_backward():
     fusion.clear()
     with pytest.raises(RuntimeError, match="double backward"):
         torch.autograd.grad(loss, list(model.parameters()), create_graph=True)
+
+
+def test_two_models_staged_on_two_streams_each_get_their_own_loss():
+    """Staged records are per thread and per (device, stream): two models
+    fitted in one process, each staged and run on its own stream, each get their own fused loss
+    (equal to the unfused loss of their own target); a forward on a stream nothing was staged for
+    runs unfused."""
+    from siren_mri_amd import dataio, fusion, loss_functions
+    ma, mb = _net(seed=6), _net(seed=7)
+    coords = dataio.get_mgrid(64)[None].to(DEV)
+    g = torch.Generator().manual_seed(12)
+    ta = torch.randn(1, 64 * 64, 1, generator=g).to(DEV)
+    tb = 3.0 * torch.randn(1, 64 * 64, 1, generator=g).to(DEV)
+    with torch.no_grad():
+        ref = {}
+        fusion.set_enabled(False)
+        try:
+            for name, m, t in (("a", ma, ta), ("b", mb, tb)):
+                out = m({"coords": coords})
+                ref[name] = float(loss_functions.image_mse(None, out, {"img": t}, high_freq=False)["img_loss"])
+        finally:
+            fusion.set_enabled(True)
+    sa, sb = torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(sa):
+        rec_a = fusion.stage_image_loss(ta, high_freq=False)
+    with torch.cuda.stream(sb):
+        rec_b = fusion.stage_image_loss(tb, high_freq=False)
+    assert rec_a is not rec_b and fusion.staged(DEV) is None  # nothing on the default stream
+    losses = {}
+    for name, m, t, s, rec in (("b", mb, tb, sb, rec_b), ("a", ma, ta, sa, rec_a)):
+        with torch.cuda.stream(s):
+            out = m({"coords": coords})
+            loss = loss_functions.image_mse(None, out, {"img": t}, high_freq=False)["img_loss"]
+            assert rec.result is not None and rec.result[2] is loss  # this stream's record ran fused
+            loss.backward()
+            losses[name] = float(loss)
+    fusion.clear(rec_a)
+    assert fusion.staged(DEV) is None
+    with torch.cuda.stream(sb):
+        assert fusion.staged(DEV) is rec_b
+    fusion.clear(rec_b)
+    torch.cuda.synchronize()
+    for name in ("a", "b"):
+        assert losses[name] == pytest.approx(ref[name], rel=1e-5), (name, losses, ref)
+    # staged on sa, run on the default stream: not picked up
+    with torch.cuda.stream(sa):
+        rec = fusion.stage_image_loss(ta, high_freq=False)
+    out = ma({"coords": coords})
+    assert rec.result is None
+    fusion.clear(rec)

@@ -179,3 +179,82 @@ def test_fwdreg_one_hidden_layer_several_rounds(rows):
     assert torch.equal(outs[0][0], outs[1][0])
     # the saved buffer: prepared weights, then the phase codes of sine layer 1 (P_0 is rebuilt)
     assert torch.equal(outs[0][1][-rows * 512:], outs[1][1][-rows * 512:])
+
+
+def test_metric_size_fused_loss_step_vs_oracle():
+    """The bench's M step exactly as it runs (bench.py step): the staged weighted_sse (image_mse's
+    1/128^2 weight) fused into the register forward's output epilogue — at 512^2 that is 1,024
+    row tiles over 256 persistent workgroups, 4 rounds of per-lane partial sums and the
+    workgroup ticket hand-off — then the native backward with dL/dloss as a device scalar.
+    Against the fp64 oracle: the loss, y, and every dW_l / db_l at the bf16 tolerances."""
+    from siren_mri_amd import dataio, fusion, loss_functions
+    from siren_mri_amd.ops import siren_mlp
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    dims = orc.siren_dims(2, 256, 3, 1)
+    params = orc.siren_init(dims, seed=11)
+    x = orc.get_mgrid(512).unsqueeze(0)
+    tgt = torch.from_numpy(dataio.smooth_random_image(512, seed=1)).float().reshape(1, -1, 1)
+    ps = [(W.double().requires_grad_(True), b.double().requires_grad_(True)) for W, b in params]
+    y_ref = orc.siren_forward(x.double(), ps)
+    l_ref = ((y_ref - tgt.double()) ** 2).sum() * loss_functions.KSPACE_WEIGHT
+    l_ref.backward()
+
+    ws = [W.to(DEV).requires_grad_(True) for W, _ in params]
+    bs = [b.to(DEV).requires_grad_(True) for _, b in params]
+    td = tgt.to(DEV)
+    st = fusion.stage_image_loss(td, weight=loss_functions.KSPACE_WEIGHT)
+    try:
+        y = siren_mlp(x.to(DEV), ws, bs, precision="bf16")
+        loss = loss_functions.weighted_sse(y, td)
+        assert st is not None and st.result is not None and st.result[2] is loss  # the fused node ran
+    finally:
+        fusion.clear(st)
+    loss.backward()
+    torch.cuda.synchronize()
+    errs = {"loss": abs(float(loss) - float(l_ref)) / abs(float(l_ref)),
+            "y": orc.norm_rel(y.detach().cpu(), y_ref.detach())}
+    for l, ((rW, rb), w, b) in enumerate(zip(ps, ws, bs)):
+        errs[f"dW{l}"] = orc.norm_rel(w.grad.cpu(), rW.grad)
+        errs[f"db{l}"] = orc.norm_rel(b.grad.cpu(), rb.grad)
+    print("\n[M fused loss step 512^2 bf16] " + " ".join(f"{k}={v:.2e}" for k, v in errs.items()))
+    ty, tg = TOL["bf16"]
+    assert errs["loss"] <= ty and errs["y"] <= ty, errs
+    for k, v in errs.items():
+        assert v <= tg, (k, errs)
+
+
+def test_c4_size_fused_dc_loss_forward_vs_oracle():
+    """Configs 4/5's hypo-net forward with the data consistency and the high-frequency-masked
+    k-space loss in its epilogue, at C4's size (32 slices x 128^2 rows, per-slice weights,
+    16 Fourier-feature inputs): y, DC(y) and the loss against the fp64 oracle
+    (data_consistency.py:32-48, loss_functions.py:66-101)."""
+    from siren_mri_amd import _native, loss_functions
+    import siren_mri_amd.ops  # noqa: F401
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    B, N = 32, 16384
+    g = torch.Generator().manual_seed(21)
+    dims = [16, 256, 256, 256, 256, 2]
+    ws, bs = [], []
+    for l in range(len(dims) - 1):
+        W, b = orc.siren_init(dims, seed=30 + l)[l]
+        ws.append((W.unsqueeze(0) * (1 + 0.1 * torch.randn(B, 1, 1, generator=g))).contiguous())
+        bs.append((b.unsqueeze(0) + 0.01 * torch.randn(B, dims[l + 1], generator=g)).contiguous())
+    x = torch.sin(torch.rand(B, N, 16, generator=g) * 6.28)
+    kspace = torch.randn(B, 2, 128, 128, generator=g) * 0.05
+    mask = (torch.rand(B, 2, 128, 128, generator=g) < 0.3).float()
+    k0 = mask * kspace
+    tgt = kspace.permute(0, 2, 3, 1).reshape(B, N, 2).contiguous()
+    with torch.no_grad():
+        y_ref = orc.siren_forward(x.double(), list(zip([w.double() for w in ws], [b.double() for b in bs])))
+        dc_ref = orc.data_consistency(y_ref, k0.double(), mask.double())
+        l_ref = orc.image_mse(None, {"model_out": dc_ref}, {"img": tgt.double()}, high_freq=True)["img_loss"]
+    hf = loss_functions.high_freq_flat(DEV)
+    y, y_dc, loss, _, _ = torch.ops.siren_mri_amd.sine_mlp_fwd_loss(
+        x.to(DEV), [w.to(DEV) for w in ws], [b.to(DEV) for b in bs], 30.0, _native.PREC_BF16, True, tgt.to(DEV),
+        k0.to(DEV), mask.to(DEV), hf, 0.0, loss_functions.KSPACE_WEIGHT)
+    torch.cuda.synchronize()
+    errs = {"y": orc.norm_rel(y.cpu(), y_ref), "dc": orc.norm_rel(y_dc.cpu(), dc_ref),
+            "loss": abs(float(loss) - float(l_ref)) / abs(float(l_ref))}
+    print("\n[C4 fused DC + hf loss forward, 32 x 128^2, bf16] " + " ".join(f"{k}={v:.2e}" for k, v in errs.items()))
+    for k, v in errs.items():
+        assert v <= TOL["bf16"][0], (k, errs)
