@@ -460,10 +460,21 @@ def kernel_flops(wl, kclass):
     return table[kclass]
 
 
-def traffic_from_profile(kclass, wl, side):
-    """HBM bytes per launch of the kernel from the committed PMC pass (profiles/pmc_traffic.json:
-    FETCH_SIZE + WRITE_SIZE per launch, gfx950 correction applied by tools/pmc_summary.py), or None
-    when this workload/kernel was not profiled."""
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md §HBM (spec)
+
+
+def traffic_key(wl):
+    """profiles/pmc_traffic.json key of a workload: precision, rows of ONE launch (the coordinate
+    rows this GPU processes per step), hidden width and hidden-layer count."""
+    return f"{wl.precision}:rows{wl.coords}:{wl.dims[1]}:{len(wl.dims) - 3}"
+
+
+def traffic_from_profile(kclass, wl):
+    """HBM bytes per launch of the kernel from the committed PMC passes (profiles/pmc_traffic.json:
+    FETCH_SIZE x 2 + WRITE_SIZE per launch, the gfx950 correction applied by tools/pmc_summary.py),
+    keyed by the launch's rows (traffic_key) and the kernel symbol, or None when this exact
+    workload / kernel was not profiled. Keyed by rows, not by the grid's side: a row shard of the
+    512^2 grid is a different launch."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     sym = KCLASS_SYMBOL.get(wl.precision, {}).get(kclass)
     if sym is None or not os.path.exists(path):
@@ -471,10 +482,21 @@ def traffic_from_profile(kclass, wl, side):
     try:
         with open(path) as f:
             d = json.load(f)
-        nh = len(wl.dims) - 3
-        ent = d.get(f"{wl.precision}:{side}:{wl.dims[1]}:{nh}", {}).get(sym)
+        ent = d.get(traffic_key(wl), {}).get(sym)
         return None if ent is None else round(ent["bytes"] / 1e9, 4)
     except (OSError, ValueError, KeyError):
+        return None
+
+
+def step_traffic_from_profile(wl):
+    """HBM bytes of one whole step of the workload (every kernel's bytes per launch x launches per
+    step) from the same PMC record, or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            v = json.load(f).get(traffic_key(wl), {}).get("_step_bytes")
+        return None if v is None else int(v)
+    except (OSError, ValueError):
         return None
 
 
@@ -664,8 +686,14 @@ def measure(cfg, args, dev, rank, world, with_kernels=True):
     if dom is not None and kt is not None and kt.launches:
         avg_s = kt.avg_ms * 1e-3
         flops = kernel_flops(wl, dom)
-        side = wl.extra.get("side")
-        traffic = traffic_from_profile(dom, wl, side) if side else None
+        traffic = traffic_from_profile(dom, wl)
+        traffic_note = None
+        if traffic and traffic / avg_s > HBM_PEAK_GBPS:
+            # a recorded byte count above what HBM can move in the measured launch time is not this
+            # launch's traffic (a stale or mismatched profile): refuse it rather than print it
+            traffic_note = (f"rejected: {traffic} GB per launch over {avg_s * 1e3:.4f} ms would be "
+                            f"{traffic / avg_s:.0f} GB/s, above the {HBM_PEAK_GBPS:.0f} GB/s HBM peak")
+            traffic = None
         res["roofline"] = {
             "bound": "mfma", "kernel": KCLASS_NAMES[dom], "kernel_symbol": KCLASS_SYMBOL.get(wl.precision, {}).get(dom),
             "achieved": round(flops / avg_s / 1e12, 2), "peak": round(peak / 1e12, 1), "unit": "TFLOP/s",
@@ -675,15 +703,19 @@ def measure(cfg, args, dev, rank, world, with_kernels=True):
                       "region of K eager steps" + (" (the reported value is the hipGraph region's)" if graph else ""),
             "traffic": traffic, "traffic_unit": "GB per launch (HBM, rocprofv3 PMC FETCH_SIZE + WRITE_SIZE)",
             "hbm_gbps_of_traffic": round(traffic * 1e9 / avg_s / 1e9, 1) if traffic else None,
+            "traffic_key": traffic_key(wl), **({"traffic_note": traffic_note} if traffic_note else {}),
             "kernel_ms_per_step": {KCLASS_NAMES[k].split(" ")[0] + f"[{k}]": round(v[0], 4) for k, v in totals.items()}}
-        if traffic:
+        step_bytes = step_traffic_from_profile(wl)
+        if traffic or step_bytes:
             # algorithmic I/O of the whole path: 12 B per coordinate (coords 8 B,
             # target 4 B) + parameters, gradients and Adam state once each (5 x 4 B per parameter)
             nparam = sum(wl.dims[i] * wl.dims[i + 1] + wl.dims[i + 1] for i in range(len(wl.dims) - 1))
             alg = 12 * wl.coords + 20 * nparam
             res["roofline"]["traffic_vs_algorithmic_io"] = {
                 "algorithmic_io_bytes_per_step": alg,
-                "dominant_kernel_traffic_over_step_io": round(traffic * 1e9 / alg, 1)}
+                "dominant_kernel_traffic_over_step_io": round(traffic * 1e9 / alg, 1) if traffic else None,
+                "step_traffic_bytes": step_bytes,
+                "step_traffic_over_step_io": round(step_bytes / alg, 1) if step_bytes else None}
     return res, wl, dom, totals
 
 

@@ -387,6 +387,13 @@ int siren_sincos_f32(const float* x, float* s, float* c, int64_t n, int impl, vo
  *   "pair_tail_reduce"  1 (default): a pair launch's weight-gradient workgroups also reduce the
  *                    previous pair launch's split-K slabs after their own rows (two slab buffers
  *                    alternate); 0: every pair launch is followed by a reduce_multi launch.
+ *   "jvp_adj"        1 (default): the analytic-derivative backward (siren_jvp_backward*) runs each
+ *                    hidden layer's adjoint GEMM with the adjoint combine in its epilogue (one
+ *                    launch, the same formula to an fp32 ulp); 0: the GEMM and the combine as
+ *                    two launches.
+ *   "jvp_tn2"        1 (default): fp32 analytic-derivative weight gradients of 256-wide layers on
+ *                    the all-rows tile kernel (X formed once per launch, double-buffered LDS);
+ *                    0: the 128x128-tile kernel.
  *   "debug_pair_roles"  3 (default); 1 / 2 run only the input- / weight-gradient role of
  *                    pair_ring_bf16_kernel (timing experiments only: the gradients are then wrong).
  *   "debug_fused_profile"  device address of an int64 buffer [grid][4] that receives per-

@@ -506,6 +506,178 @@ __global__ __launch_bounds__(256) void jvp_tn_kernel(JTNArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// jvp_tn_kernel for fp32 (exact-fp32 MFMA), restructured: a workgroup owns ALL M = 256 rows of
+// dW and 128 of its columns, so each X element (a sin / cos of a stored phase times a tangent) is
+// formed once per launch instead of once per 128-row tile of dW; 8 waves (wave (wm, wn): dW rows
+// 64 wm .. + 63, columns 64 wn .. + 63 of the tile); LDS double-buffered, one barrier per 32-row
+// chunk, and chunk k + 1's staging (global loads issued before chunk k's MFMAs, the X arithmetic
+// and the LDS stores spread between them) overlapping chunk k's MFMAs. Same products and the same
+// K order within a split as jvp_tn_kernel<kPrecF32>; half as many splits (a workgroup covers twice
+// the dW tile), so the split-K sums round differently (fp32 rounding level).
+constexpr int JTN2_KC = 32;
+constexpr int JTN2_BN = 128;
+constexpr int JTN2_DROW = 256 + 4;  // fp32 words per staged D row (16-byte aligned rows)
+constexpr int JTN2_XROW = 128 + 4;
+
+template <bool LAP>
+__global__ __launch_bounds__(512) void jvp_tn2_kernel(JTNArgs a) {
+  using PT = Prec<kPrecF32>;
+  constexpr int KC = JTN2_KC;
+  __shared__ __attribute__((aligned(16))) float Ds[2][KC * JTN2_DROW];
+  __shared__ __attribute__((aligned(16))) float Xs[2][KC * JTN2_XROW];
+  __shared__ float dbs[8][256];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int j0 = blockIdx.x * JTN2_BN;
+  const int split = blockIdx.y;
+  const int64_t b = blockIdx.z;
+  const int64_t rows = (int64_t)a.S * a.N;
+  const int64_t r_begin = (int64_t)split * a.rows_per_split;
+  const int64_t r_end = min(r_begin + a.rows_per_split, rows);
+  const int64_t plane = a.N * (int64_t)a.Kin;
+  const float* Dg = (const float*)a.D + b * rows * a.M;
+  const float* Pg = (const float*)a.P + b * plane;
+  const float* Ug = a.U + b * a.Su * plane;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  f32x4 dbacc = {0.f, 0.f, 0.f, 0.f};  // db of columns 4 (tid & 63) .. + 3 over this thread's stream-0 rows
+
+  // staging units: D q < 4: row (tid >> 6) + 8 q, columns 4 (tid & 63) .. + 3 (M = 256);
+  //                X q < 2: row (tid >> 5) + 16 q, columns j0 + 4 (tid & 31) .. + 3
+  f32x4 dr[4], pr[2], ur[2];
+  int xs_[2];
+  int64_t xn_[2];
+  const int dcol = 4 * (tid & 63), xcol = 4 * (tid & 31);
+  auto fetch = [&](int64_t rc) {
+    const int64_t s0 = rc / a.N, nn0 = rc - s0 * a.N;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t row = rc + (tid >> 6) + 8 * q;
+      dr[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (row < r_end && dcol < a.M) dr[q] = *(const f32x4*)(Dg + row * a.M + dcol);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int r = (tid >> 5) + 16 * q;
+      const int64_t row = rc + r;
+      pr[q] = ur[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      xs_[q] = -1;
+      if (row < r_end && j0 + xcol < a.Kin) {
+        int s = (int)s0;
+        int64_t n = nn0 + r;
+        while (n >= a.N) {
+          n -= a.N;
+          ++s;
+        }
+        xs_[q] = s;
+        xn_[q] = n;
+        pr[q] = *(const f32x4*)(Pg + n * a.Kin + j0 + xcol);
+        // (a Laplacian-stream row reads its C + 1 planes when it is staged)
+        if (s >= 1 && s <= a.C) ur[q] = *(const f32x4*)(Ug + (int64_t)(s - 1) * plane + n * a.Kin + j0 + xcol);
+      }
+    }
+  };
+  auto stage_d = [&](int buf, int q, int64_t rc) {
+    const int r = (tid >> 6) + 8 * q;
+    *(f32x4*)(&Ds[buf][r * JTN2_DROW + dcol]) = dr[q];
+    const int64_t row = rc + r;
+    if (row < r_end && row < a.N) dbacc += dr[q];  // stream-0 rows are the first N stacked rows
+  };
+  auto stage_x = [&](int buf, int q) {
+    const int r = (tid >> 5) + 16 * q;
+    const int s = xs_[q];
+    f32x4 xv = {0.f, 0.f, 0.f, 0.f};
+    if (s == 0) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) xv[e] = PT::sinp(pr[q][e]);
+    } else if (s >= 1 && (!LAP || s <= a.C)) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) xv[e] = a.w0 * PT::cosp(pr[q][e]) * ur[q][e];
+    } else if constexpr (LAP) {
+      if (s == a.C + 1) {
+        const int64_t n = xn_[q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float* Ue = Ug + n * a.Kin + j0 + xcol + e;
+          float qq = 0.f;
+          for (int j = 0; j < a.C; ++j) qq = fmaf(Ue[j * plane], Ue[j * plane], qq);
+          const float p = pr[q][e];
+          xv[e] = a.w0 * PT::cosp(p) * Ue[a.C * plane] - a.w0 * a.w0 * PT::sinp(p) * qq;
+        }
+      }
+    }
+    *(f32x4*)(&Xs[buf][r * JTN2_XROW + xcol]) = xv;
+  };
+
+  const int r32 = lane & 31, h = lane >> 5;
+  int buf = 0;
+  fetch(r_begin);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) stage_d(0, q, r_begin);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) stage_x(0, q);
+  __syncthreads();
+  for (int64_t rc = r_begin; rc < r_end; rc += KC) {
+    const bool more = rc + KC < r_end;
+    if (more) fetch(rc + KC);
+    const float* D_ = Ds[buf];
+    const float* X_ = Xs[buf];
+    static_for<0, KC / 2>([&](auto ks_c) {
+      constexpr int ks = decltype(ks_c)::value;
+      float af[2], bfr[2];
+#pragma unroll
+      for (int bm = 0; bm < 2; ++bm) af[bm] = D_[(2 * ks + h) * JTN2_DROW + 64 * wm + 32 * bm + r32];
+#pragma unroll
+      for (int bn = 0; bn < 2; ++bn) bfr[bn] = X_[(2 * ks + h) * JTN2_XROW + 64 * wn + 32 * bn + r32];
+#pragma unroll
+      for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn)
+          acc[bm][bn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[bm], bfr[bn], acc[bm][bn], 0, 0, 0);
+      // the next chunk's staging, spread over the K steps (the other buffer: its last reads were
+      // the previous chunk's MFMAs, before the barrier that ended it)
+      if (more) {
+        if constexpr (ks == 3 || ks == 5 || ks == 7 || ks == 9) stage_d(buf ^ 1, (ks - 3) / 2, rc + KC);
+        if constexpr (ks == 11 || ks == 13) stage_x(buf ^ 1, (ks - 11) / 2);
+      }
+    });
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  float* part = a.part + (int64_t)split * a.split_stride + b * ((int64_t)a.M * a.Kin + a.M);
+#pragma unroll
+  for (int bn = 0; bn < 2; ++bn) {
+    const int col = j0 + 64 * wn + 32 * bn + r32;
+    if (col >= a.Kin) continue;
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = 64 * wm + 32 * bm + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (row < a.M) part[(int64_t)row * a.Kin + col] = acc[bm][bn][e];
+      }
+  }
+  if (j0 == 0) {
+    // db: the 8 waves' column sums (wave w summed rows w + 8 q), added in wave order
+    *(f32x4*)(&dbs[wave][dcol]) = dbacc;
+    __syncthreads();
+    if (tid < a.M) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) s += dbs[w][tid];
+      part[(int64_t)a.M * a.Kin + tid] = s;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // First layer: P0 = enc(w0 (x W0^T + b0)), U0[k] = W0[:, k] broadcast over rows, V0 = 0.
 struct JFirstArgs {
   const float* x;     // [B][N][C]
@@ -758,6 +930,212 @@ __global__ __launch_bounds__(256) void jvp_combine_kernel(JCombArgs a) {
       float* part = a.part + (int64_t)blockIdx.x * a.split_stride + b * (int64_t)(a.O * a.F + a.O);
       for (int o = 0; o < a.O; ++o) part[o * a.F + f] = dwl;
       if (f < a.O) part[a.O * a.F + f] = 0.f;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// The adjoint GEMM of a hidden layer WITH the combine in its epilogue (replaces jvp_nt_kernel
+// <JMODE_BWD> + jvp_combine_kernel<top = 0>): raw[s] = D[s] W_l for all S adjoint streams of the
+// same 64 rows in one workgroup, so a lane holds h_bar, t_bar^1..C (and S_bar) of the same
+// (row, feature) in its accumulators and forms the layer below's adjoints [a_bar; u_bar^k; V_bar]
+// in registers (the formulas of jvp_combine_kernel on the same fp32 accumulator values; the
+// compiler's FMA contraction may differ by an ulp). The fp32 raw tensor never goes to HBM: per layer
+// 2 x S x 4 B per (row, feature) less traffic and one launch less.
+//
+// Tile: 64 rows x S streams (A) x 256 output features (B, all of them: each D row is read once),
+// 8 waves: wave (wm, wn) owns rows 32 wm .. 32 wm + 31 of EVERY stream and features 64 wn .. + 63.
+// K chunks of 32, operands staged through LDS (fp32 rows padded to 33 words / bf16 to 40), the next
+// chunk's raw values in registers during this chunk's MFMAs.
+struct JAdjArgs {
+  const void* D;      // [B][S][N][K] grad_t: adjoints of layer l (K = its width)
+  const void* W;      // [nb_w][Nout][K] op_t: W_l^T (prepared for the adjoint)
+  const void* P;      // [B][N][Nout] phase_t of layer l - 1
+  const float* U;     // [B][Su][N][Nout] tangents of layer l - 1
+  void* Dout;         // [B][S][N][Nout] grad_t: adjoints of layer l - 1
+  int64_t N;
+  int Su;
+  int64_t w_bstride;
+  int K, Nout;
+  float w0;
+};
+
+constexpr int JADJ_ROWS = 64;
+constexpr int JADJ_BN = 256;
+
+template <int PREC, int S, bool LAP>
+__global__ __launch_bounds__(512) void jvp_adj_kernel(JAdjArgs a) {
+  using PT = Prec<PREC>;
+  using phase_t = typename PT::phase_t;
+  using grad_t = typename PT::grad_t;
+  using op_t = typename PT::op_t;
+  constexpr bool BF = PREC == kPrecBF16;
+  constexpr int C = LAP ? S - 2 : S - 1;
+  static_assert(C >= 1, "at least one tangent stream");
+  constexpr int ROW = JNTLds<PREC>::ROW;
+  constexpr int AROWS = S * JADJ_ROWS;
+  __shared__ __attribute__((aligned(16))) op_t As[AROWS * ROW];
+  __shared__ __attribute__((aligned(16))) op_t Bs[JADJ_BN * ROW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int64_t b = blockIdx.y;
+  const int64_t N = a.N;
+  const int64_t n0 = (int64_t)blockIdx.x * JADJ_ROWS;
+  const int K = a.K;
+  const op_t* W = (const op_t*)a.W + b * a.w_bstride;
+  const grad_t* Dg = (const grad_t*)a.D + b * (int64_t)S * N * K;
+
+  f32x16 acc[S][2];
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[s][j][e] = 0.f;
+
+  // A chunk: S x 64 rows x 32 k in units of 4 -> S * 512 / 512 = S units per thread (unit u: row
+  // u >> 3 = stream (u >> 9) and row (u >> 3) & 63, k 4 (u & 7)); B chunk: 256 x 32 -> 4 units.
+  constexpr int AU = S;
+  float areg[AU][4];
+  float breg[4][4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < AU; ++q) {
+      const int u = tid + 512 * q;
+      const int s = u >> 9, r = (u >> 3) & 63, k = k0 + (u & 7) * 4;
+      const int64_t n = n0 + r;
+      if (n < N) {
+        const grad_t* src = Dg + ((int64_t)s * N + n) * K + k;
+        if constexpr (BF) {
+          const bf16x4 v = *(const bf16x4*)src;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) areg[q][e] = (float)v[e];
+        } else {
+          const f32x4 v = *(const f32x4*)src;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) areg[q][e] = v[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) areg[q][e] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int u = tid + 512 * q;
+      const int c = u >> 3, k = k0 + (u & 7) * 4;
+      if (c < a.Nout) {
+        if constexpr (BF) {
+          const bf16x4 v = *(const bf16x4*)(W + (int64_t)c * K + k);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) breg[q][e] = (float)v[e];
+        } else {
+          const f32x4 v = *(const f32x4*)((const float*)W + (int64_t)c * K + k);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) breg[q][e] = v[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) breg[q][e] = 0.f;
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int q = 0; q < AU; ++q) {
+      const int u = tid + 512 * q;
+      const int r = u >> 3, kq = (u & 7) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) As[r * ROW + kq + e] = from_f32<op_t>(areg[q][e]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int u = tid + 512 * q;
+      const int c = u >> 3, kq = (u & 7) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Bs[c * ROW + kq + e] = from_f32<op_t>(breg[q][e]);
+    }
+  };
+
+  const int r32 = lane & 31, h = lane >> 5;
+  const int nk = K / JNT_KC;
+  load(0);
+  for (int kc = 0; kc < nk; ++kc) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (kc + 1 < nk) load((kc + 1) * JNT_KC);
+    if constexpr (BF) {
+#pragma unroll
+      for (int ks = 0; ks < JNT_KC / 16; ++ks) {
+        bf16x8 af[S], bfr[2];
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) af[s][e] = As[(s * JADJ_ROWS + 32 * wm + r32) * ROW + ks * 16 + h * 8 + e];
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bfr[bn][e] = Bs[(64 * wn + 32 * bn + r32) * ROW + ks * 16 + h * 8 + e];
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+          for (int bn = 0; bn < 2; ++bn)
+            acc[s][bn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bfr[bn], acc[s][bn], 0, 0, 0);
+      }
+    } else {
+#pragma unroll 4
+      for (int ks = 0; ks < JNT_KC / 2; ++ks) {
+        float af[S], bfr[2];
+#pragma unroll
+        for (int s = 0; s < S; ++s) af[s] = As[(s * JADJ_ROWS + 32 * wm + r32) * ROW + 2 * ks + h];
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn) bfr[bn] = Bs[(64 * wn + 32 * bn + r32) * ROW + 2 * ks + h];
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+          for (int bn = 0; bn < 2; ++bn)
+            acc[s][bn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bfr[bn], acc[s][bn], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- the combine (jvp_combine_kernel, top = 0) on the accumulators ----
+  const int F = a.Nout;
+  const int64_t plane = N * (int64_t)F;
+  const float w0 = a.w0, w02 = a.w0 * a.w0;
+  grad_t* Do = (grad_t*)a.Dout + b * (int64_t)S * plane;
+  const phase_t* Pb = (const phase_t*)a.P + b * plane;
+  const float* Ub = a.U + b * (int64_t)a.Su * plane;
+#pragma unroll
+  for (int bn = 0; bn < 2; ++bn) {
+    const int f = 64 * wn + 32 * bn + r32;
+    if (f >= F) continue;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int64_t n = n0 + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (n >= N) continue;
+      const int64_t idx = n * F + f;
+      const phase_t p = Pb[idx];
+      const float c = PT::cosp(p), sn = PT::sinp(p);
+      const float hbar = acc[0][bn][e];
+      const float sbar = LAP ? acc[1 + C][bn][e] : 0.f;
+      float cross = 0.f, q = 0.f;
+#pragma unroll
+      for (int k = 0; k < C; ++k) {
+        const float u = Ub[(int64_t)k * plane + idx];
+        const float tbar = acc[1 + k][bn][e];
+        cross = fmaf(tbar, u, cross);
+        q = fmaf(u, u, q);
+        Do[(int64_t)(1 + k) * plane + idx] = from_f32<grad_t>(w0 * c * tbar - 2.f * w02 * sn * sbar * u);
+      }
+      float abar = c * hbar - w0 * sn * cross;
+      if constexpr (LAP) {
+        const float v = Ub[(int64_t)C * plane + idx];
+        abar -= w0 * sbar * (sn * v + w0 * c * q);
+        Do[(int64_t)(1 + C) * plane + idx] = from_f32<grad_t>(w0 * c * sbar);
+      }
+      Do[idx] = from_f32<grad_t>(w0 * abar);
     }
   }
 }

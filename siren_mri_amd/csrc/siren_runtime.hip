@@ -98,6 +98,8 @@ bool g_pair_ring = true;   // both gradients of a ring layer in one launch (pair
 int g_pair_roles = 3;      // debug timing: which pair_ring roles run (results are wrong unless 3)
 bool g_dx_stagger = false;  // middle/top input-gradient ring: staggered wave halves (measured slower: +5-9 us/step)
 bool g_tail_reduce = true;  // a pair launch reduces the previous pair launch's slabs (no reduce launch)
+bool g_jvp_adj = true;
+bool g_jvp_tn2 = true;      // fp32 analytic-derivative weight gradients on jvp_tn2_kernel      // analytic-derivative backward: adjoint GEMM + combine in one launch (jvp_adj_kernel)
 // pair_ring role split, input-gradient workgroups per 32 of the grid, per pair kind (middle, top,
 // bottom); 16 = the paired mapping (npair + npair, same tiles on one XCD)
 int g_pair_split[3] = {16, 16, 16};
@@ -1351,6 +1353,23 @@ int jvp_forward_impl(const siren_mlp_desc* d, int order, const float* x, float* 
   return SIREN_OK;
 }
 
+// jvp_tn2_kernel (fp32 weight gradient of a hidden layer): dW of 256 rows (the layer's width M), input
+// width a multiple of 4; option jvp_tn2 (default on)
+bool jvp_tn2_ok(int M, int N) { return g_jvp_tn2 && M == 256 && N % 4 == 0; }
+Split jtn2_split(const Geo& g, int64_t stacked_rows, int N) {
+  const int64_t want = std::max<int64_t>(1, 256 / (cdiv(N, JTN2_BN) * g.nb));
+  Split s;
+  s.rows_per_split = std::max<int64_t>(JTN2_KC, align_up(cdiv(stacked_rows, want), JTN2_KC));
+  s.nsplit = std::max<int64_t>(1, cdiv(stacked_rows, s.rows_per_split));
+  return s;
+}
+
+// jvp_adj_kernel's shapes: 2..4 adjoint streams (gradient with C <= 3, Laplacian with C <= 2) and a
+// layer below of at most 256 features (one column tile)
+bool jvp_adj_fused(int S, int lap, int Nout) {
+  return g_jvp_adj && S >= 2 && S <= 4 && !(lap && S < 3) && Nout <= JADJ_BN;
+}
+
 template <int PREC>
 int jvp_backward_impl(const siren_mlp_desc* d, int order, const float* x, const float* dout,
                       const char* saved, char* ws, float* const* dW, float* const* db, float* dx, hipStream_t st,
@@ -1414,13 +1433,52 @@ int jvp_backward_impl(const siren_mlp_desc* d, int order, const float* x, const 
       a.M = M;
       a.Kin = N;
       a.w0 = d->w0;
-      dim3 grid((unsigned)(cdiv(M, 128) * cdiv(N, 128)), (unsigned)s.nsplit, (unsigned)g.nb);
-      if (lapmode) hipLaunchKernelGGL((jvp_tn_kernel<PREC, true>), grid, dim3(256), 0, st, a);
-      else hipLaunchKernelGGL((jvp_tn_kernel<PREC>), grid, dim3(256), 0, st, a);
-      if ((rc = check_launch("jvp_tn"))) return rc;
-      if ((rc = launch_reduce(part, s.nsplit, a.split_stride, g.nb, (int64_t)M * N + M, (int64_t)M * N,
-                              dW[l], db[l], st)))
-        return rc;
+      if (PREC == kPrecF32 && jvp_tn2_ok(M, N)) {
+        // fp32: all 256 dW rows per workgroup (jvp_tn2_kernel), with its own, smaller split count
+        const Split s2 = jtn2_split(g, (int64_t)jl.Sb * g.rows, N);
+        a.rows_per_split = s2.rows_per_split;
+        dim3 grid2((unsigned)cdiv(N, JTN2_BN), (unsigned)s2.nsplit, (unsigned)g.nb);
+        if (lapmode) hipLaunchKernelGGL((jvp_tn2_kernel<true>), grid2, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((jvp_tn2_kernel<false>), grid2, dim3(512), 0, st, a);
+        if ((rc = check_launch("jvp_tn2"))) return rc;
+        if ((rc = launch_reduce(part, s2.nsplit, a.split_stride, g.nb, (int64_t)M * N + M, (int64_t)M * N,
+                                dW[l], db[l], st)))
+          return rc;
+      } else {
+        dim3 grid((unsigned)(cdiv(M, 128) * cdiv(N, 128)), (unsigned)s.nsplit, (unsigned)g.nb);
+        if (lapmode) hipLaunchKernelGGL((jvp_tn_kernel<PREC, true>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((jvp_tn_kernel<PREC>), grid, dim3(256), 0, st, a);
+        if ((rc = check_launch("jvp_tn"))) return rc;
+        if ((rc = launch_reduce(part, s.nsplit, a.split_stride, g.nb, (int64_t)M * N + M, (int64_t)M * N,
+                                dW[l], db[l], st)))
+          return rc;
+      }
+    }
+    if (jvp_adj_fused(jl.Sb, lapmode, N)) {
+      // adjoint GEMM + combine in one launch (jvp_adj_kernel)
+      JAdjArgs a;
+      a.D = ws + jl.d_off[cur];
+      a.W = saved + jl.base.wt_op_off[l];
+      a.P = pptr(l - 1);
+      a.U = (const float*)(saved + jl.u_off[l - 1]);
+      a.Dout = ws + jl.d_off[cur ^ 1];
+      a.N = g.rows;
+      a.Su = jl.Su;
+      a.w_bstride = d->weights_batched ? (int64_t)M * N : 0;
+      a.K = M;
+      a.Nout = N;
+      a.w0 = d->w0;
+      const dim3 grid((unsigned)cdiv(g.rows, JADJ_ROWS), (unsigned)g.nb);
+      switch (jl.Sb * 2 + lapmode) {
+        case 4: hipLaunchKernelGGL((jvp_adj_kernel<PREC, 2, false>), grid, dim3(512), 0, st, a); break;
+        case 6: hipLaunchKernelGGL((jvp_adj_kernel<PREC, 3, false>), grid, dim3(512), 0, st, a); break;
+        case 7: hipLaunchKernelGGL((jvp_adj_kernel<PREC, 3, true>), grid, dim3(512), 0, st, a); break;
+        case 8: hipLaunchKernelGGL((jvp_adj_kernel<PREC, 4, false>), grid, dim3(512), 0, st, a); break;
+        default: hipLaunchKernelGGL((jvp_adj_kernel<PREC, 4, true>), grid, dim3(512), 0, st, a); break;
+      }
+      if ((rc = check_launch("jvp_adj"))) return rc;
+      cur ^= 1;
+      continue;
     }
     {
       JNTArgs a;
@@ -2188,6 +2246,14 @@ int siren_config_set(const char* key, int64_t value) {
     g_tail_reduce = value != 0;
     return SIREN_OK;
   }
+  if (key && strcmp(key, "jvp_adj") == 0 && (value == 0 || value == 1)) {
+    g_jvp_adj = value != 0;
+    return SIREN_OK;
+  }
+  if (key && strcmp(key, "jvp_tn2") == 0 && (value == 0 || value == 1)) {
+    g_jvp_tn2 = value != 0;
+    return SIREN_OK;
+  }
   if (key && strncmp(key, "pair_split_", 11) == 0 && value >= 16 && value <= 31) {
     const char* k = key + 11;
     const int i = strcmp(k, "mid") == 0 ? 0 : strcmp(k, "top") == 0 ? 1 : strcmp(k, "bot") == 0 ? 2 : -1;
@@ -2237,6 +2303,8 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "dw_ring") == 0) return g_dw_ring ? 1 : 0;
   if (key && strcmp(key, "bwd_ring") == 0) return g_bwd_ring ? 1 : 0;
   if (key && strcmp(key, "pair_tail_reduce") == 0) return g_tail_reduce ? 1 : 0;
+  if (key && strcmp(key, "jvp_adj") == 0) return g_jvp_adj ? 1 : 0;
+  if (key && strcmp(key, "jvp_tn2") == 0) return g_jvp_tn2 ? 1 : 0;
   if (key && strcmp(key, "top_share") == 0) return g_top_share ? 1 : 0;
   if (key && strcmp(key, "debug_top_pass") == 0) return g_top_debug;
   if (key && strcmp(key, "pair_split_mid") == 0) return g_pair_split[0];

@@ -338,3 +338,62 @@ def test_primal_reuse_matches_recomputed_primal(order, batched):
         assert orc.norm_rel(a.cpu(), b.cpu()) < 1e-5
     if dx0 is not None:
         assert orc.norm_rel(dx1.cpu(), dx0.cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("order", ["gradient", "laplace", "jacobian"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("batched", [False, True])
+def test_fused_adjoint_combine_matches_two_launches(order, precision, batched):
+    """jvp_adj_kernel (the hidden layers' adjoint GEMM with the adjoint combine in its epilogue,
+    option jvp_adj, default on) against the two-launch path (jvp_nt adjoint GEMM, then
+    jvp_combine): the same formula on the same fp32 accumulators. Ragged rows (41^2, not a
+    multiple of the 64-row tile)."""
+    from siren_mri_amd import _native, jvp
+    from siren_mri_amd.meta import get_subdict
+    out = 2 if order == "jacobian" else 1
+    m = _model(256, 3, 33, precision, out=out)
+    B = 2 if batched else 1
+    coords = orc.get_mgrid(41)[None].repeat(B, 1, 1).to(DEV)
+    params = None
+    if batched:
+        params = {k: torch.stack([v * (1 + 0.03 * i) for i in range(B)]).requires_grad_(True)
+                  for k, v in m.state_dict().items()}
+    fn = {"gradient": jvp.siren_gradient, "laplace": jvp.siren_laplace, "jacobian": jvp.siren_jacobian}[order]
+    res = []
+    assert _native.get_option("jvp_adj") == 1 and _native.get_option("jvp_tn2") == 1
+    for fused, tn2 in ((1, 1), (0, 1), (1, 0)):
+        _native.set_option("jvp_adj", fused)
+        _native.set_option("jvp_tn2", tn2)
+        try:
+            m.zero_grad(set_to_none=True)
+            if params is not None:
+                for p in params.values():
+                    p.grad = None
+            x = coords.clone().requires_grad_(True)
+            o = m({"coords": x}, params=params)
+            sub = get_subdict(params, "net") if params is not None else None
+            val = fn(o["model_in"], m.net, sub)
+            torch.manual_seed(5)
+            w = torch.randn_like(val)
+            (val * w).sum().backward()
+            torch.cuda.synchronize()
+            grads = [p.grad.clone() for p in (params.values() if params is not None else m.parameters())
+                     if p.grad is not None]
+            res.append((grads, o["model_in"].grad.clone()))
+        finally:
+            _native.set_option("jvp_adj", 1)
+            _native.set_option("jvp_tn2", 1)
+    (g1, dx1), (g0, dx0), (gt, dxt) = res
+    assert len(g1) == len(g0) > 0
+    # the combine's fp32 arithmetic is the two-launch path's formula; the compiler contracts its
+    # products into FMAs differently in the two kernels (1-ulp differences), which the bf16 path's
+    # stored adjoints can round either way
+    tol = 1e-6 if precision == "fp32" else 5e-3
+    for a, b in zip(g1, g0):
+        assert orc.norm_rel(a.cpu(), b.cpu()) < tol
+    assert orc.norm_rel(dx1.cpu(), dx0.cpu()) < tol
+    # jvp_tn2 (fp32 weight gradients, all 256 rows per workgroup) vs the 128x128-tile kernel: the
+    # same products, split-K sums over other row ranges (fp32 rounding)
+    for a, b in zip(g1, gt):
+        assert orc.norm_rel(a.cpu(), b.cpu()) < 1e-6
+    assert torch.equal(dx1, dxt)
