@@ -86,10 +86,11 @@ DEV float cos_f32(float x) {
   return ((q + 1) & 2) ? -v : v;
 }
 
-// Fourier feature f of a row (features.py:21-41 as siren_kspace.hip fourier_kernel computes it,
-// with sin_f32 / cos_f32 for sincosf): z = sum_c x[c] B[c][k] (fma chain from 0), k = f mod m,
-// sin(2 pi z) for f < m, cos(2 pi z) for m <= f < 2m, 0 past 2m. Arguments stay inside the
-// Cody-Waite range for any |x| <= 1 coordinates and |B| entries below ~4000 (no far path here).
+// Fourier feature f of a row (features.py:21-41): z = sum_c x[c] B[c][k] (fma chain from 0), k = f
+// mod m, sin(2 pi z) for f < m, cos(2 pi z) for m <= f < 2m, 0 past 2m — bit-identical to
+// siren_kspace.hip fourier_kernel (the same chain, argument and sincos_poly), so features formed
+// here equal the materialised ones. Arguments stay inside the Cody-Waite range for any |x| <= 1
+// coordinates and |B| entries below ~4000 (no far path here).
 DEV float ff_feature(const float* xr, const float* B, int cin, int m, int f) {
   if (f >= 2 * m) return 0.f;
   const bool cosine = f >= m;

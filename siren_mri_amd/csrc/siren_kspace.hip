@@ -160,8 +160,22 @@ __global__ __launch_bounds__(KS_THREADS) void fourier_kernel(FourierArgs a) {
     float z = 0.f;
     for (int c = 0; c < a.cin; ++c) z = fmaf(a.x[r * a.cin + c], a.B[c * a.m + k], z);
     const float arg = __fmul_rn(6.2831854820251465f, z);  // (float)(2 pi), as 2 * np.pi * z in fp32
+    // the sin / cos of siren_common.h ff_feature (Cody-Waite + minimax, one reduction for both):
+    // the features the register forward forms in its first layer from the raw coordinates are then
+    // bit-identical to these, so the fused and the materialised paths compute the same network
     float sv, cv;
-    sincosf(arg, &sv, &cv);
+    if (__builtin_expect(__builtin_fabsf(arg) < 1.0e5f, 1)) {
+      float sn, cs;
+      int qd;
+      sincos_poly(arg, sn, cs, qd);
+      sv = (qd & 1) ? cs : sn;
+      sv = (qd & 2) ? -sv : sv;
+      cv = ((qd + 1) & 1) ? cs : sn;
+      cv = ((qd + 1) & 2) ? -cv : cv;
+    } else {
+      sv = sin_f32(arg);
+      cv = cos_f32(arg);
+    }
     a.out[r * 2 * a.m + k] = sv;
     a.out[r * 2 * a.m + a.m + k] = cv;
   }
