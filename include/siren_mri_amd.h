@@ -113,7 +113,10 @@ int siren_mlp_backward(const siren_mlp_desc* d, const float* x, const float* dy,
  * weight set), loss = weight * sum d^2 (deterministic order), y_dc = p and
  * dy = 2 weight hf d dDC/dy — dL/dy for a unit upstream gradient, which siren_mlp_backward_ex
  * scales by the device scalar dy_scale (the loss's upstream gradient) inside its output-layer
- * kernels. Shapes: the bf16 register-resident forward's (siren_mlp_loss_check).
+ * kernels. Where the loss runs (siren_mlp_loss_check): the bf16 register-resident forward's output
+ * epilogue (its shapes with 3+ layers; one output for 1..4 inputs), or the per-layer path's output
+ * kernel — fp32 mode (the reference's arithmetic) and bf16 shapes outside the register forward,
+ * up to 8 outputs. outermost_linear only.
  */
 typedef struct siren_loss_desc {
   const float* target;  /* [B * N, O]                                                  */

@@ -402,6 +402,12 @@ int prep_weights(const siren_mlp_desc* d, const Geo& g, const Layout& lo, char* 
 
 template <int PREC, int IT, int MAXO>
 void launch_last_fwd(const LastFwdArgs& a, int64_t nb, hipStream_t st) {
+  if (a.lloss) {  // fused image loss: at most SSE_MAX_BLOCKS workgroups (the hand-off's slots)
+    const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(a.rows_per_batch, 8),
+                                                                        std::max<int64_t>(1, SSE_MAX_BLOCKS / nb)));
+    hipLaunchKernelGGL((last_fwd_kernel<PREC, IT, MAXO, true>), dim3(gx, (unsigned)nb), dim3(256), 0, st, a);
+    return;
+  }
   const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(a.rows_per_batch, 8),
                                                                       std::max<int64_t>(1, 4096 / nb)));
   hipLaunchKernelGGL((last_fwd_kernel<PREC, IT, MAXO>), dim3(gx, (unsigned)nb), dim3(256), 0, st, a);
@@ -697,14 +703,16 @@ int fused_forward(const siren_mlp_desc* d, const Geo& g, const Layout& lo, const
   return check_launch("fused_fwd");
 }
 
+// L: the fused image loss in the output layer's epilogue (siren_mlp_forward_loss on the per-layer
+// path; the register forward has its own, fused_forward_reg)
 template <int PREC>
 int forward_impl(const siren_mlp_desc* d, const float* x, float* y, char* saved, char* ws,
-                 hipStream_t st) {
+                 hipStream_t st, const siren_loss_desc* L = nullptr) {
   const Geo g = geo_of(d);
   const Layout lo = layout_of(d);
   char* wbuf = saved ? saved : ws;  // prepared weights live in `saved` so backward reuses them
   const bool fused = PREC == kPrecBF16 && g_fused_forward && fused_shape(d);
-  if (fused) return fused_forward(d, g, lo, x, y, saved, wbuf, st);  // prepares its own weights
+  if (fused && !L) return fused_forward(d, g, lo, x, y, saved, wbuf, st);  // prepares its own weights
   int rc = prep_weights<PREC>(d, g, lo, wbuf, st);
   if (rc) return rc;
   auto phase_buf = [&](int l) -> char* {
@@ -780,6 +788,23 @@ int forward_impl(const siren_mlp_desc* d, const float* x, float* y, char* saved,
     a.O = d->dims[l + 1];
     a.sine_out = d->outermost_linear ? 0 : 1;
     a.w0 = d->w0;
+    a.ltgt = a.lk0 = a.lmask = a.lhf = nullptr;
+    a.ldc = a.ldy = a.lloss = a.lpart = nullptr;
+    a.lcounter = nullptr;
+    a.lnoise = a.lweight = 0.f;
+    if (L) {
+      a.ltgt = L->target;
+      a.lk0 = L->k0;
+      a.lmask = L->mask;
+      a.lhf = L->hf;
+      a.ldc = L->y_dc;
+      a.ldy = L->dy;
+      a.lloss = L->loss;
+      a.lpart = (float*)L->loss_workspace;
+      a.lcounter = (unsigned*)((char*)L->loss_workspace + SSE_MAX_BLOCKS * 4);
+      a.lnoise = L->noise;
+      a.lweight = L->weight;
+    }
     if ((rc = dispatch_last_fwd<PREC>(a, g.nb, st))) return rc;
   }
   return SIREN_OK;
@@ -1647,16 +1672,36 @@ int siren_mlp_backward(const siren_mlp_desc* d, const float* x, const float* dy,
                                  st);
 }
 
+}  // extern "C"
+namespace {
+// Which forward carries a fused image loss: the bf16 register-resident forward (its output-layer
+// epilogue, fused_fwd_reg_kernel<.., LOSS>) or the per-layer path's output kernel (last_fwd_kernel
+// <.., LOSS>: fp32 mode, and bf16 shapes that are not the fused forward's); 0 = none applies.
+int loss_path(const siren_mlp_desc* d) {
+  const int O = d->dims[d->num_layers];
+  if (!d->outermost_linear) return 0;
+  const bool fused = d->prec == SIREN_PREC_BF16 && g_fused_forward && fused_shape(d);
+  if (fused)
+    return (g_fwd_reg && d->num_layers >= 3 && !g_freg_magic && (fused_wide(d) || O == 1)) ? 1 : 0;
+  if (d->ff_B) return 0;  // (a Fourier-feature input is a register-forward form)
+  return O <= 8 ? 2 : 0;
+}
+
+int loss_path_fail(const siren_mlp_desc* d) {
+  if (!d->outermost_linear) return fail(SIREN_EINVAL, "fused loss: needs outermost_linear");
+  if (g_freg_magic) return fail(SIREN_EINVAL, "fused loss: not with option freg_magic");
+  return fail(SIREN_EINVAL, "fused loss: shape not supported (bf16 fused shapes: the register forward's "
+                            "forms with 3+ layers and 1 output for 1..4 inputs; per-layer path: <= 8 outputs)");
+}
+}  // namespace
+extern "C" {
+
 int siren_mlp_loss_check(const siren_mlp_desc* d, const siren_loss_desc* l) {
   int rc = siren_mlp_check(d);
   if (rc) return rc;
   if (!l) return fail(SIREN_EINVAL, "null loss descriptor");
-  if (d->prec != SIREN_PREC_BF16 || !g_fused_forward || !g_fwd_reg || !fused_shape(d) || d->num_layers < 3)
-    return fail(SIREN_EINVAL, "fused loss: needs the bf16 register-resident forward's shapes");
-  if (!d->outermost_linear) return fail(SIREN_EINVAL, "fused loss: needs outermost_linear");
-  if (g_freg_magic) return fail(SIREN_EINVAL, "fused loss: not with option freg_magic");
-  const int O = d->dims[d->num_layers];
-  if (!fused_wide(d) && O != 1) return fail(SIREN_EINVAL, "fused loss: 1..4 inputs need one output");
+  const int path = loss_path(d);
+  if (!path) return loss_path_fail(d);
   if (!l->target || !l->dy || !l->loss || !l->loss_workspace)
     return fail(SIREN_EINVAL, "fused loss: null target / dy / loss / workspace");
   if (l->loss_workspace_bytes < siren_sse_workspace_bytes())
@@ -1668,7 +1713,8 @@ int siren_mlp_loss_check(const siren_mlp_desc* d, const siren_loss_desc* l) {
     return fail(SIREN_EINVAL, "fused loss: hf has %lld entries for %lld rows per weight set", (long long)l->hf_len,
                 (long long)d->rows_per_batch);
   const Geo g = geo_of(d);
-  const int64_t wgs = std::min<int64_t>(cdiv(g.rows, FREG_WG_ROWS), std::max<int64_t>(1, 256 / g.nb)) * g.nb;
+  const int64_t wgs = path == 1 ? std::min<int64_t>(cdiv(g.rows, FREG_WG_ROWS), std::max<int64_t>(1, 256 / g.nb)) * g.nb
+                                : g.nb;  // (per-layer path: at most SSE_MAX_BLOCKS / nb workgroups per weight set)
   if (wgs > SSE_MAX_BLOCKS) return fail(SIREN_EINVAL, "fused loss: %lld workgroups > %d", (long long)wgs, SSE_MAX_BLOCKS);
   return SIREN_OK;
 }
@@ -1685,8 +1731,13 @@ int siren_mlp_forward_loss(const siren_mlp_desc* d, const siren_loss_desc* l, co
   if (!x || !y) return fail(SIREN_EINVAL, "null x or y");
   g_err.clear();
   const Geo g = geo_of(d);
-  char* wbuf = saved ? (char*)saved : (char*)workspace;
-  return fused_forward_reg(d, g, lo, x, y, (char*)saved, wbuf, (hipStream_t)stream, l);
+  if (loss_path(d) == 1) {
+    char* wbuf = saved ? (char*)saved : (char*)workspace;
+    return fused_forward_reg(d, g, lo, x, y, (char*)saved, wbuf, (hipStream_t)stream, l);
+  }
+  if (d->prec == SIREN_PREC_BF16)
+    return forward_impl<kPrecBF16>(d, x, y, (char*)saved, (char*)workspace, (hipStream_t)stream, l);
+  return forward_impl<kPrecF32>(d, x, y, (char*)saved, (char*)workspace, (hipStream_t)stream, l);
 }
 
 int siren_mlp_backward_ex(const siren_mlp_desc* d, const float* x, const float* dy, const float* dy_scale,

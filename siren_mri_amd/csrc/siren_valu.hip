@@ -37,6 +37,18 @@ struct LastFwdArgs {
   int F, O;
   int sine_out;        // 1: y = sin(w0 * z) (outermost_linear == False)
   float w0;
+  // LOSS (last_fwd_kernel<.., true>): the image loss of siren_mlp_forward_loss in the output
+  // epilogue, the register forward's arithmetic (siren_fwdreg.hip FwdRegArgs l* fields)
+  const float* ltgt;   // [B*N, O]
+  const float* lk0;    // [B, O, N] or null
+  const float* lmask;  // [B, O, N]
+  const float* lhf;    // [N] or null
+  float* ldc;          // [B*N, O] or null
+  float* ldy;          // [B*N, O]
+  float* lloss;        // [1]
+  float* lpart;        // [grid] per-workgroup sums
+  unsigned* lcounter;  // zero between launches
+  float lnoise, lweight;
 };
 
 struct LastBwdArgs {
@@ -178,11 +190,17 @@ __global__ __launch_bounds__(256) void first_fwd_kernel(FirstFwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-template <int PREC, int IT, int MAXO>
+// LOSS: also the fused image loss (siren_mlp_forward_loss on the per-layer path: fp32 mode and the
+// bf16 shapes outside the register forward): per output element p = DC(y) (with k0), d = hf (p - t),
+// the lane's sum of d^2, DC(y) and dL/dy = 2 w hf d dDC/dy — fused_fwd_reg_kernel's LOSS epilogue
+// arithmetic — then the workgroup sums through the write-through ticket hand-off of siren_loss.hip
+// (deterministic: fixed per-lane row order, wave / workgroup trees, workgroup sums in index order).
+template <int PREC, int IT, int MAXO, bool LOSS = false>
 __global__ __launch_bounds__(256) void last_fwd_kernel(LastFwdArgs a) {
   using PT = Prec<PREC>;
   using phase_t = typename PT::phase_t;
   const int l32 = threadIdx.x & 31;
+  float lsum = 0.f;
   const int64_t batch = blockIdx.y;
   const float* W = a.W + batch * a.w_bstride;
   const float* bias = a.b + batch * a.b_bstride;
@@ -222,7 +240,54 @@ __global__ __launch_bounds__(256) void last_fwd_kernel(LastFwdArgs a) {
       if (o < a.O) {
         float z = half_sum(acc[o]) + bias[o];
         if (a.sine_out) z = PT::sinr(a.w0 * z);
-        if (l32 == o) a.y[row * a.O + o] = z;
+        if (l32 == o) {
+          a.y[row * a.O + o] = z;
+          if constexpr (LOSS) {
+            const int64_t q = row * a.O + o;  // [B*N, O] element
+            float p = z, coef = 1.f;
+            if (a.lk0) {
+              const int64_t pl = (batch * a.O + o) * a.rows_per_batch + r;  // NCHW plane element
+              const float m = a.lmask[pl];
+              p = dc_value(z, a.lk0[pl], m, a.lnoise);
+              coef = dc_coef(m, a.lnoise);
+              a.ldc[q] = p;
+            }
+            const float h = a.lhf ? a.lhf[r] : 1.f;
+            const float dd = __fmul_rn(h, __fsub_rn(p, a.ltgt[q]));
+            lsum = fmaf(dd, dd, lsum);
+            float v = h * (dd * (2.f * a.lweight));
+            if (a.lk0) v *= coef;
+            a.ldy[q] = v;
+          }
+        }
+      }
+    }
+  }
+  if constexpr (LOSS) {
+    __shared__ float lred[4];
+    __shared__ unsigned lticket;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const float ws_ = wave_sum(lsum);
+    if (lane == 0) lred[wave] = ws_;
+    __syncthreads();
+    const unsigned nwg = gridDim.x * gridDim.y, wg = blockIdx.y * gridDim.x + blockIdx.x;
+    if (tid == 0) {
+      const float sacc = (lred[0] + lred[1]) + (lred[2] + lred[3]);
+      __hip_atomic_store(a.lpart + wg, sacc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lticket = __hip_atomic_fetch_add(a.lcounter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (lticket == nwg - 1) {
+      float sacc = 0.f;
+      for (unsigned b = tid; b < nwg; b += 256) sacc += __hip_atomic_load(a.lpart + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sacc = wave_sum(sacc);
+      __syncthreads();
+      if (lane == 0) lred[wave] = sacc;
+      __syncthreads();
+      if (tid == 0) {
+        a.lloss[0] = ((lred[0] + lred[1]) + (lred[2] + lred[3])) * a.lweight;
+        __hip_atomic_store(a.lcounter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }

@@ -514,7 +514,9 @@ def siren_mlp(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence
         ws, bs = [w[0] for w in ws], [b[0] for b in bs]
     keep = torch.is_grad_enabled() and (x.requires_grad or any(t.requires_grad for t in ws + bs))
     st = fusion.pending(x.device)
-    if st is not None and keep and outermost_linear and not return_saved and prec == _native.PREC_BF16:
+    if st is not None and keep and outermost_linear and not return_saved:
+        # the staged image loss in the forward's output epilogue: the bf16 register forward, or the
+        # per-layer path's output kernel (fp32 mode; siren_mlp_loss_check decides)
         y = _fused_loss_forward(st, x, ws, bs, w0, prec, geo)
         if y is not None:
             return y

@@ -284,3 +284,79 @@ def test_two_models_staged_on_two_streams_each_get_their_own_loss():
     out = ma({"coords": coords})
     assert rec.result is None
     fusion.clear(rec)
+
+
+@pytest.mark.parametrize("side,high_freq,hidden", [(128, True, 256), (128, False, 256), (96, True, 128)])
+def test_fp32_image_mse_fused_matches_unfused(side, high_freq, hidden):
+    """fp32 mode (the reference's arithmetic, precision's default): the staged image loss runs in the
+    per-layer path's output kernel (last_fwd_kernel's LOSS form) — y bit-identical to the unfused
+    forward, the loss and every gradient at the fp32 level of a reordered sum."""
+    from siren_mri_amd import dataio, fusion, loss_functions, modules
+    torch.manual_seed(side + hidden)
+    model = modules.SingleBVPNet(type="sine", hidden_features=hidden, num_hidden_layers=2, precision="fp32").to(DEV)
+    coords = dataio.get_mgrid(side)[None].to(DEV)
+    tgt = torch.randn(1, side * side, 1, generator=torch.Generator().manual_seed(side)).to(DEV)
+    ran = []
+
+    def step():
+        model.zero_grad(set_to_none=True)
+        st = fusion.stage_image_loss(tgt, high_freq=high_freq)
+        out = model({"coords": coords})
+        loss = loss_functions.image_mse(None, out, {"img": tgt}, high_freq=high_freq)["img_loss"]
+        ran.append(st is not None and st.result is not None and st.result[2] is loss)
+        fusion.clear(st)
+        (1.5 * loss).backward()
+        return out["model_out"].detach().clone(), loss.detach().clone(), _grads(model)
+
+    yf, lf, gf = _run(step, True)
+    yu, lu, gu = _run(step, False)
+    assert ran == [True, False]
+    assert torch.equal(yf, yu)
+    assert float(lf) == pytest.approx(float(lu), rel=1e-6)
+    assert gf.keys() == gu.keys() and len(gf) == 8
+    for k in gf:
+        assert orc.norm_rel(gf[k].cpu(), gu[k].cpu()) < 1e-6, k
+
+
+def test_fp32_hypernetwork_dc_loss_fused_matches_unfused():
+    """Configs 4/5's chain (DC + high-frequency-masked k-space loss) with an fp32 hypo-net: the
+    DC and the loss in last_fwd_kernel's epilogue."""
+    from siren_mri_amd import dataio, features, fusion, loss_functions, meta_modules
+    torch.manual_seed(1)
+    model = meta_modules.ConvolutionalNeuralProcessImplicit2DHypernetFourierFeatures(
+        in_features=16, out_features=2, image_resolution=(128, 128), fourier_features_size=16, latent_dim=16,
+        hidden_features=128, num_hidden_layers=2, hyper_hidden_features=32, hyper_hidden_layers=1,
+        conv_kernel_size=3, num_conv_res_blocks=1, w0=30, precision="fp32").to(DEV)
+    model.dc.noise_lvl = 0.25
+    B = 2
+    g = torch.Generator().manual_seed(13)
+    kspace = torch.randn(B, 2, 128, 128, generator=g).to(DEV)
+    mask = (torch.rand(B, 2, 128, 128, generator=g) < 0.3).float().to(DEV)
+    torch.manual_seed(0)
+    ff = features.GaussianFourierFeatureTransform(2, 8, 21, device=DEV)
+    coords = ff(dataio.get_mgrid(128)[None].repeat(B, 1, 1).to(DEV))
+    mi = {"coords": coords, "img_sparse": mask * kspace, "dc_mask": mask}
+    gt = {"img": kspace.permute(0, 2, 3, 1).reshape(B, -1, 2).contiguous()}
+    ran = []
+
+    def step():
+        model.zero_grad(set_to_none=True)
+        st = fusion.stage_image_loss(gt["img"])
+        out = model(mi)
+        ran.append(st is not None and st.result is not None and st.result[1] is out["model_out"])
+        hl = loss_functions.image_hypernetwork_loss(None, 2.78e-8, 6.4e-6, out, gt)
+        fusion.clear(st)
+        sum(v.mean() for v in hl.values()).backward()
+        return out["model_out"].detach().clone(), hl["img_loss"].detach().clone(), _grads(model)
+
+    yf, lf, gf = _run(step, True)
+    yu, lu, gu = _run(step, False)
+    assert ran == [True, False]
+    assert torch.equal(yf, yu)
+    assert float(lf) == pytest.approx(float(lu), rel=1e-6)
+    checked = 0
+    for k in gf:
+        if k.startswith("hyper_net"):
+            assert orc.norm_rel(gf[k].cpu(), gu[k].cpu()) < 1e-5, k
+            checked += 1
+    assert checked >= 4

@@ -258,3 +258,42 @@ def test_c4_size_fused_dc_loss_forward_vs_oracle():
     print("\n[C4 fused DC + hf loss forward, 32 x 128^2, bf16] " + " ".join(f"{k}={v:.2e}" for k, v in errs.items()))
     for k, v in errs.items():
         assert v <= TOL["bf16"][0], (k, errs)
+
+
+def test_metric_size_fp32_fused_loss_step_vs_oracle():
+    """The metric fit in fp32 (the reference's arithmetic) with the staged loss fused into the
+    per-layer path's output kernel: loss, y and every gradient vs the fp64 oracle at the fp32
+    tolerances."""
+    from siren_mri_amd import dataio, fusion, loss_functions
+    from siren_mri_amd.ops import siren_mlp
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    dims = orc.siren_dims(2, 256, 3, 1)
+    params = orc.siren_init(dims, seed=12)
+    x = orc.get_mgrid(512).unsqueeze(0)
+    tgt = torch.from_numpy(dataio.smooth_random_image(512, seed=2)).float().reshape(1, -1, 1)
+    ps = [(W.double().requires_grad_(True), b.double().requires_grad_(True)) for W, b in params]
+    y_ref = orc.siren_forward(x.double(), ps)
+    l_ref = ((y_ref - tgt.double()) ** 2).sum() * loss_functions.KSPACE_WEIGHT
+    l_ref.backward()
+    ws = [W.to(DEV).requires_grad_(True) for W, _ in params]
+    bs = [b.to(DEV).requires_grad_(True) for _, b in params]
+    td = tgt.to(DEV)
+    st = fusion.stage_image_loss(td, weight=loss_functions.KSPACE_WEIGHT)
+    try:
+        y = siren_mlp(x.to(DEV), ws, bs, precision="fp32")
+        loss = loss_functions.weighted_sse(y, td)
+        assert st is not None and st.result is not None and st.result[2] is loss
+    finally:
+        fusion.clear(st)
+    loss.backward()
+    torch.cuda.synchronize()
+    errs = {"loss": abs(float(loss) - float(l_ref)) / abs(float(l_ref)),
+            "y": orc.norm_rel(y.detach().cpu(), y_ref.detach())}
+    for l, ((rW, rb), w, b) in enumerate(zip(ps, ws, bs)):
+        errs[f"dW{l}"] = orc.norm_rel(w.grad.cpu(), rW.grad)
+        errs[f"db{l}"] = orc.norm_rel(b.grad.cpu(), rb.grad)
+    print("\n[M fused loss step 512^2 fp32] " + " ".join(f"{k}={v:.2e}" for k, v in errs.items()))
+    ty, tg = TOL["fp32"]
+    assert errs["loss"] <= ty and errs["y"] <= ty, errs
+    for k, v in errs.items():
+        assert v <= tg, (k, errs)

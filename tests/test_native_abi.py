@@ -115,3 +115,33 @@ def test_adam_rejects_bad_descriptors():
     assert lib.siren_adam_step(ctypes.byref(d), None) != 0
     d.num_tensors = 0
     assert lib.siren_adam_step(ctypes.byref(d), None) == 0
+
+
+def _loss_desc(**kw):
+    ld = _native.SirenLossDesc()
+    ld.target = ld.dy = ld.loss = ld.loss_workspace = 256
+    ld.loss_workspace_bytes = int(_native.load_library().siren_sse_workspace_bytes())
+    for k, v in kw.items():
+        setattr(ld, k, v)
+    return ld
+
+
+def test_fused_loss_check_paths():
+    """siren_mlp_loss_check: the bf16 register forward's shapes and (round 5) the per-layer path —
+    fp32 mode, the reference's arithmetic — take the fused image loss; a sine output layer or an
+    incomplete descriptor does not."""
+    lib = _native.load_library()
+    ok = [([2, 256, 256, 256, 256, 1], _native.PREC_BF16, {}),
+          ([2, 256, 256, 256, 256, 1], _native.PREC_F32, {}),
+          ([16, 256, 256, 256, 256, 2], _native.PREC_F32, dict(batch=32, weights_batched=True)),
+          ([2, 128, 128, 3], _native.PREC_BF16, {})]
+    for dims, prec, kw in ok:
+        d = _desc(dims, prec=prec, rows_per_batch=16384, **kw)
+        assert lib.siren_mlp_loss_check(ctypes.byref(d), ctypes.byref(_loss_desc())) == 0, (dims, _native.last_error())
+    d = _desc([2, 256, 256, 1], prec=_native.PREC_F32, rows_per_batch=4096, outermost_linear=False)
+    assert lib.siren_mlp_loss_check(ctypes.byref(d), ctypes.byref(_loss_desc())) != 0
+    assert "outermost_linear" in _native.last_error()
+    d = _desc([2, 256, 256, 1], prec=_native.PREC_F32, rows_per_batch=4096)
+    bad = _loss_desc(k0=256)  # k0 without mask / y_dc
+    assert lib.siren_mlp_loss_check(ctypes.byref(d), ctypes.byref(bad)) != 0
+    assert "together" in _native.last_error()
