@@ -463,6 +463,26 @@ def kernel_flops(wl, kclass):
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md §HBM (spec)
 
 
+def kernel_bytes(wl, kclass):
+    """Algorithmic HBM bytes of ONE launch of a kernel class (every input read once,
+    every output written once; split-K partial slabs, an implementation artefact, excluded), or
+    None for a class without a stated count. R rows per launch, F hidden width, C inputs, O outputs;
+    phases / gradients 2 B each in bf16 mode, 4 B in fp32."""
+    d = wl.dims
+    R, C, F, O = wl.coords, d[0], d[1], d[-1]
+    ps = 2 if wl.precision == "bf16" else 4
+    table = {
+        4: R * (4 * C + 3 * 2 * F + 3 * 4 * O),   # x; P_1..P_3 codes; y, the loss target, dL/dy
+        12: R * (3 * 2 * F),                      # dZ_l, P_{l-1} in; dZ_{l-1} out
+        13: R * (3 * 2 * F + 4 * O),              # P_top, dy, P_{top-1} in; dZ_{top-1} out
+        14: R * (2 * F + 2 * 4 * C),              # dZ_1, x in; dx out
+        1: R * (2 * ps * F),                      # P_{l-1} in, P_l out
+        2: R * (3 * ps * F),                      # dZ_l, P_{l-1} in, dZ_{l-1} out
+        3: R * (2 * ps * F),                      # dZ_l, P_{l-1} in
+    }
+    return table.get(kclass)
+
+
 def traffic_key(wl):
     """profiles/pmc_traffic.json key of a workload: precision, rows of ONE launch (the coordinate
     rows this GPU processes per step), hidden width and hidden-layer count."""
@@ -694,10 +714,24 @@ def measure(cfg, args, dev, rank, world, with_kernels=True):
             traffic_note = (f"rejected: {traffic} GB per launch over {avg_s * 1e3:.4f} ms would be "
                             f"{traffic / avg_s:.0f} GB/s, above the {HBM_PEAK_GBPS:.0f} GB/s HBM peak")
             traffic = None
+        nbytes = kernel_bytes(wl, dom)
+        mfma_frac = flops / avg_s / peak
+        hbm_frac = nbytes / avg_s / HBM_PEAK if nbytes else None
+        # the binding ceiling of the roofline model: HBM when the launch's arithmetic intensity
+        # (algorithmic FLOPs / algorithmic bytes) is below the ridge point peak / HBM bandwidth
+        ai = flops / nbytes if nbytes else None
+        hbm_bound = ai is not None and ai < peak / HBM_PEAK
         res["roofline"] = {
-            "bound": "mfma", "kernel": KCLASS_NAMES[dom], "kernel_symbol": KCLASS_SYMBOL.get(wl.precision, {}).get(dom),
-            "achieved": round(flops / avg_s / 1e12, 2), "peak": round(peak / 1e12, 1), "unit": "TFLOP/s",
-            "frac": round(flops / avg_s / peak, 4), "flops_per_launch": flops,
+            "bound": "hbm" if hbm_bound else "mfma", "kernel": KCLASS_NAMES[dom],
+            "kernel_symbol": KCLASS_SYMBOL.get(wl.precision, {}).get(dom),
+            "achieved": round(nbytes / avg_s / 1e9, 1) if hbm_bound else round(flops / avg_s / 1e12, 2),
+            "peak": HBM_PEAK / 1e9 if hbm_bound else round(peak / 1e12, 1),
+            "unit": "GB/s" if hbm_bound else "TFLOP/s",
+            "frac": round(hbm_frac if hbm_bound else mfma_frac, 4),
+            "mfma_frac": round(mfma_frac, 4), "hbm_frac": round(hbm_frac, 4) if hbm_frac else None,
+            "arithmetic_intensity_flop_per_byte": round(ai, 1) if ai else None,
+            "ridge_flop_per_byte": round(peak / HBM_PEAK, 1),
+            "bytes_per_launch": nbytes, "flops_per_launch": flops,
             "avg_launch_ms": round(kt.avg_ms, 4), "launches": kt.launches,
             "timing": "HIP event pairs on the launch stream around every launch of the kernel over a timed "
                       "region of K eager steps" + (" (the reported value is the hipGraph region's)" if graph else ""),
