@@ -38,10 +38,6 @@ struct TopArgs {
   float* partL;        // tn_dw only: dW_L / db_L partial slabs [split][nb][O*F_top + O]
   int64_t partL_stride;
   int O;
-  // pair_ring only: the output layer's dW_L / db_L sums are shared between the roles — the input-
-  // gradient role takes rows 0..15 of every 32-row tile (its dZ_top pass reads the same phases and
-  // dy) into slab npair + pair, the weight-gradient role rows 16..31 into slab pair
-  int dx_share;
 };
 // First-layer fusion into the bottom hidden layer's input-gradient kernel (C <= 4, no dx): the
 // epilogue accumulates dW_0 = dZ_0^T x and db_0 = sum dZ_0 (first_bwd_kernel's sums) instead of
@@ -99,9 +95,6 @@ struct TNArgs {
   int64_t rec_b0_bstride;
   TopArgs top;         // TOP: D = dZ_top formed from P_top, dy and W_L; also dW_L / db_L partials
   int pair_roles;      // pair_ring (debug timing only): bit 0 runs the dx role, bit 1 the dw role
-  int pair_nx;         // pair_ring: 0 = paired mapping (npair + npair); else the first pair_nx workgroups
-                       // take the input-gradient role and the rest the weight-gradient role, each
-                       // role's workgroups splitting the tiles evenly among themselves
   long long* prof;     // debug: [grid.x][8 waves][RING_NPROF] segment cycle counters (null: off)
 };
 
@@ -1287,17 +1280,6 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
 #pragma unroll
       for (int e = 0; e < 8; ++e) twl[o][e] = a.top.WL[batch * a.top.wl_bstride + (int64_t)o * K + 8 * (tid & 31) + e] * a.w0;
   }
-  // TOPO with dx_share: this thread's dW_L / db_L sums over rows tid / 32 of every tile (the
-  // weight-gradient role's arithmetic for those rows)
-  constexpr int TO = TOPO > 0 ? TOPO : 1;
-  const bool share = TOPO > 0 && (a.top.dx_share & 1);
-  float tdw[TO][8], tdb[TO];
-#pragma unroll
-  for (int o = 0; o < TO; ++o) {
-    tdb[o] = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) tdw[o][e] = 0.f;
-  }
 
   // both images: row r (512 B), 16-byte chunk c stored at chunk c ^ (r & 15)
   const uint32_t boff0 = r32 * 512 + 16 * (h ^ (r32 & 15));  // B fragment of K step 0 (ring_chain)
@@ -1386,7 +1368,6 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
   // separates it from the MFMAs that read it (the next iteration's barrier publishes it)
   auto top_pass = [&](int st) {
     if constexpr (TOPO > 0) {
-      if (a.top.dx_share & 2) return;  // debug timing only (results wrong): no dZ_top pass
       char* base = smem + st * STAGE;
       const float* gt = (const float*)(base + A_BYTES + C_BYTES);
 #pragma unroll
@@ -1407,18 +1388,6 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
           v[e] = (bf16)(dh * PT::cosp(ph[e]));
         }
         *(bf16x8*)pp = v;
-        if (q == 0 && share) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float sv = PT::sinp(ph[e]);
-#pragma unroll
-            for (int o = 0; o < TOPO; ++o) tdw[o][e] = fmaf(gg[o], sv, tdw[o][e]);
-          }
-          if (c == 0) {
-#pragma unroll
-            for (int o = 0; o < TOPO; ++o) tdb[o] += gg[o];
-          }
-        }
       }
     }
   };
@@ -1468,7 +1437,7 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
       // this stage's DMA (this wave's part) landed; then every wave's part, and every wave is done
       // with the stage the next DMA overwrites (tile i - 1: MFMA reads and its store pass)
       if (io) {
-        if (TOPO > 0 && !(a.top.dx_share & 4)) {  // (4: debug timing only, the plain ring's wait)
+        if constexpr (TOPO > 0) {
           if (i + 1 < niter) {
             if (i >= S - 2 && i + S - 2 < niter) vm_wait<STEADY_T>();
             else vm_drain();
@@ -1510,31 +1479,7 @@ DEV void dx_ring_body_v2(const NTArgs& a, char* smem, const int64_t t0, const in
   };
   if (a.stagger && wave >= 4) loop(std::true_type{});
   else loop(std::false_type{});
-  if constexpr (TOPO > 0) {
-    if (share) {
-      // dW_L [O][K] and db_L [O] over the 16 row slots (dw_ring_body's slab form), slab `slab`
-      __syncthreads();
-      float* red = (float*)smem;
-      constexpr int RS = TOPO * 256 + TOPO;
-      const int cth = tid & 31, rth = tid >> 5;
-#pragma unroll
-      for (int o = 0; o < TOPO; ++o)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) red[rth * RS + o * 256 + 8 * cth + e] = tdw[o][e];
-      if (cth == 0) {
-#pragma unroll
-        for (int o = 0; o < TOPO; ++o) red[rth * RS + TOPO * 256 + o] = tdb[o];
-      }
-      __syncthreads();
-      float* pl = a.top.partL + slab * a.top.partL_stride + batch * (int64_t)RS;
-      for (int idx = tid; idx < RS; idx += 512) {
-        float sum = 0.f;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) sum += red[k * RS + idx];
-        pl[idx] = sum;
-      }
-    }
-  }
+  (void)slab;
 }
 
 // dx_ring body of the bottom hidden layer with the first layer folded in and P_0 rebuilt from x
@@ -1930,8 +1875,6 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
   constexpr int TO = TOPO > 0 ? TOPO : 1;
   float twl[TO][8], tdw[TO][8], tdb[TO];
   const float dys = (TOPO > 0 && a.top.dy_scale) ? *a.top.dy_scale : 1.f;
-  // pair_ring with dx_share: the input-gradient role sums rows 0..15 of each chunk
-  const bool share = TOPO > 0 && (a.top.dx_share & 1);
 #pragma unroll
   for (int o = 0; o < TO; ++o) {
     tdb[o] = 0.f;
@@ -1992,14 +1935,12 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
 #pragma unroll
         for (int o = 1; o < TO; ++o) dh = fmaf(gg[o], twl[o][e], dh);
         dz[e] = (bf16)(dh * PT::cosp(pt[e]));
-        if (!share || qq == 1) {
-          const float sv = PT::sinp(pt[e]);
+        const float sv = PT::sinp(pt[e]);
 #pragma unroll
-          for (int o = 0; o < TO; ++o) tdw[o][e] = fmaf(gg[o], sv, tdw[o][e]);
-        }
+        for (int o = 0; o < TO; ++o) tdw[o][e] = fmaf(gg[o], sv, tdw[o][e]);
       }
       *(bf16x8*)(Db + off) = dz;
-      if (cth == 0 && (!share || qq == 1)) {
+      if (cth == 0) {
 #pragma unroll
         for (int o = 0; o < TO; ++o) tdb[o] += gg[o];
       }
@@ -2180,27 +2121,17 @@ __global__ __launch_bounds__(512) void pair_ring_bf16_kernel(NTArgs ax, TNArgs a
   const int64_t G = gridDim.x;
   const int64_t rows = ax.rows_per_batch;
   const int64_t ntiles = (rows + RING_BM - 1) / RING_BM;
-  // role, index within the role, workgroups of the role; nw = weight-gradient workgroups (slabs)
-  bool dxrole;
-  int64_t idx, nrole, nw;
-  if (aw.pair_nx <= 0) {
-    idx = (b & 7) | ((b >> 4) << 3);
-    nrole = nw = G >> 1;
-    dxrole = ((b >> 3) & 1) == 0;
-  } else {
-    // uneven split (the input-gradient role is the slower one): the roles no longer walk the same
-    // tiles on one XCD, but both sweep the rows front to back at the same pace
-    const int64_t nx = aw.pair_nx;
-    nw = G - nx;
-    dxrole = b < nx;
-    idx = dxrole ? b : b - nx;
-    nrole = dxrole ? nx : nw;
-  }
+  // pair (b & 7) + 16 k, (b & 7) + 16 k + 8: two workgroups on one XCD under round-robin dispatch
+  // (speed only), the first as the input-gradient role, the second as the weight-gradient role, both
+  // walking the same tile range; npair = weight-gradient workgroups = slabs
+  const int64_t idx = (b & 7) | ((b >> 4) << 3);
+  const int64_t nrole = G >> 1, nw = nrole;
+  const bool dxrole = ((b >> 3) & 1) == 0;
   const int64_t tb = ntiles * idx / nrole, te = ntiles * (idx + 1) / nrole;
   if (dxrole) {
     if (!(aw.pair_roles & 1)) return;
-    // slab: the first-layer slab (BOTC), or the shared output-layer slab after the nw of the other role
-    dx_ring_body<BOTC, DXOUT, REC, TOPO>(ax, smem, tb, 1, te - tb, TOPO > 0 ? nw + idx : idx);
+    // slab: the first-layer slab (BOTC)
+    dx_ring_body<BOTC, DXOUT, REC, TOPO>(ax, smem, tb, 1, te - tb, idx);
   } else {
     const int64_t r_end = te * RING_BM < rows ? te * RING_BM : rows;
     if (aw.pair_roles & 2) dw_ring_body<RECC, TOPO>(aw, smem, tb * RING_BM, r_end, idx);

@@ -102,9 +102,6 @@ bool g_jvp_adj = true;
 bool g_jvp_tn2 = true;      // fp32 analytic-derivative weight gradients on jvp_tn2_kernel      // analytic-derivative backward: adjoint GEMM + combine in one launch (jvp_adj_kernel)
 // pair_ring role split, input-gradient workgroups per 32 of the grid, per pair kind (middle, top,
 // bottom); 16 = the paired mapping (npair + npair, same tiles on one XCD)
-int g_pair_split[3] = {16, 16, 16};
-bool g_top_share = false;
-int g_top_debug = 0;  // debug timing only (results wrong unless 0): top pair dx role, 2 = no dZ_top pass, 4 = plain ring wait   // top pair: the dx role takes half the rows of the output layer's dW_L / db_L sums (measured: no gain, +1 % step)
 long long* g_ring_prof = nullptr;   // debug: pair_ring segment cycle counters, one block per launch
 int g_ring_prof_n = 0;
 long long* g_fused_prof = nullptr;
@@ -293,12 +290,12 @@ Layout layout_of(const siren_mlp_desc* d) {
   if (g.L >= 3) {
     const int F = d->dims[g.L - 1], O = d->dims[g.L];
     const int64_t ns = std::max(std::max(tn_split(g, F, d->dims[g.L - 2]).nsplit, dw_ring_split(g).nsplit),
-                                2 * pair_count(g));  // (top pair with the shared dW_L sums: 2 slabs a pair)
+                                pair_count(g));
     off = align_up(off + ns * split_stride(g, (int64_t)O * F + O) * 4, 256);
   }
   lo.partB_off = off;
-  // (the bottom pair's input-gradient role: up to 2 npair - 8 first-layer slabs, pair_split)
-  if (lo.p0_rec) off = align_up(off + 2 * kMaxPairs * split_stride(g, (int64_t)d->dims[1] * d->dims[0] + d->dims[1]) * 4, 256);
+  // (the bottom pair's input-gradient role: one first-layer slab per pair)
+  if (lo.p0_rec) off = align_up(off + kMaxPairs * split_stride(g, (int64_t)d->dims[1] * d->dims[0] + d->dims[1]) * 4, 256);
   lo.xcopy_off = off;
   if (lo.p0_rec) off = align_up(off + g.total * d->dims[0] * 4, 256);
   // paired 256x256 layers alternate between part and part2: a pair launch reduces the previous
@@ -863,18 +860,7 @@ int launch_pair(const siren_mlp_desc* d, const Geo& g, const Layout& lo, int kin
     a.bot.split_stride = bot_stride;
     a.bot.C = C;
   }
-  // top pair: dW_L / db_L sums split between the roles (slabs pair and npair + pair)
-  const bool share = kind == 2 && g_top_share;
-  a.top.dx_share = w.top.dx_share = (share ? 1 : 0) | (kind == 2 ? g_top_debug : 0);
-  // role split: nx input-gradient + nw weight-gradient workgroups (nw <= npair: the slab buffers)
-  int64_t nx = npair, nw = npair;
-  w.pair_nx = 0;
-  const int split = g_pair_split[kind - 1];
-  if (split != 16) {
-    nx = std::min<int64_t>(2 * npair - 8, std::max<int64_t>(npair, (2 * npair * split / 32) / 8 * 8));
-    nw = 2 * npair - nx;
-    if (nx != npair) w.pair_nx = (int)nx;
-  }
+  const int64_t nx = npair, nw = npair;  // input-gradient / weight-gradient workgroups (slabs)
   const dim3 grid((unsigned)(2 * npair), (unsigned)g.nb);
   const int kcls = kind == 1 ? SIREN_KCLASS_PAIR_RING : kind == 2 ? SIREN_KCLASS_PAIR_RING_TOP : SIREN_KCLASS_PAIR_RING_BOT;
   tmark_begin(kcls, st);
@@ -902,7 +888,7 @@ int launch_pair(const siren_mlp_desc* d, const Geo& g, const Layout& lo, int kin
   // this launch's slabs: reduced by the next pair launch, or by a reduce_multi launch (flush)
   ReduceList red;
   red.add(part, nw, w.split_stride, g.nb, (int64_t)M * N + M, (int64_t)M * N, dW[l], db[l]);
-  if (kind == 2) red.add(ta.partL, share ? nw + nx : nw, ta.partL_stride, g.nb, (int64_t)O * M + O, (int64_t)O * M, dW[g.L - 1], db[g.L - 1]);
+  if (kind == 2) red.add(ta.partL, nw, ta.partL_stride, g.nb, (int64_t)O * M + O, (int64_t)O * M, dW[g.L - 1], db[g.L - 1]);
   if (kind == 3) red.add(a.bot.part, nx, bot_stride, g.nb, (int64_t)F0 * C + F0, (int64_t)F0 * C, dW[0], db[0]);
   pend = red;
   return SIREN_OK;
@@ -2305,22 +2291,6 @@ int siren_config_set(const char* key, int64_t value) {
     g_jvp_tn2 = value != 0;
     return SIREN_OK;
   }
-  if (key && strncmp(key, "pair_split_", 11) == 0 && value >= 16 && value <= 31) {
-    const char* k = key + 11;
-    const int i = strcmp(k, "mid") == 0 ? 0 : strcmp(k, "top") == 0 ? 1 : strcmp(k, "bot") == 0 ? 2 : -1;
-    if (i >= 0) {
-      g_pair_split[i] = (int)value;
-      return SIREN_OK;
-    }
-  }
-  if (key && strcmp(key, "debug_top_pass") == 0 && (value == 0 || value == 2 || value == 4 || value == 6)) {
-    g_top_debug = (int)value;
-    return SIREN_OK;
-  }
-  if (key && strcmp(key, "top_share") == 0 && (value == 0 || value == 1)) {
-    g_top_share = value != 0;
-    return SIREN_OK;
-  }
   if (key && strcmp(key, "pair_ring") == 0 && (value == 0 || value == 1)) {
     g_pair_ring = value != 0;
     return SIREN_OK;
@@ -2356,11 +2326,6 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "pair_tail_reduce") == 0) return g_tail_reduce ? 1 : 0;
   if (key && strcmp(key, "jvp_adj") == 0) return g_jvp_adj ? 1 : 0;
   if (key && strcmp(key, "jvp_tn2") == 0) return g_jvp_tn2 ? 1 : 0;
-  if (key && strcmp(key, "top_share") == 0) return g_top_share ? 1 : 0;
-  if (key && strcmp(key, "debug_top_pass") == 0) return g_top_debug;
-  if (key && strcmp(key, "pair_split_mid") == 0) return g_pair_split[0];
-  if (key && strcmp(key, "pair_split_top") == 0) return g_pair_split[1];
-  if (key && strcmp(key, "pair_split_bot") == 0) return g_pair_split[2];
   if (key && strcmp(key, "dx_stagger") == 0) return g_dx_stagger ? 1 : 0;
   if (key && strcmp(key, "pair_ring") == 0) return g_pair_ring ? 1 : 0;
   if (key && strcmp(key, "debug_keep_p0") == 0) return g_keep_p0 ? 1 : 0;

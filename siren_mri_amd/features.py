@@ -57,11 +57,12 @@ torch.library.register_fake("siren_mri_amd::fourier_features",
 
 
 # Fourier features formed in the SIREN's first layer (GaussianFourierFeatureTransform.model_input,
-# ops.siren_mlp(ff_B=...)): OFF by default — the in-kernel features measured 1 % off the
-# materialised ones in the loss on the GPU at the end of round 4 (tests/test_gpu_fourier_input.py,
-# xfail); SIREN_MRI_AMD_FUSED_FOURIER=1 opts in. Off: the features are materialised by the
-# fourier_features op (one launch), the reference's data flow.
-FUSED_INPUT = os.environ.get("SIREN_MRI_AMD_FUSED_FOURIER", "0") == "1"
+# ops.siren_mlp(ff_B=...)): ON by default since round 5 — the kernels form the features with the
+# fourier_features op's own arithmetic (siren_common.h ff_feature = siren_kspace.hip fourier_kernel),
+# so the fused and the materialised paths compute the same network bit for bit
+# (tests/test_gpu_fourier_input.py). SIREN_MRI_AMD_FUSED_FOURIER=0 materialises the features with
+# the fourier_features op (one launch), the reference's data flow.
+FUSED_INPUT = os.environ.get("SIREN_MRI_AMD_FUSED_FOURIER", "1") == "1"
 
 
 def fourier_features(x, B):

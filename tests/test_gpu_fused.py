@@ -256,53 +256,3 @@ def test_pair_options_bit_identical(dims, n, option):
     for (a1, b1), (a0, b0) in zip(g1, g0):
         assert torch.equal(a1, a0) and torch.equal(b1, b0)
     assert torch.equal(dx1, dx0)
-
-
-@pytest.mark.parametrize("dims,n", [([2, 256, 256, 256, 256, 1], 70000), ([3, 256, 256, 256, 2], 999)])
-def test_top_share_matches(dims, n):
-    """top_share: the top pair's input-gradient role sums the output layer's dW_L / db_L over half of
-    every tile's rows (its own slabs); the result differs from the weight-gradient role's sums
-    only in fp32 summation order, and every other gradient is bit-identical."""
-    from siren_mri_amd import _native
-    params = _params(dims, None, seed=n)
-    x = torch.rand(1, n, dims[0], generator=torch.Generator().manual_seed(n)) * 2 - 1
-    res = {}
-    default = _native.get_option("top_share")
-    for v in (1, 0):
-        _native.set_option("top_share", v)
-        try:
-            res[v] = _grads(x, params, True, True, None)
-        finally:
-            _native.set_option("top_share", default)
-    (g1, dx1), (g0, dx0) = res[1], res[0]
-    L = len(g1)
-    for l, ((a1, b1), (a0, b0)) in enumerate(zip(g1, g0)):
-        if l == L - 1:
-            assert orc.norm_rel(a1, a0) < 1e-5 and orc.norm_rel(b1, b0) < 1e-5
-        else:
-            assert torch.equal(a1, a0) and torch.equal(b1, b0)
-    assert torch.equal(dx1, dx0)
-
-
-@pytest.mark.parametrize("option,value", [("pair_split_mid", 18), ("pair_split_top", 17), ("pair_split_bot", 20),
-                                          ("pair_split_bot", 31)])
-@pytest.mark.parametrize("dims,n", [([2, 256, 256, 256, 256, 1], 70000), ([3, 256, 256, 256, 256, 2], 999)])
-def test_pair_split_matches(dims, n, option, value):
-    """pair_split_*: more input-gradient than weight-gradient workgroups in a pair launch. The
-    input gradient of every tile is the same arithmetic (bit-identical dx); the weight gradients
-    are the same sums over other slab boundaries (fp32 summation order only)."""
-    from siren_mri_amd import _native
-    params = _params(dims, None, seed=n + value)
-    x = torch.rand(1, n, dims[0], generator=torch.Generator().manual_seed(n)) * 2 - 1
-    res = {}
-    default = _native.get_option(option)
-    for v in (value, 16):
-        _native.set_option(option, v)
-        try:
-            res[v] = _grads(x, params, True, True, None)
-        finally:
-            _native.set_option(option, default)
-    (g1, dx1), (g0, dx0) = res[value], res[16]
-    for (a1, b1), (a0, b0) in zip(g1, g0):
-        assert orc.norm_rel(a1, a0) < 1e-5 and orc.norm_rel(b1, b0) < 1e-5
-    assert torch.equal(dx1, dx0)
