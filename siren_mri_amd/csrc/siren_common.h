@@ -251,8 +251,13 @@ DEV void store_complete2(const T& data, const U& held) {
 // single wait state there. These stores carry their own `s_nop 1` (2 wait states) inside the asm
 // statement that takes the data as input, so nothing can write those registers before it has
 // passed — instead of waiting for the store to complete.
+// SIREN_STORE_MOD: cache-policy modifiers of these stores (timing experiments, e.g. " nt")
+#ifndef SIREN_STORE_MOD
+#define SIREN_STORE_MOD ""
+#endif
 DEV void store_b128_ws2(const u32x4_t& v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(r), "s"(soff)
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen" SIREN_STORE_MOD "\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(r),
+               "s"(soff)
                : "memory");
 }
 DEV void store_b32_ws2(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {

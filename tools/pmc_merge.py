@@ -58,7 +58,7 @@ def main(prefix, key, step_kernel="siren::adam_kernel"):
                   "the whole step's traffic (launches per step from dispatch counts)")
     with open(path, "w") as f:
         json.dump(d, f, indent=1, sort_keys=True)
-    print(json.dumps({k: v for k, v in entry.items() if k.startswith("_")}))
+    print(json.dumps({k: v for k, v in entry.items() if k.startswith("_step")}))
     for sym, e in sorted(((s, e) for s, e in entry.items() if not s.startswith("_")), key=lambda t: -t[1]["bytes"]):
         print(f"{e['bytes'] / 1e6:10.1f} MB  x{e['dispatches']:5d}  {sym}")
 
