@@ -273,7 +273,7 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
 #ifdef SIREN_FREG_DBG
   // timing builds only (compile-time, so the schedule of the rest is unchanged): 1: no hidden-
   // layer epilogue, 2: no barriers / ring refills, 4: no phase stores, 8: no layer-0 epilogue,
-  // 16: no hidden-layer MFMAs
+  // 16: no hidden-layer MFMAs, 256: half of the phase stores, 512: phase codes computed, not stored
   constexpr int dbg = SIREN_FREG_DBG;
 #else
   constexpr int dbg = 0;
@@ -468,6 +468,24 @@ __global__ __launch_bounds__(512) void fused_fwd_reg_kernel(FwdRegArgs a) {
   u32x4_t prevst = {0u, 0u, 0u, 0u};  // SIREN_FREG_DEFER: the data of the last code store
   auto p_store = [&](int pl, int pfb, int half, const u32x4_t& c, const u32x4_t& held) __attribute__((always_inline)) {
     if constexpr ((dbg & 4) != 0) return;
+    if constexpr ((dbg & 512) != 0) {  // timing only: the codes computed, not stored
+      asm volatile("" ::"v"(c));
+      return;
+    }
+    if constexpr ((dbg & 256) != 0) {  // timing only: half of the code stores (half 0 of every block)
+      if (half == 1) {
+        asm volatile("" ::"v"(c));
+        return;
+      }
+    }
+    if constexpr ((dbg & 1024) != 0) {
+      // timing only: every store instruction writes whole 128-byte lines — store k = 2 (pfb & 1) +
+      // half of a block pair covers rows 8 k .. 8 k + 7 of the wave, the pair's 128 bytes each
+      const int k = 2 * (pfb & 1) + half;
+      const uint32_t vo = (uint32_t)((wave * FREG_WROWS + 8 * k + (lane >> 3)) * (F * 2) + (lane & 7) * 16);
+      store_b128_ws2(c, p_rsrc(pl), vo, (pfb >> 1) * 128);
+      return;
+    }
     if constexpr ((dbg & 32) != 0) {  // timing only: the same bytes as one contiguous 1 KB per store
       __builtin_amdgcn_raw_buffer_store_b128(c, p_rsrc(pl), wave * 16384 + lane * 16, (pfb * 2 + half) * 1024, 0);
       return;

@@ -892,39 +892,65 @@ __global__ __launch_bounds__(256) void jvp_combine_kernel(JCombArgs a) {
     if (a.top)
       for (int o = 0; o < a.O; ++o) ws += WL[o * a.F + f];
     float dwl = 0.f;
-    for (int64_t n = r_begin; n < r_end; ++n) {
-      const phase_t p = ((const phase_t*)a.P)[(b * a.N + n) * a.F + f];
-      const float c = PT::cosp(p), s = PT::sinp(p);
-      const float* Ub = a.U + b * (int64_t)a.Su * plane + n * a.F + f;
-      const float* rw = a.top ? nullptr : a.raw + (b * S * a.N + n) * a.F + f;  // stream j: rw[j * plane]
-      const float hbar = a.top ? 0.f : rw[0];
-      float sbar = 0.f;
-      if (a.lap) sbar = a.top ? a.lbar[b * a.N + n] * ws : rw[(int64_t)(1 + a.C) * plane];
-      float cross = 0.f, q = 0.f;
-      for (int k = 0; k < a.C; ++k) {
-        const float u = Ub[(int64_t)k * plane];
-        float tbar = 0.f;
+    // four rows at a time: every load of the four first (in flight together), then the arithmetic
+    // and the stores — the stores would otherwise order each row's loads behind the previous row's
+    constexpr int RR = 4, MC = 4;  // rows per group; tangent streams (jvp_check: in_features <= 4)
+    for (int64_t n0 = r_begin; n0 < r_end; n0 += RR) {
+      phase_t pv[RR];
+      float uv[RR][MC + 1], rv[RR][MC + 2], gv[RR][MC], lv[RR];
+#pragma unroll
+      for (int j = 0; j < RR; ++j) {
+        const int64_t n = n0 + j < r_end ? n0 + j : r_end - 1;
+        pv[j] = ((const phase_t*)a.P)[(b * a.N + n) * a.F + f];
+        const float* Ub = a.U + b * (int64_t)a.Su * plane + n * a.F + f;
+#pragma unroll
+        for (int k = 0; k < MC + 1; ++k) uv[j][k] = k < a.Su ? Ub[(int64_t)k * plane] : 0.f;
         if (a.top) {
-          if (a.gbar) {
-            const float gk = a.gbar[(b * a.N + n) * a.C + k];
-            tbar = gk * ws;
-            dwl = fmaf(gk, w0 * c * u, dwl);
-          }
+#pragma unroll
+          for (int k = 0; k < MC; ++k) gv[j][k] = (a.gbar && k < a.C) ? a.gbar[(b * a.N + n) * a.C + k] : 0.f;
+          lv[j] = a.lap ? a.lbar[b * a.N + n] : 0.f;
         } else {
-          tbar = rw[(int64_t)(1 + k) * plane];
+          const float* rw = a.raw + (b * S * a.N + n) * a.F + f;  // stream j: rw[j * plane]
+#pragma unroll
+          for (int k = 0; k < MC + 2; ++k) rv[j][k] = k < S ? rw[(int64_t)k * plane] : 0.f;
         }
-        cross = fmaf(tbar, u, cross);
-        q = fmaf(u, u, q);
-        D[((b * S + 1 + k) * a.N + n) * a.F + f] = from_f32<grad_t>(w0 * c * tbar - 2.f * w02 * s * sbar * u);
       }
-      float abar = c * hbar - w0 * s * cross;
-      if (a.lap) {
-        const float v = Ub[(int64_t)a.C * plane];
-        abar -= w0 * sbar * (s * v + w0 * c * q);
-        D[((b * S + 1 + a.C) * a.N + n) * a.F + f] = from_f32<grad_t>(w0 * c * sbar);
-        if (a.top) dwl = fmaf(a.lbar[b * a.N + n], w0 * c * v - w02 * s * q, dwl);
+#pragma unroll
+      for (int j = 0; j < RR; ++j) {
+        const int64_t n = n0 + j;
+        if (n >= r_end) break;
+        const float c = PT::cosp(pv[j]), s = PT::sinp(pv[j]);
+        const float hbar = a.top ? 0.f : rv[j][0];
+        float sbar = 0.f;
+        if (a.lap) sbar = a.top ? lv[j] * ws : rv[j][1 + a.C];
+        float cross = 0.f, q = 0.f;
+#pragma unroll
+        for (int k = 0; k < MC; ++k) {
+          if (k >= a.C) break;
+          const float u = uv[j][k];
+          float tbar = 0.f;
+          if (a.top) {
+            if (a.gbar) {
+              const float gk = gv[j][k];
+              tbar = gk * ws;
+              dwl = fmaf(gk, w0 * c * u, dwl);
+            }
+          } else {
+            tbar = rv[j][1 + k];
+          }
+          cross = fmaf(tbar, u, cross);
+          q = fmaf(u, u, q);
+          D[((b * S + 1 + k) * a.N + n) * a.F + f] = from_f32<grad_t>(w0 * c * tbar - 2.f * w02 * s * sbar * u);
+        }
+        float abar = c * hbar - w0 * s * cross;
+        if (a.lap) {
+          const float v = uv[j][a.C];
+          abar -= w0 * sbar * (s * v + w0 * c * q);
+          D[((b * S + 1 + a.C) * a.N + n) * a.F + f] = from_f32<grad_t>(w0 * c * sbar);
+          if (a.top) dwl = fmaf(lv[j], w0 * c * v - w02 * s * q, dwl);
+        }
+        D[(b * S * a.N + n) * a.F + f] = from_f32<grad_t>(w0 * abar);
       }
-      D[(b * S * a.N + n) * a.F + f] = from_f32<grad_t>(w0 * abar);
     }
     if (a.top) {
       float* part = a.part + (int64_t)blockIdx.x * a.split_stride + b * (int64_t)(a.O * a.F + a.O);
@@ -1101,29 +1127,43 @@ __global__ __launch_bounds__(512) void jvp_adj_kernel(JAdjArgs a) {
   }
 
   // ---- the combine (jvp_combine_kernel, top = 0) on the accumulators ----
+  // Per 32-column block: the block's 16 phases and C (+1) tangents of every row this lane holds are
+  // loaded first (all in flight together: one memory latency per block, not one per element — the
+  // stores in between would otherwise order every load behind the previous element's stores),
+  // then combined and stored.
   const int F = a.Nout;
   const int64_t plane = N * (int64_t)F;
   const float w0 = a.w0, w02 = a.w0 * a.w0;
   grad_t* Do = (grad_t*)a.Dout + b * (int64_t)S * plane;
   const phase_t* Pb = (const phase_t*)a.P + b * plane;
   const float* Ub = a.U + b * (int64_t)a.Su * plane;
+  constexpr int NU = LAP ? C + 1 : C;
 #pragma unroll
   for (int bn = 0; bn < 2; ++bn) {
     const int f = 64 * wn + 32 * bn + r32;
     if (f >= F) continue;
+    phase_t pv[16];
+    float uv[NU][16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int64_t n = n0 + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+      const int64_t idx = (n < N ? n : N - 1) * F + f;
+      pv[e] = Pb[idx];
+#pragma unroll
+      for (int k = 0; k < NU; ++k) uv[k][e] = Ub[(int64_t)k * plane + idx];
+    }
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int64_t n = n0 + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
       if (n >= N) continue;
       const int64_t idx = n * F + f;
-      const phase_t p = Pb[idx];
-      const float c = PT::cosp(p), sn = PT::sinp(p);
+      const float c = PT::cosp(pv[e]), sn = PT::sinp(pv[e]);
       const float hbar = acc[0][bn][e];
       const float sbar = LAP ? acc[1 + C][bn][e] : 0.f;
       float cross = 0.f, q = 0.f;
 #pragma unroll
       for (int k = 0; k < C; ++k) {
-        const float u = Ub[(int64_t)k * plane + idx];
+        const float u = uv[k][e];
         const float tbar = acc[1 + k][bn][e];
         cross = fmaf(tbar, u, cross);
         q = fmaf(u, u, q);
@@ -1131,7 +1171,7 @@ __global__ __launch_bounds__(512) void jvp_adj_kernel(JAdjArgs a) {
       }
       float abar = c * hbar - w0 * sn * cross;
       if constexpr (LAP) {
-        const float v = Ub[(int64_t)C * plane + idx];
+        const float v = uv[C][e];
         abar -= w0 * sbar * (sn * v + w0 * c * q);
         Do[(int64_t)(1 + C) * plane + idx] = from_f32<grad_t>(w0 * c * sbar);
       }
