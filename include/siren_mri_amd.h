@@ -290,6 +290,23 @@ int siren_conv_fwd_k5(const void* x, const void* w, const void* bias, int relu, 
                       void* stream);
 int siren_conv_wrw_k5(const void* x, const void* dy, int N, int H, int W, int C, float* dw, void* ws, int64_t ws_bytes,
                       void* stream);
+/* The encoder's other convolution shapes (round 5; ConvImgEncoder's cnn[0], modules.py:351 — 64 ->
+ * 128 channels, 7x7 in configs 4/5 — its input gradient as a forward convolution of the flipped,
+ * transposed filter, and the 3x3 forms), stride 1, 'same' padding, bf16 NHWC, fp32 accumulation:
+ * filter size KS in {3, 5, 7}, CI in {64, 128} input channels.
+ *   siren_conv_fwd : y = conv(x, w) (+ bias, ReLU as siren_conv_fwd_k5); W = 128, H even, CO a
+ *                    multiple of 64; w is [CO][KS][KS][CI].
+ *   siren_conv_wrw : dw[CO][KS][KS][CI] (fp32) = the weight gradient of that convolution; W a
+ *                    multiple of 64, CO a multiple of 128 (CI 64) or 64 (CI 128); split-K partials
+ *                    in ws (siren_conv_wrw_ws_bytes) added in split order (deterministic).
+ *   siren_conv_check: SIREN_OK when the shape (kind 0 forward, 1 weight gradient) runs natively;
+ *                    the encoder falls back to MIOpen otherwise. */
+int siren_conv_check(int kind, int N, int H, int W, int CI, int CO, int KS);
+int siren_conv_fwd(const void* x, const void* w, const void* bias, int relu, void* y, int N, int H, int W, int CI,
+                   int CO, int KS, void* stream);
+int64_t siren_conv_wrw_ws_bytes(int N, int H, int W, int CI, int CO, int KS);
+int siren_conv_wrw(const void* x, const void* dy, int N, int H, int W, int CI, int CO, int KS, float* dw, void* ws,
+                   int64_t ws_bytes, void* stream);
 int siren_enc_relu_bwd(const void* g1, const void* g2, const void* y, void* out, float* db, int64_t P, int C, void* ws,
                        int64_t ws_bytes, void* stream);
 int siren_enc_bias_relu(void* y, const void* cb, int64_t P, int C, void* stream);

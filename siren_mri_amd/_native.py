@@ -53,6 +53,10 @@ EXPORTED_SYMBOLS = (
     "siren_conv_wrw_workspace_bytes",
     "siren_conv_wrw_k5",
     "siren_conv_fwd_k5",
+    "siren_conv_check",
+    "siren_conv_fwd",
+    "siren_conv_wrw_ws_bytes",
+    "siren_conv_wrw",
     "siren_enc_bias_relu",
     "siren_enc_relu_bwd",
     "siren_enc_res_fwd",
@@ -229,6 +233,14 @@ def _declare(lib):
     lib.siren_conv_wrw_k5.restype = ci
     lib.siren_conv_fwd_k5.argtypes = [vp, vp, vp, ci, vp, ci, ci, ci, ci, vp]
     lib.siren_conv_fwd_k5.restype = ci
+    lib.siren_conv_check.argtypes = [ci, ci, ci, ci, ci, ci, ci]
+    lib.siren_conv_check.restype = ci
+    lib.siren_conv_fwd.argtypes = [vp, vp, vp, ci, vp, ci, ci, ci, ci, ci, ci, vp]
+    lib.siren_conv_fwd.restype = ci
+    lib.siren_conv_wrw_ws_bytes.argtypes = [ci, ci, ci, ci, ci, ci]
+    lib.siren_conv_wrw_ws_bytes.restype = i64
+    lib.siren_conv_wrw.argtypes = [vp, vp, ci, ci, ci, ci, ci, ci, vp, vp, i64, vp]
+    lib.siren_conv_wrw.restype = ci
     lib.siren_enc_workspace_bytes.argtypes = []
     lib.siren_enc_workspace_bytes.restype = i64
     lib.siren_enc_relu_bwd.argtypes = [vp, vp, vp, vp, vp, i64, ci, vp, i64, vp]

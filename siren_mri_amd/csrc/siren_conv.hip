@@ -402,3 +402,372 @@ __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
 }
 
 }  // namespace siren
+
+namespace siren {
+
+// ------------------------------------------------------------------------------------------
+// The same two kernels for the encoder's other convolution shapes: an odd
+// filter size KS (3, 5, 7), CI input channels (a multiple of 32), output channels in tiles of COT
+// (forward) or 32 CB (weight gradient), images 128 pixels wide (forward) / a multiple of 64
+// (weight gradient). ConvImgEncoder's cnn[0] (64 -> 128, 7x7 in configs 4/5: modules.py:351) and
+// its input gradient (128 -> 64, the flipped filter), their 3x3 forms (kernel_size=3, the default),
+// and the 128 -> 128 5x5 residual convolutions (which keep conv_fwd_k5_kernel / conv_wrw_k5_kernel).
+// Same tiling, pipelines and arithmetic as those: per stage one filter row kh and a 32-channel
+// chunk; the K order per output element is (kh, chunk, kw, channel), as there.
+// ------------------------------------------------------------------------------------------
+struct ConvGArgs {
+  const bf16* x;     // [N][H][W][CI]
+  const bf16* w;     // forward: [CO][KS][KS][CI]
+  const bf16* bias;  // [CO] or null
+  bf16* y;           // forward: [N][H][W][CO]
+  const bf16* dy;    // weight gradient: [N][H][W][CO]
+  float* part;       // weight gradient: [nsplit][KS][KS][CO][CI]
+  float* dw;         // weight gradient: [CO][KS][KS][CI]
+  int N, H, W, CO;
+  int relu;
+  int64_t rows_per_split;
+  int nsplit;
+};
+
+// wait for all but the N youngest LDS reads, then tie every fragment to that wait (the compiler
+// takes an asm output as defined at the asm: an MFMA operand tied after the wait reads landed data)
+// (the counter holds 15 at most: a larger N waits for 15, i.e. for more of the reads — still correct)
+template <int N>
+DEV void lgkm_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N < 15 ? N : 15) : "memory");
+}
+DEV void tie(TrFrag& f) { asm volatile("" : "+v"(f.lo), "+v"(f.hi)); }
+DEV void tie(bf16x8& v) { asm volatile("" : "+v"(v)); }
+
+template <int KS, int CI, int COT>
+__global__ __launch_bounds__(512) void conv_fwd_gen_kernel(ConvGArgs a) {
+  constexpr int HALO = CF_W + KS - 1;
+  constexpr int XB = 2 * HALO * CF_ROWB;
+  constexpr int WB = KS * COT * CF_ROWB;
+  constexpr int STAGE = XB + WB;
+  constexpr int XP = 2 * HALO * 4, WP = KS * COT * 4;
+  constexpr int NL = (XP + WP + 511) / 512;
+  constexpr int NCC = CI / CF_CC;
+  constexpr int NS = KS * NCC;
+  constexpr int NI = COT / 64;  // 32-channel blocks per wave
+  static_assert(CI % CF_CC == 0 && (COT == 64 || COT == 128) && KS % 2 == 1, "conv shape");
+  static_assert(2 * STAGE <= 160 * 1024, "two LDS stages");
+  __shared__ __attribute__((aligned(16))) char smem_g[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wc = wave & 1, wp = wave >> 1;
+  const int hp = a.H / 2;
+  const int n = blockIdx.x / hp, h0 = 2 * (blockIdx.x % hp);
+  const int co0 = blockIdx.y * COT;
+  // the epilogue's kernel arguments, loaded here: a scalar load left in flight inside the K loop
+  // would void its counted LDS waits (lgkmcnt counts both, scalar loads out of order;
+  // tools/check_lds_hazard.py)
+  int CO = a.CO, relu = a.relu;
+  uint64_t ybits = (uint64_t)a.y, bbits = (uint64_t)a.bias;
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(CO), "+s"(relu), "+s"(ybits), "+s"(bbits));
+  bf16* const yout = (bf16*)ybits;
+  const bf16* const bias = (const bf16*)bbits;
+
+  f32x16 acc[NI][2];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  u32x4_t lv[2][NL];
+  const u32x4_t zero = {0u, 0u, 0u, 0u};
+  auto load = [&](int s, auto set_c) {
+    constexpr int set = decltype(set_c)::value;
+    const int kh = s / NCC, cc = s % NCC;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int q = tid + 512 * i;
+      u32x4_t v = zero;
+      if (q < XP) {
+        const int r = q / (4 * HALO), j = (q >> 2) % HALO, pc = q & 3;
+        const int xr = h0 + r + kh - KS / 2, w = j - KS / 2;
+        if (xr >= 0 && xr < a.H && w >= 0 && w < CF_W)
+          v = *(const u32x4_t*)(a.x + (((int64_t)n * a.H + xr) * CF_W + w) * CI + CF_CC * cc + 8 * pc);
+      } else if (q < XP + WP) {
+        const int q2 = q - XP, kw = q2 / (4 * COT), co = (q2 >> 2) % COT, pc = q2 & 3;
+        v = *(const u32x4_t*)(a.w + ((int64_t)((co0 + co) * KS + kh) * KS + kw) * CI + CF_CC * cc + 8 * pc);
+      }
+      lv[set][i] = v;
+    }
+  };
+  auto stage = [&](auto set_c, int buf) {
+    constexpr int set = decltype(set_c)::value;
+    char* base = smem_g + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int q = tid + 512 * i;
+      if (q < XP) {
+        const int r = q / (4 * HALO), j = (q >> 2) % HALO, pc = q & 3;
+        *(u32x4_t*)(base + (r * HALO + j) * CF_ROWB + 16 * pc) = lv[set][i];
+      } else if (q < XP + WP) {
+        const int q2 = q - XP, kw = q2 / (4 * COT), co = (q2 >> 2) % COT, pc = q2 & 3;
+        *(u32x4_t*)(base + XB + (kw * COT + co) * CF_ROWB + 16 * pc) = lv[set][i];
+      }
+    }
+  };
+
+  // A (filter) lane -> out channel (COT / 2) wc + 32 i + (lane & 31); B (pixels) lane -> pixel
+  // 64 wp + 32 j + (lane & 31) of the row pair, the tap's halo column + kw
+  const int l32 = lane & 31, kh2 = lane >> 5;
+  uint32_t aoff[NI], boff[2];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) aoff[i] = XB + ((COT / 2) * wc + 32 * i + l32) * CF_ROWB + 16 * kh2;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int px = 64 * wp + 32 * j + l32;
+    boff[j] = ((px >> 7) * HALO + (px & 127)) * CF_ROWB + 16 * kh2;
+  }
+  const uint32_t sbase = lds_addr(smem_g);
+
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  load(0, S0{});
+  stage(S0{}, 0);
+  if (NS > 1) load(1, S1{});
+  __syncthreads();
+  auto iter = [&](int s, auto par_c) {
+    constexpr int par = decltype(par_c)::value;
+    using SN = std::integral_constant<int, par ^ 1>;
+    using SC = std::integral_constant<int, par>;
+    if (s + 1 < NS) stage(SN{}, (s + 1) & 1);
+    if (s + 2 < NS) load(s + 2, SC{});
+    const uint32_t sb = sbase + (s & 1) * STAGE;
+    // 2 KS K steps (kw, ks); step i + 1's fragments are read while step i's MFMAs run
+    bf16x8 af[2][NI], bfr[2][2];
+#define SIREN_CG_RD(I)                                                                                               \
+  {                                                                                                                  \
+    constexpr int kw_ = (I) >> 1, ks_ = (I) & 1, b_ = (I) & 1;                                                       \
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(af[b_][0]) : "v"(sb + aoff[0]), "n"(kw_ * COT * CF_ROWB + 32 * ks_)); \
+    if constexpr (NI > 1)                                                                                            \
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(af[b_][NI - 1]) : "v"(sb + aoff[NI - 1]), "n"(kw_ * COT * CF_ROWB + 32 * ks_)); \
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bfr[b_][0]) : "v"(sb + boff[0]), "n"(kw_ * CF_ROWB + 32 * ks_));    \
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bfr[b_][1]) : "v"(sb + boff[1]), "n"(kw_ * CF_ROWB + 32 * ks_));    \
+  }
+    static_assert(NI == 1 || NI == 2, "one or two 32-channel blocks per wave");
+    SIREN_CG_RD(0)
+    static_for<0, 2 * KS>([&](auto i_c) {
+      constexpr int i = decltype(i_c)::value, b = i & 1;
+      if constexpr (i + 1 < 2 * KS) {
+        SIREN_CG_RD(i + 1)
+        lgkm_wait<NI + 2>();
+      } else {
+        lgkm_wait<0>();
+      }
+#pragma unroll
+      for (int ii = 0; ii < NI; ++ii) tie(af[b][ii]);
+      tie(bfr[b][0]);
+      tie(bfr[b][1]);
+#pragma unroll
+      for (int ii = 0; ii < NI; ++ii)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[b][ii], bfr[b][j], acc[ii][j], 0, 0, 0);
+    });
+#undef SIREN_CG_RD
+    __syncthreads();
+  };
+  for (int s = 0; s < NS; s += 2) {
+    iter(s, S0{});
+    if (s + 1 < NS) iter(s + 1, S1{});
+  }
+
+  // epilogue: D[co][px] -> LDS tile [256 px][COT] bf16, then 16-byte stores of whole pixel rows
+  constexpr int OROW = COT * 2 + 16;
+  static_assert(256 * OROW <= 2 * STAGE, "output tile");
+  char* ot = smem_g;
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int px = 64 * wp + 32 * j + l32;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int co = (COT / 2) * wc + 32 * i + 8 * g + 4 * kh2 + e;
+          float z = (float)(bf16)acc[i][j][4 * g + e];
+          if (bias) {
+            z = (float)(bf16)(z + (float)bias[co0 + co]);
+            if (relu) z = fmaxf(z, 0.f);
+          }
+          v[e] = (bf16)z;
+        }
+        const int co = (COT / 2) * wc + 32 * i + 8 * g + 4 * kh2;
+        *(bf16x4*)(ot + px * OROW + co * 2) = v;
+      }
+    }
+  __syncthreads();
+  // the pair's 256 px x COT channels as 16-byte buffer stores (each with its 2 wait states)
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(yout + ((int64_t)n * a.H + h0) * CF_W * CO, 2 * CF_W * CO * 2);
+  constexpr int PPR = COT / 8;  // 16-byte pieces per pixel
+#pragma unroll
+  for (int k = 0; k < 256 * PPR / 512; ++k) {
+    const int q = tid + 512 * k;
+    const int px = q / PPR, pc = q % PPR;
+    store_b128_ws2(*(const u32x4_t*)(ot + px * OROW + 16 * pc), ry, (uint32_t)((px * CO + co0 + 8 * pc) * 2), 0);
+  }
+}
+
+template <int KS, int CI, int CB>
+__global__ __launch_bounds__(512) void conv_wrw_gen_kernel(ConvGArgs a) {
+  constexpr int IB = CI / 32;
+  static_assert(CB * IB == 8, "8 waves: CB co blocks x IB ci blocks");
+  constexpr int COW = 32 * CB;                 // output channels per workgroup
+  constexpr int XR = CW_PX + KS - 1;           // halo rows
+  constexpr int DROW = COW + 32, XROW = CI + 32;  // bf16 per staged row (+64-byte pad)
+  constexpr int DP = CW_PX * COW / 8, XPC = XR * CI / 8;  // 16-byte pieces
+  constexpr int NDL = (DP + 511) / 512, NXL = (XPC + 511) / 512;
+  __shared__ __attribute__((aligned(16))) bf16 sD[CW_NB][CW_PX * DROW];
+  __shared__ __attribute__((aligned(16))) bf16 sX[CW_NB][XR * XROW];
+  const int split = blockIdx.x, kh = blockIdx.y, ch = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cb = wave % CB, ib = wave / CB;
+  const int nrows = a.N * a.H;
+  const int64_t r0 = (int64_t)split * a.rows_per_split;
+  const int64_t r1 = r0 + a.rows_per_split < nrows ? r0 + a.rows_per_split : nrows;
+  const int nch = a.W / CW_PX;
+  const int64_t T = r1 > r0 ? (r1 - r0) * nch : 0;
+  const int CO = a.CO;
+
+  f32x16 acc[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[k][e] = 0.f;
+
+  u32x4_t dv[2][NDL], xv[2][NXL];
+  const u32x4_t zero = {0u, 0u, 0u, 0u};
+  auto load = [&](int64_t t, auto set_c) {
+    constexpr int set = decltype(set_c)::value;
+    const int64_t r = r0 + t / nch;
+    const int px0 = (int)(t % nch) * CW_PX;
+    const int n = (int)(r / a.H), h = (int)(r % a.H);
+    const int xr = h + kh - KS / 2;
+    const bool rowok = xr >= 0 && xr < a.H;
+#pragma unroll
+    for (int i = 0; i < NDL; ++i) {
+      const int q = tid + 512 * i;
+      const int px = q / (COW / 8), pc = q % (COW / 8);
+      dv[set][i] = q < DP ? *(const u32x4_t*)(a.dy + (((int64_t)n * a.H + h) * a.W + px0 + px) * CO + COW * ch + 8 * pc)
+                          : zero;
+    }
+    const bf16* xrow = a.x + ((int64_t)n * a.H + (rowok ? xr : 0)) * a.W * CI;
+#pragma unroll
+    for (int i = 0; i < NXL; ++i) {
+      const int p = tid + 512 * i;
+      const int w = px0 - KS / 2 + p / (CI / 8);
+      const bool ok = p < XPC && rowok && w >= 0 && w < a.W;
+      xv[set][i] = ok ? *(const u32x4_t*)(xrow + (int64_t)w * CI + 8 * (p % (CI / 8))) : zero;
+    }
+  };
+  auto stage = [&](auto set_c, int buf) {
+    constexpr int set = decltype(set_c)::value;
+#pragma unroll
+    for (int i = 0; i < NDL; ++i) {
+      const int q = tid + 512 * i;
+      if (q < DP) *(u32x4_t*)(&sD[buf][(q / (COW / 8)) * DROW + 8 * (q % (COW / 8))]) = dv[set][i];
+    }
+#pragma unroll
+    for (int i = 0; i < NXL; ++i) {
+      const int p = tid + 512 * i;
+      if (p < XPC) *(u32x4_t*)(&sX[buf][(p / (CI / 8)) * XROW + 8 * (p % (CI / 8))]) = xv[set][i];
+    }
+  };
+
+  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  const int ca = 32 * cb + 16 * (g & 1) + 4 * tp;
+  const int cx = 32 * ib + 16 * (g & 1) + 4 * tp;
+  const int r8 = 8 * (g >> 1) + tq;
+  const uint32_t dbase = lds_addr(&sD[0][0]) + (uint32_t)((r8 * DROW + ca) * 2);
+  const uint32_t xbase = lds_addr(&sX[0][0]) + (uint32_t)((r8 * XROW + cx) * 2);
+  constexpr uint32_t DSTAGE = CW_PX * DROW * 2, XSTAGE = XR * XROW * 2;
+  constexpr int DROWB = DROW * 2, XROWB = XROW * 2;
+  constexpr int NRD = 2 + 2 * KS;  // fragment reads per K step
+
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  if (T > 0) {
+    load(0, S0{});
+    stage(S0{}, 0);
+  }
+  if (T > 1) load(1, S1{});
+  __syncthreads();
+  auto iter = [&](int64_t t, auto par_c) {
+    constexpr int par = decltype(par_c)::value;
+    using SN = std::integral_constant<int, par ^ 1>;
+    using SC = std::integral_constant<int, par>;
+    if (t + 1 < T) stage(SN{}, (int)((t + 1) % CW_NB));
+    if (t + 2 < T) load(t + 2, SC{});
+    const int buf = (int)(t % CW_NB);
+    const uint32_t db = dbase + buf * DSTAGE, xb = xbase + buf * XSTAGE;
+    TrFrag fa[2], fb[2][KS];
+#define SIREN_CWG_RD(KS_)                                                         \
+  {                                                                               \
+    constexpr int ks_ = (KS_), b_ = (KS_) & 1;                                    \
+    tr16_read<16 * ks_ * DROWB>(fa[b_].lo, db);                                   \
+    tr16_read<16 * ks_ * DROWB + 4 * DROWB>(fa[b_].hi, db);                       \
+    static_for<0, KS>([&](auto kw_c) {                                            \
+      constexpr int kw = decltype(kw_c)::value;                                   \
+      tr16_read<(16 * ks_ + kw) * XROWB>(fb[b_][kw].lo, xb);                      \
+      tr16_read<(16 * ks_ + kw + 4) * XROWB>(fb[b_][kw].hi, xb);                  \
+    });                                                                           \
+  }
+    SIREN_CWG_RD(0)
+    static_for<0, CW_PX / 16>([&](auto ks_c) {
+      constexpr int ks = decltype(ks_c)::value, b = ks & 1;
+      if constexpr (ks + 1 < CW_PX / 16) {
+        SIREN_CWG_RD(ks + 1)
+        lgkm_wait<NRD>();
+      } else {
+        lgkm_wait<0>();
+      }
+      tie(fa[b]);
+      static_for<0, KS>([&](auto kw_c) { tie(fb[b][decltype(kw_c)::value]); });
+      static_for<0, KS>([&](auto kw_c) {
+        constexpr int kw = decltype(kw_c)::value;
+        acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr16_value(fa[b]), tr16_value(fb[b][kw]), acc[kw], 0, 0, 0);
+      });
+    });
+#undef SIREN_CWG_RD
+    __syncthreads();
+  };
+  for (int64_t t = 0; t < T; t += 2) {
+    iter(t, S0{});
+    if (t + 1 < T) iter(t + 1, S1{});
+  }
+
+  // partial: [split][kh][kw][co][ci]
+  float* P = a.part + ((int64_t)split * KS + kh) * KS * (int64_t)CO * CI;
+#pragma unroll
+  for (int kw = 0; kw < KS; ++kw) {
+    const int ci = 32 * ib + (lane & 31);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int co = COW * ch + 32 * cb + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+      P[((int64_t)kw * CO + co) * CI + ci] = acc[kw][e];
+    }
+  }
+}
+
+// dw[co][kh][kw][ci] = sum_s part[s][kh][kw][co][ci], splits in order
+template <int KS, int CI>
+__global__ __launch_bounds__(256) void conv_wrw_gen_reduce_kernel(ConvGArgs a) {
+  const int64_t slab = (int64_t)KS * KS * a.CO * CI;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // over [kh][kw][co][ci]
+  if (i >= slab) return;
+  const int ci = (int)(i % CI);
+  const int co = (int)((i / CI) % a.CO);
+  const int tap = (int)(i / ((int64_t)CI * a.CO));
+  float s = 0.f;
+  for (int sp = 0; sp < a.nsplit; ++sp) s += a.part[(int64_t)sp * slab + i];
+  a.dw[((int64_t)co * KS * KS + tap) * CI + ci] = s;
+}
+
+}  // namespace siren

@@ -1968,6 +1968,112 @@ int siren_conv_fwd_k5(const void* x, const void* w, const void* bias, int relu, 
   return check_launch("conv_fwd_k5");
 }
 
+}  // extern "C"
+namespace {
+// Native shapes of the generic encoder convolutions (siren_conv.hip conv_*_gen_kernel).
+int conv_shape_check(int kind, int N, int H, int W, int CI, int CO, int KS) {
+  if (N < 1 || H < 1) return fail(SIREN_EINVAL, "conv: empty input");
+  if (KS != 3 && KS != 5 && KS != 7) return fail(SIREN_EINVAL, "conv: filter size %d not native (3, 5, 7)", KS);
+  if (CI != 64 && CI != 128) return fail(SIREN_EINVAL, "conv: %d input channels not native (64, 128)", CI);
+  if (kind == 0) {
+    if (W != CF_W || H % 2 != 0) return fail(SIREN_EINVAL, "conv fwd: needs W = %d and H even (H = %d, W = %d)", CF_W, H, W);
+    if (CO < 64 || CO % 64 != 0) return fail(SIREN_EINVAL, "conv fwd: %d output channels (a multiple of 64)", CO);
+  } else {
+    if (W < CW_PX || W % CW_PX != 0) return fail(SIREN_EINVAL, "conv wrw: W = %d not a multiple of %d", W, CW_PX);
+    const int cow = CI == 64 ? 128 : 64;
+    if (CO % cow != 0) return fail(SIREN_EINVAL, "conv wrw: %d output channels (a multiple of %d)", CO, cow);
+  }
+  return SIREN_OK;
+}
+int conv_wrw_nsplit(int N, int H, int CI, int CO, int KS) {
+  const int64_t rows = (int64_t)N * H;
+  const int64_t blocks = (int64_t)KS * (CO / (CI == 64 ? 128 : 64));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(rows, std::max<int64_t>(1, 256 / blocks)));
+}
+}  // namespace
+extern "C" {
+
+int siren_conv_check(int kind, int N, int H, int W, int CI, int CO, int KS) {
+  return conv_shape_check(kind, N, H, W, CI, CO, KS);
+}
+
+int siren_conv_fwd(const void* x, const void* w, const void* bias, int relu, void* y, int N, int H, int W, int CI,
+                   int CO, int KS, void* stream) {
+  int rc = conv_shape_check(0, N, H, W, CI, CO, KS);
+  if (rc) return rc;
+  if (!x || !w || !y) return fail(SIREN_EINVAL, "conv fwd: null pointer");
+  ConvGArgs a;
+  memset(&a, 0, sizeof(a));
+  a.x = (const bf16*)x;
+  a.w = (const bf16*)w;
+  a.bias = (const bf16*)bias;
+  a.y = (bf16*)y;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.CO = CO;
+  a.relu = relu ? 1 : 0;
+  const bool big = KS <= 5 && CO % 128 == 0;  // 128-channel tiles (the 7x7 stages need 64 to fit in LDS)
+  const dim3 grid((unsigned)(N * (H / 2)), (unsigned)(CO / (big ? 128 : 64)));
+  hipStream_t st = (hipStream_t)stream;
+#define SIREN_CF(K, C, T) hipLaunchKernelGGL((conv_fwd_gen_kernel<K, C, T>), grid, dim3(512), 0, st, a)
+  if (KS == 3) {
+    if (CI == 64) { if (big) SIREN_CF(3, 64, 128); else SIREN_CF(3, 64, 64); }
+    else { if (big) SIREN_CF(3, 128, 128); else SIREN_CF(3, 128, 64); }
+  } else if (KS == 5) {
+    if (CI == 64) { if (big) SIREN_CF(5, 64, 128); else SIREN_CF(5, 64, 64); }
+    else { if (big) SIREN_CF(5, 128, 128); else SIREN_CF(5, 128, 64); }
+  } else {
+    if (CI == 64) SIREN_CF(7, 64, 64);
+    else SIREN_CF(7, 128, 64);
+  }
+#undef SIREN_CF
+  return check_launch("conv_fwd_gen");
+}
+
+int64_t siren_conv_wrw_ws_bytes(int N, int H, int W, int CI, int CO, int KS) {
+  if (conv_shape_check(1, N, H, W, CI, CO, KS)) return -1;
+  return (int64_t)conv_wrw_nsplit(N, H, CI, CO, KS) * KS * KS * CO * CI * 4;
+}
+
+int siren_conv_wrw(const void* x, const void* dy, int N, int H, int W, int CI, int CO, int KS, float* dw, void* ws,
+                   int64_t ws_bytes, void* stream) {
+  int rc = conv_shape_check(1, N, H, W, CI, CO, KS);
+  if (rc) return rc;
+  if (!x || !dy || !dw) return fail(SIREN_EINVAL, "conv wrw: null pointer");
+  const int nsplit = conv_wrw_nsplit(N, H, CI, CO, KS);
+  const int64_t need = (int64_t)nsplit * KS * KS * CO * CI * 4;
+  if (!ws || ws_bytes < need) return fail(SIREN_ENOSPACE, "conv wrw: workspace %lld < %lld bytes", (long long)ws_bytes, (long long)need);
+  ConvGArgs a;
+  memset(&a, 0, sizeof(a));
+  a.x = (const bf16*)x;
+  a.dy = (const bf16*)dy;
+  a.part = (float*)ws;
+  a.dw = dw;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.CO = CO;
+  a.nsplit = nsplit;
+  a.rows_per_split = cdiv((int64_t)N * H, nsplit);
+  hipStream_t st = (hipStream_t)stream;
+  const int cow = CI == 64 ? 128 : 64;
+  const dim3 grid((unsigned)nsplit, (unsigned)KS, (unsigned)(CO / cow));
+  const int64_t slab = (int64_t)KS * KS * CO * CI;
+  const dim3 rgrid((unsigned)cdiv(slab, 256));
+#define SIREN_CW(K, C, B)                                                               \
+  {                                                                                      \
+    hipLaunchKernelGGL((conv_wrw_gen_kernel<K, C, B>), grid, dim3(512), 0, st, a);        \
+    if ((rc = check_launch("conv_wrw_gen"))) return rc;                                  \
+    hipLaunchKernelGGL((conv_wrw_gen_reduce_kernel<K, C>), rgrid, dim3(256), 0, st, a);   \
+  }
+  if (KS == 3) { if (CI == 64) SIREN_CW(3, 64, 4) else SIREN_CW(3, 128, 2) }
+  else if (KS == 5) { if (CI == 64) SIREN_CW(5, 64, 4) else SIREN_CW(5, 128, 2) }
+  else { if (CI == 64) SIREN_CW(7, 64, 4) else SIREN_CW(7, 128, 2) }
+#undef SIREN_CW
+  return check_launch("conv_wrw_gen_reduce");
+}
+
 int siren_enc_relu_bwd(const void* g1, const void* g2, const void* y, void* out, float* db, int64_t P, int C, void* ws,
                        int64_t ws_bytes, void* stream) {
   EncArgs a;

@@ -66,6 +66,7 @@ def _w_flip(wb):
 
 
 _CONV_NATIVE = [True]
+_CONV_OK = {}
 
 
 def _native_conv(x, wb):
@@ -74,10 +75,24 @@ def _native_conv(x, wb):
     return _CONV_NATIVE[0] and co == ci == 128 and k == 5 and w == 128 and h % 2 == 0
 
 
+def _native_gen(kind, x, wb):
+    """Whether the generic native kernels (siren_conv_fwd / siren_conv_wrw: 3x3 / 5x5 / 7x7, 64 or
+    128 input channels) take this shape (kind 0 forward, 1 weight gradient)."""
+    co, ci, k, _ = wb.shape
+    n, _, h, w = x.shape
+    key = (kind, n, h, w, ci, co, k)
+    hit = _CONV_OK.get(key)
+    if hit is None:
+        hit = _CONV_OK[key] = _native.lib().siren_conv_check(kind, n, h, w, ci, co, k) == 0
+    return _CONV_NATIVE[0] and hit
+
+
 def _conv(x, wb, bb, pad, relu=False):
-    """Stride-1 'same' convolution, bf16 NHWC out: the native MFMA kernel for the residual blocks'
-    128 -> 128 5x5 shape (siren_conv_fwd_k5, bias + ReLU in its epilogue), MIOpen otherwise
-    (relu=True needs a bias on that path and is applied by siren_enc_bias_relu)."""
+    """Stride-1 'same' convolution, bf16 NHWC out: the native MFMA kernels — the residual blocks'
+    128 -> 128 5x5 shape (siren_conv_fwd_k5), the other 3x3 / 5x5 / 7x7 shapes with 64 or 128
+    input channels (siren_conv_fwd: cnn[0] and its input gradient), bias + ReLU in their epilogue —
+    and MIOpen for the rest (conv_theta's 2 input channels, other widths; relu=True needs a bias on
+    that path and is applied by siren_enc_bias_relu)."""
     if _native_conv(x, wb):
         n, _, h, w = x.shape
         y = torch.empty((n, wb.shape[0], h, w), dtype=torch.bfloat16, device=x.device, memory_format=_CL)
@@ -85,6 +100,14 @@ def _conv(x, wb, bb, pad, relu=False):
                                                       bb.data_ptr() if bb is not None else None, 1 if relu else 0,
                                                       y.data_ptr(), n, h, w, wb.shape[1],
                                                       _native.stream_handle(x.device)), "siren_conv_fwd_k5")
+        return y
+    if _native_gen(0, x, wb):
+        n, ci, h, w = x.shape
+        co, k = wb.shape[0], wb.shape[2]
+        y = torch.empty((n, co, h, w), dtype=torch.bfloat16, device=x.device, memory_format=_CL)
+        _native.check(_native.lib().siren_conv_fwd(x.data_ptr(), wb.data_ptr(), bb.data_ptr() if bb is not None else None,
+                                                   1 if relu else 0, y.data_ptr(), n, h, w, ci, co, k,
+                                                   _native.stream_handle(x.device)), "siren_conv_fwd")
         return y
     y = F.conv2d(x, wb, None if relu else bb, padding=pad).contiguous(memory_format=_CL)
     if relu:
@@ -98,9 +121,10 @@ _WGRAD_NATIVE = [True]
 
 
 def _wgrad(g, x, wb, pad):
-    """dL/dW of a stride-1 'same' convolution: the native MFMA kernel for the residual blocks'
-    128 -> 128 5x5 shape (siren_conv_wrw_k5, fp32 out in the filter's channels-last layout),
-    MIOpen's weight-gradient convolution otherwise."""
+    """dL/dW of a stride-1 'same' convolution: the native MFMA kernels for the residual blocks'
+    128 -> 128 5x5 shape (siren_conv_wrw_k5) and the other 3x3 / 5x5 / 7x7 shapes with 64 or 128
+    input channels (siren_conv_wrw), fp32 out in the filter's channels-last layout; MIOpen's
+    weight-gradient convolution otherwise."""
     co, ci, k, _ = wb.shape
     n, _, h, w = x.shape
     if _WGRAD_NATIVE[0] and co == ci == 128 and k == 5 and w % 64 == 0:
@@ -109,6 +133,13 @@ def _wgrad(g, x, wb, pad):
         ws = torch.empty(int(lib.siren_conv_wrw_workspace_bytes(n, h, w)), dtype=torch.uint8, device=x.device)
         _native.check(lib.siren_conv_wrw_k5(x.data_ptr(), g.data_ptr(), n, h, w, ci, dw.data_ptr(), ws.data_ptr(),
                                             ws.numel(), _native.stream_handle(x.device)), "siren_conv_wrw_k5")
+        return dw
+    if _WGRAD_NATIVE[0] and _native_gen(1, x, wb):
+        lib = _native.lib()
+        dw = torch.empty(wb.shape, dtype=torch.float32, device=x.device, memory_format=_CL)
+        ws = torch.empty(int(lib.siren_conv_wrw_ws_bytes(n, h, w, ci, co, k)), dtype=torch.uint8, device=x.device)
+        _native.check(lib.siren_conv_wrw(x.data_ptr(), g.data_ptr(), n, h, w, ci, co, k, dw.data_ptr(), ws.data_ptr(),
+                                         ws.numel(), _native.stream_handle(x.device)), "siren_conv_wrw")
         return dw
     return torch.ops.aten.convolution_backward(g, x, wb, None, [1, 1], [pad, pad], [1, 1], False, [0, 0], 1,
                                                [False, True, False])[1]

@@ -5,7 +5,9 @@ modules.py:340-380 / 433-450), and its native passes (siren_encoder.hip) against
 Tolerances: on MIOpen's convolutions the node's forward has the autocast chain's roundings, so the
 embedding agrees to fp32 summation order (1e-5); with the native 5x5 kernels (another summation
 order inside each convolution) to the bf16 level (3e-3); parameter gradients agree to the bf16
-level (2e-2 norm-relative); against fp32 no further off than the autocast chain.
+level (2e-2 norm-relative; 3e-2 with every 64/128-channel convolution native, cnn[0] and its input
+gradient included: two bf16 paths each ~1-2 % from fp32, measured 2.1e-2 on a residual block's
+weight); against fp32 no further off than the autocast chain (test_fused_node_against_fp32_encoder).
 """
 import pytest
 import torch
@@ -56,7 +58,7 @@ def test_fused_node_matches_autocast_chain(blocks, hidden, k, native_conv):
     assert orc.norm_rel(e_f.cpu(), e_c.cpu()) < (3e-3 if native_conv else 1e-5)
     assert g_f.keys() == g_c.keys()
     for n in g_f:
-        assert orc.norm_rel(g_f[n].cpu(), g_c[n].cpu()) < 2e-2, n
+        assert orc.norm_rel(g_f[n].cpu(), g_c[n].cpu()) < (3e-2 if native_conv else 2e-2), n
 
 
 def test_fused_node_against_fp32_encoder():
@@ -245,3 +247,75 @@ def test_conv_forward_kernel_against_fp32(bias, relu):
     # fp32 sums in another order: at most one bf16 rounding step apart
     assert orc.norm_rel(outs[0].float().cpu(), ref.float()) < 4e-3
     assert (d.abs() <= ref.float().abs() * 2 ** -7 + 1e-6).float().mean() > 0.999
+
+
+@pytest.mark.parametrize("k,ci,co", [(7, 64, 128), (7, 128, 64), (3, 64, 128), (3, 128, 128), (5, 64, 64),
+                                     (5, 128, 128)])
+@pytest.mark.parametrize("bias,relu", [(False, False), (True, True)])
+def test_generic_conv_forward_kernel_against_fp32(k, ci, co, bias, relu):
+    """siren_conv_fwd (round 5: the encoder's other shapes — cnn[0]'s 64 -> 128 7x7, its input
+    gradient 128 -> 64, the 3x3 forms) against the fp64 convolution of the same bf16 operands
+    (then the conv + bias-add chain's bf16 roundings), bit-equal on a rerun."""
+    from siren_mri_amd import _native
+    import torch.nn.functional as F
+    lib = _native.lib()
+    N, H = 2, 6
+    assert lib.siren_conv_check(0, N, H, 128, ci, co, k) == 0, _native.last_error()
+    g = torch.Generator().manual_seed(k * 1000 + ci + co + bias)
+    x = torch.randn(N, ci, H, 128, generator=g).to(torch.bfloat16)
+    w = (torch.randn(co, ci, k, k, generator=g) / (ci * k)).to(torch.bfloat16)
+    b = torch.randn(co, generator=g).to(torch.bfloat16)
+    ref = F.conv2d(x.double(), w.double(), padding=k // 2).to(torch.bfloat16)
+    if bias:
+        ref = ref + b.view(1, -1, 1, 1)
+        if relu:
+            ref = torch.relu(ref)
+    xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
+    wd = w.to(DEV).contiguous(memory_format=torch.channels_last)
+    bd = b.to(DEV)
+    outs = []
+    for _ in range(2):
+        y = torch.empty(N, co, H, 128, dtype=torch.bfloat16, device=DEV).contiguous(memory_format=torch.channels_last)
+        _native.check(lib.siren_conv_fwd(xd.data_ptr(), wd.data_ptr(), bd.data_ptr() if bias else None, int(relu),
+                                         y.data_ptr(), N, H, 128, ci, co, k, _native.stream_handle(DEV)), "conv_fwd")
+        outs.append(y)
+    assert torch.equal(outs[0], outs[1])
+    d = (outs[0].float().cpu() - ref.float())
+    assert orc.norm_rel(outs[0].float().cpu(), ref.float()) < 4e-3
+    assert (d.abs() <= ref.float().abs() * 2 ** -7 + 1e-6).float().mean() > 0.999
+
+
+@pytest.mark.parametrize("k,ci,co", [(7, 64, 128), (3, 128, 64), (5, 64, 128)])
+@pytest.mark.parametrize("N,H,W", [(2, 128, 128), (3, 7, 64)])
+def test_generic_conv_weight_gradient_kernel_against_fp32(k, ci, co, N, H, W):
+    """siren_conv_wrw against the fp64 weight gradient of the same bf16 operands, bit-equal on a rerun."""
+    from siren_mri_amd import _native
+    lib = _native.lib()
+    assert lib.siren_conv_check(1, N, H, W, ci, co, k) == 0, _native.last_error()
+    g = torch.Generator().manual_seed(N * 1000 + H + W + k + ci)
+    x = torch.randn(N, ci, H, W, generator=g).to(torch.bfloat16)
+    dy = torch.randn(N, co, H, W, generator=g).to(torch.bfloat16)
+    ref = torch.nn.grad.conv2d_weight(x.double(), (co, ci, k, k), dy.double(), padding=k // 2).float()
+    xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
+    dyd = dy.to(DEV).contiguous(memory_format=torch.channels_last)
+    ws = torch.empty(int(lib.siren_conv_wrw_ws_bytes(N, H, W, ci, co, k)), dtype=torch.uint8, device=DEV)
+    outs = []
+    for _ in range(2):
+        dw = torch.empty(co, ci, k, k, device=DEV).contiguous(memory_format=torch.channels_last)
+        _native.check(lib.siren_conv_wrw(xd.data_ptr(), dyd.data_ptr(), N, H, W, ci, co, k, dw.data_ptr(), ws.data_ptr(),
+                                         ws.numel(), _native.stream_handle(DEV)), "conv_wrw")
+        outs.append(dw)
+    assert torch.equal(outs[0], outs[1])
+    assert orc.norm_rel(outs[0].cpu(), ref) < 1e-6
+
+
+def test_c4_encoder_has_no_miopen_cnn0():
+    """Configs 4/5's encoder (kernel_size 7): cnn[0] and its gradients run on the native kernels —
+    only conv_theta (2 input channels) still takes MIOpen's."""
+    from siren_mri_amd import encoder
+    enc = _encoder("bf16", blocks=1, hidden=128, k=7)
+    x = torch.empty(2, 64, 128, 128, dtype=torch.bfloat16, device=DEV).contiguous(memory_format=torch.channels_last)
+    wb = encoder._w_bf16(enc.cnn[0].weight)
+    assert encoder._native_gen(0, x, wb) and encoder._native_gen(1, x, wb)
+    g = torch.empty(2, 128, 128, 128, dtype=torch.bfloat16, device=DEV).contiguous(memory_format=torch.channels_last)
+    assert encoder._native_gen(0, g, encoder._w_flip(wb))
