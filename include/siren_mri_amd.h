@@ -293,12 +293,14 @@ int siren_conv_wrw_k5(const void* x, const void* dy, int N, int H, int W, int C,
 /* The encoder's other convolution shapes (round 5; ConvImgEncoder's cnn[0], modules.py:351 — 64 ->
  * 128 channels, 7x7 in configs 4/5 — its input gradient as a forward convolution of the flipped,
  * transposed filter, and the 3x3 forms), stride 1, 'same' padding, bf16 NHWC, fp32 accumulation:
- * filter size KS in {3, 5, 7}, CI in {64, 128} input channels.
- *   siren_conv_fwd : y = conv(x, w) (+ bias, ReLU as siren_conv_fwd_k5); W = 128, H even, CO a
- *                    multiple of 64; w is [CO][KS][KS][CI].
- *   siren_conv_wrw : dw[CO][KS][KS][CI] (fp32) = the weight gradient of that convolution; W a
- *                    multiple of 64, CO a multiple of 128 (CI 64) or 64 (CI 128); split-K partials
- *                    in ws (siren_conv_wrw_ws_bytes) added in split order (deterministic).
+ * filter size KS in {3, 5, 7}, CI in {2, 64, 128} input channels (2: conv_theta over the real /
+ * imaginary k-space image, modules.py:359).
+ *   siren_conv_fwd : y = conv(x, w) (+ bias, ReLU as siren_conv_fwd_k5); W = 128; CI 64/128: H
+ *                    even, CO a multiple of 64; CI 2: CO in {32, 64, 96, 128}; w is [CO][KS][KS][CI].
+ *   siren_conv_wrw : dw[CO][KS][KS][CI] (fp32) = the weight gradient of that convolution; CI 64/128:
+ *                    W a multiple of 64, CO a multiple of 128 (CI 64) or 64 (CI 128); CI 2: W a
+ *                    multiple of 64, CO in {32, 64, 96, 128}; split-K partials in ws
+ *                    (siren_conv_wrw_ws_bytes) added in split order (deterministic).
  *   siren_conv_check: SIREN_OK when the shape (kind 0 forward, 1 weight gradient) runs natively;
  *                    the encoder falls back to MIOpen otherwise. */
 int siren_conv_check(int kind, int N, int H, int W, int CI, int CO, int KS);

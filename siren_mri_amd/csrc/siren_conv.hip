@@ -771,3 +771,283 @@ __global__ __launch_bounds__(256) void conv_wrw_gen_reduce_kernel(ConvGArgs a) {
 }
 
 }  // namespace siren
+
+namespace siren {
+
+// ------------------------------------------------------------------------------------------
+// conv_theta: ConvImgEncoder's first convolution (modules.py:359) over the 2-channel k-space image
+// (real, imaginary): CI = 2, a KS x KS filter (3, 5, 7), CO a multiple of 32 up to 128. The
+// reduction per output is only 2 KS^2 <= 98 long, so the GEMM is laid out per filter row: one
+// 32x32x16 MFMA per (kh, 32 outputs, 32 channels) whose 16 K slots are the row's (kw, ci) pairs —
+// 2 KS consecutive bf16 of the NHWC input row, zero-weighted past 2 KS. The output (64 channels,
+// 67 MB per C4 step) is the traffic that bounds the forward; the weight gradient reads dy once.
+// ------------------------------------------------------------------------------------------
+struct ConvTArgs {
+  const bf16* x;      // [N][H][W][2]
+  const bf16* w;      // forward: [CO][KS][KS][2]
+  const bf16* bias;   // [CO] or null
+  bf16* y;            // forward: [N][H][W][CO]
+  const bf16* dy;     // weight gradient: [N][H][W][CO]
+  float* part;        // weight gradient: [nsplit][CO][32 NNT] (column kh * 16 + 2 kw + ci)
+  float* dw;          // weight gradient: [CO][KS][KS][2]
+  int N, H, W, CO;
+  int relu;
+  int rows_per_block;      // forward: image rows per workgroup
+  int64_t chunks_per_split;  // weight gradient: 32-pixel chunks per split
+  int nsplit;
+};
+
+constexpr int CT_W = 128;   // forward: image width (4 waves x 32 pixels)
+constexpr int CT_RPB = 4;   // forward: image rows per workgroup
+
+template <int KS, int NCT>
+__global__ __launch_bounds__(256) void conv_t_fwd_kernel(ConvTArgs a) {
+  constexpr int PAD = KS / 2, CO = 32 * NCT, OROW = CO * 2 + 16;
+  static_assert(KS % 2 == 1 && KS <= 7 && NCT >= 1 && NCT <= 4, "conv_theta shape");
+  __shared__ __attribute__((aligned(16))) char ot[CT_W * OROW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hf = lane >> 5;
+  const int px = 32 * wave + l32;
+  const int H = a.H;
+  const int64_t nrows = (int64_t)a.N * H;
+  const int64_t r0 = (int64_t)blockIdx.x * a.rows_per_block;
+  const int64_t r1 = r0 + a.rows_per_block < nrows ? r0 + a.rows_per_block : nrows;
+
+  // A operands (filter rows): lane -> out channel 32 ct + l32, K slots 8 hf .. 8 hf + 7 = (kw, ci)
+  bf16x8 af[KS][NCT];
+#pragma unroll
+  for (int kh = 0; kh < KS; ++kh)
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int kw = 4 * hf + (j >> 1), ci = j & 1;
+        af[kh][ct][j] = kw < KS ? a.w[(((32 * ct + l32) * KS + kh) * KS + kw) * 2 + ci] : (bf16)0.f;
+      }
+  const uint32_t* xw = (const uint32_t*)a.x;  // one 32-bit word = one pixel's two channels
+
+  for (int64_t r = r0; r < r1; ++r) {
+    const int n = (int)(r / H), h = (int)(r % H);
+    // B operands: lane -> pixel px, K slots (kw = 4 hf + q, ci): 4 words per filter row
+    u32x4_t xv[KS];
+#pragma unroll
+    for (int kh = 0; kh < KS; ++kh) {
+      const int xr = h + kh - PAD;
+      const bool rok = xr >= 0 && xr < H;
+      const int64_t rb = ((int64_t)n * H + (rok ? xr : 0)) * a.W;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int kw = 4 * hf + q, p = px + kw - PAD;
+        xv[kh][q] = (rok && kw < KS && p >= 0 && p < a.W) ? xw[rb + p] : 0u;
+      }
+    }
+    f32x16 acc[NCT];
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[ct][e] = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < KS; ++kh) {
+      const bf16x8 bv = __builtin_bit_cast(bf16x8, xv[kh]);
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kh][ct], bv, acc[ct], 0, 0, 0);
+    }
+    // D[co][px] -> LDS tile [128 px][CO] (bias, ReLU: the conv + bias-add + ReLU chain's roundings)
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int co = 32 * ct + 8 * g + 4 * hf + e;
+          float z = (float)(bf16)acc[ct][4 * g + e];
+          if (a.bias) {
+            z = (float)(bf16)(z + (float)a.bias[co]);
+            if (a.relu) z = fmaxf(z, 0.f);
+          }
+          v[e] = (bf16)z;
+        }
+        *(bf16x4*)(ot + px * OROW + (32 * ct + 8 * g + 4 * hf) * 2) = v;
+      }
+    __syncthreads();
+    // the row's CT_W x CO outputs as 16-byte buffer stores, each with its 2 wait states
+    // (siren_common.h store_b128_ws2)
+    constexpr int PPR = CO / 8;  // 16-byte pieces per pixel
+    const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.y + r * (int64_t)CT_W * CO, CT_W * CO * 2);
+#pragma unroll
+    for (int k = 0; k < CT_W * PPR / 256; ++k) {
+      const int q = tid + 256 * k;
+      const int p = q / PPR, pc = q % PPR;
+      store_b128_ws2(*(const u32x4_t*)(ot + p * OROW + 16 * pc), ry, (uint32_t)(q * 16), 0);
+    }
+    __syncthreads();
+  }
+}
+
+// Weight gradient: D[co][kh 16 + 2 kw + ci] = sum over pixels of dy[px][co] x[px + (kh, kw)][ci].
+// Per 64-pixel chunk of an image row: an LDS dy tile [64 px][CO], the chunk's KS input rows
+// (64 + KS - 1 pixels each, staged as they come from HBM), and from those an im2col tile
+// [64 px][32 NNT] (the KS rows' (kw, ci) pairs, zero past each row's 2 KS slots); both tiles are
+// read by transposing fragment reads (pixels = K). Each chunk's dy and input words are loaded
+// into registers two chunks ahead of its expansion and multiply (~48 KB in flight per CU at 3
+// workgroups). 4 waves, the (CO / 32) x NNT output tiles dealt round-robin; one partial slab per split, reduced in split order by
+// conv_t_wrw_reduce_kernel.
+constexpr int CT_PX = 64;  // weight gradient: pixels per chunk
+template <int KS, int NCT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NCT == 4 ? 2 : 3))) void conv_t_wrw_kernel(ConvTArgs a) {
+  constexpr int PAD = KS / 2, CO = 32 * NCT;
+  constexpr int NNT = (KS * 16 + 31) / 32, NCOL = 32 * NNT;
+  constexpr int NTILE = NCT * NNT, TPW = (NTILE + 3) / 4;
+  constexpr int DROW = CO + 16, XROW = NCOL + 16;  // bf16 per LDS row (+32-byte pad)
+  constexpr int XW = CT_PX + KS - 1;              // input pixels per staged row
+  constexpr int NDY = CT_PX * CO / 8 / 256;       // 16-byte dy pieces per thread
+  constexpr int NXV = (KS * XW + 255) / 256;      // input words per thread
+  static_assert(CT_PX * CO / 8 % 256 == 0, "dy pieces");
+  __shared__ __attribute__((aligned(16))) bf16 sD[CT_PX * DROW];
+  __shared__ __attribute__((aligned(16))) bf16 sX[CT_PX * XROW];
+  __shared__ uint32_t sR[KS * XW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int split = blockIdx.x;
+  const int nch = a.W / CT_PX;
+  const int64_t nchunk = (int64_t)a.N * a.H * nch;
+  const int64_t c0 = (int64_t)split * a.chunks_per_split;
+  const int64_t c1 = c0 + a.chunks_per_split < nchunk ? c0 + a.chunks_per_split : nchunk;
+
+  // the im2col tile's zero columns (past 2 KS in each row's 16, and rows kh >= KS) are never
+  // rewritten: clear the whole tile once
+  for (int i = tid; i < CT_PX * XROW / 2; i += 256) ((uint32_t*)sX)[i] = 0u;
+
+  f32x16 acc[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+
+  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  const int r8 = 8 * (g >> 1) + tq, cc = 16 * (g & 1) + 4 * tp;
+  const uint32_t dl = lds_addr(sD) + (uint32_t)((r8 * DROW + cc) * 2);
+  const uint32_t xl = lds_addr(sX) + (uint32_t)((r8 * XROW + cc) * 2);
+  const uint32_t* xw = (const uint32_t*)a.x;
+
+  // two chunks' loads in flight ahead of the one being multiplied (register sets 0 / 1)
+  u32x4_t dyv[2][NDY];
+  uint32_t xv[2][NXV];
+  auto load = [&](int64_t c, auto set_c) {
+    constexpr int set = decltype(set_c)::value;
+    const int64_t r = c / nch;
+    const int px0 = (int)(c % nch) * CT_PX;
+    const int n = (int)(r / a.H), h = (int)(r % a.H);
+#pragma unroll
+    for (int i = 0; i < NDY; ++i) {
+      const int q = tid + 256 * i;
+      const int p = q / (CO / 8), pc = q % (CO / 8);
+      dyv[set][i] = *(const u32x4_t*)(a.dy + (r * a.W + px0 + p) * CO + 8 * pc);
+    }
+#pragma unroll
+    for (int i = 0; i < NXV; ++i) {
+      const int q = tid + 256 * i;
+      const int kh = q / XW, j = q % XW;
+      const int xr = h + kh - PAD, xp = px0 + j - PAD;
+      xv[set][i] = (q < KS * XW && xr >= 0 && xr < a.H && xp >= 0 && xp < a.W) ? xw[((int64_t)n * a.H + xr) * a.W + xp]
+                                                                                 : 0u;
+    }
+  };
+  auto body = [&](int64_t c, auto set_c) {
+    constexpr int set = decltype(set_c)::value;
+    __syncthreads();  // the previous chunk's fragment reads and expansion are done
+#pragma unroll
+    for (int i = 0; i < NDY; ++i) {
+      const int q = tid + 256 * i;
+      *(u32x4_t*)(sD + (q / (CO / 8)) * DROW + 8 * (q % (CO / 8))) = dyv[set][i];
+    }
+#pragma unroll
+    for (int i = 0; i < NXV; ++i) {
+      const int q = tid + 256 * i;
+      if (q < KS * XW) sR[q] = xv[set][i];
+    }
+    if (c + 2 < c1) load(c + 2, set_c);
+    __syncthreads();
+    // im2col: pixel p, filter row kh, tap kw -> one 32-bit word (both channels)
+    for (int q = tid; q < CT_PX * KS * KS; q += 256) {
+      const int p = q % CT_PX, t = q / CT_PX, kw = t % KS, kh = t / KS;
+      *(uint32_t*)(sX + p * XROW + kh * 16 + 2 * kw) = sR[kh * XW + p + kw];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < CT_PX / 16; ++ks) {
+      TrFrag fa[TPW], fb[TPW];
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) {
+        const int t = wave + 4 * i;
+        const int ct = t < NTILE ? t / NNT : 0, nt = t < NTILE ? t % NNT : 0;
+        const uint32_t da = dl + (uint32_t)((16 * ks * DROW + 32 * ct) * 2);
+        const uint32_t xa = xl + (uint32_t)((16 * ks * XROW + 32 * nt) * 2);
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(fa[i].lo) : "v"(da));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(fa[i].hi) : "v"(da), "n"(4 * DROW * 2));
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(fb[i].lo) : "v"(xa));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(fb[i].hi) : "v"(xa), "n"(4 * XROW * 2));
+      }
+      lgkm_wait<0>();
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) {
+        tie(fa[i]);
+        tie(fb[i]);
+        if (wave + 4 * i < NTILE)
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr16_value(fa[i]), tr16_value(fb[i]), acc[i], 0, 0, 0);
+      }
+    }
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  if (c0 < c1) load(c0, S0{});
+  if (c0 + 1 < c1) load(c0 + 1, S1{});
+  for (int64_t c = c0; c < c1; c += 2) {
+    body(c, S0{});
+    if (c + 1 < c1) body(c + 1, S1{});
+  }
+
+  float* P = a.part + (int64_t)split * CO * NCOL;
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int t = wave + 4 * i;
+    if (t >= NTILE) continue;
+    const int ct = t / NNT, nt = t % NNT;
+    const int col = 32 * nt + (lane & 31);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int co = 32 * ct + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+      P[(int64_t)co * NCOL + col] = acc[i][e];
+    }
+  }
+}
+
+// dw[co][kh][kw][ci] = sum over splits of part[s][co][kh 16 + 2 kw + ci]: 16 outputs per
+// workgroup, 16 split groups (s = g mod 16) summed in order, then the groups in order
+template <int KS>
+__global__ __launch_bounds__(256) void conv_t_wrw_reduce_kernel(ConvTArgs a) {
+  constexpr int NCOL = 32 * ((KS * 16 + 31) / 32);
+  __shared__ float red[16][17];
+  const int o = threadIdx.x & 15, gs = threadIdx.x >> 4;
+  const int64_t i = (int64_t)blockIdx.x * 16 + o;  // over [co][kh][kw][ci]
+  const int64_t total = (int64_t)a.CO * KS * KS * 2;
+  float s = 0.f;
+  int64_t src = 0;
+  if (i < total) {
+    const int ci = (int)(i & 1), kw = (int)((i >> 1) % KS), kh = (int)((i / (2 * KS)) % KS), co = (int)(i / (2 * KS * KS));
+    src = (int64_t)co * NCOL + kh * 16 + 2 * kw + ci;
+    const int64_t slab = (int64_t)a.CO * NCOL;
+    for (int sp = gs; sp < a.nsplit; sp += 16) s += a.part[sp * slab + src];
+  }
+  red[gs][o] = s;
+  __syncthreads();
+  if (gs == 0 && i < total) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][o];
+    a.dw[i] = t;
+  }
+}
+
+}  // namespace siren
+

@@ -1974,7 +1974,13 @@ namespace {
 int conv_shape_check(int kind, int N, int H, int W, int CI, int CO, int KS) {
   if (N < 1 || H < 1) return fail(SIREN_EINVAL, "conv: empty input");
   if (KS != 3 && KS != 5 && KS != 7) return fail(SIREN_EINVAL, "conv: filter size %d not native (3, 5, 7)", KS);
-  if (CI != 64 && CI != 128) return fail(SIREN_EINVAL, "conv: %d input channels not native (64, 128)", CI);
+  if (CI == 2) {  // conv_theta (conv_t_fwd_kernel / conv_t_wrw_kernel)
+    if (CO < 32 || CO > 128 || CO % 32 != 0) return fail(SIREN_EINVAL, "conv (2 channels): %d output channels (32, 64, 96, 128)", CO);
+    if (kind == 0 && W != CT_W) return fail(SIREN_EINVAL, "conv fwd (2 channels): needs W = %d (W = %d)", CT_W, W);
+    if (kind != 0 && (W < CT_PX || W % CT_PX != 0)) return fail(SIREN_EINVAL, "conv wrw (2 channels): W = %d not a multiple of %d", W, CT_PX);
+    return SIREN_OK;
+  }
+  if (CI != 64 && CI != 128) return fail(SIREN_EINVAL, "conv: %d input channels not native (2, 64, 128)", CI);
   if (kind == 0) {
     if (W != CF_W || H % 2 != 0) return fail(SIREN_EINVAL, "conv fwd: needs W = %d and H even (H = %d, W = %d)", CF_W, H, W);
     if (CO < 64 || CO % 64 != 0) return fail(SIREN_EINVAL, "conv fwd: %d output channels (a multiple of 64)", CO);
@@ -1985,6 +1991,12 @@ int conv_shape_check(int kind, int N, int H, int W, int CI, int CO, int KS) {
   }
   return SIREN_OK;
 }
+// conv_theta weight gradient: splits of 64-pixel chunks (one workgroup each, ~3 per CU) and the
+// partial slab of one split ([CO][32 NNT] floats)
+int conv_t_nsplit(int N, int H, int W) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>(768, (int64_t)N * H * (W / CT_PX)));
+}
+int64_t conv_t_slab(int CO, int KS) { return (int64_t)CO * 32 * ((KS * 16 + 31) / 32); }
 int conv_wrw_nsplit(int N, int H, int CI, int CO, int KS) {
   const int64_t rows = (int64_t)N * H;
   const int64_t blocks = (int64_t)KS * (CO / (CI == 64 ? 128 : 64));
@@ -2013,9 +2025,36 @@ int siren_conv_fwd(const void* x, const void* w, const void* bias, int relu, voi
   a.W = W;
   a.CO = CO;
   a.relu = relu ? 1 : 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (CI == 2) {
+    ConvTArgs t;
+    memset(&t, 0, sizeof(t));
+    t.x = a.x;
+    t.w = a.w;
+    t.bias = a.bias;
+    t.y = a.y;
+    t.N = N;
+    t.H = H;
+    t.W = W;
+    t.CO = CO;
+    t.relu = a.relu;
+    t.rows_per_block = CT_RPB;
+    const dim3 tg((unsigned)cdiv((int64_t)N * H, CT_RPB));
+#define SIREN_CT(K)                                                                              \
+  switch (CO / 32) {                                                                             \
+    case 1: hipLaunchKernelGGL((conv_t_fwd_kernel<K, 1>), tg, dim3(256), 0, st, t); break;      \
+    case 2: hipLaunchKernelGGL((conv_t_fwd_kernel<K, 2>), tg, dim3(256), 0, st, t); break;      \
+    case 3: hipLaunchKernelGGL((conv_t_fwd_kernel<K, 3>), tg, dim3(256), 0, st, t); break;      \
+    default: hipLaunchKernelGGL((conv_t_fwd_kernel<K, 4>), tg, dim3(256), 0, st, t); break;     \
+  }
+    if (KS == 3) { SIREN_CT(3) }
+    else if (KS == 5) { SIREN_CT(5) }
+    else { SIREN_CT(7) }
+#undef SIREN_CT
+    return check_launch("conv_t_fwd");
+  }
   const bool big = KS <= 5 && CO % 128 == 0;  // 128-channel tiles (the 7x7 stages need 64 to fit in LDS)
   const dim3 grid((unsigned)(N * (H / 2)), (unsigned)(CO / (big ? 128 : 64)));
-  hipStream_t st = (hipStream_t)stream;
 #define SIREN_CF(K, C, T) hipLaunchKernelGGL((conv_fwd_gen_kernel<K, C, T>), grid, dim3(512), 0, st, a)
   if (KS == 3) {
     if (CI == 64) { if (big) SIREN_CF(3, 64, 128); else SIREN_CF(3, 64, 64); }
@@ -2033,6 +2072,7 @@ int siren_conv_fwd(const void* x, const void* w, const void* bias, int relu, voi
 
 int64_t siren_conv_wrw_ws_bytes(int N, int H, int W, int CI, int CO, int KS) {
   if (conv_shape_check(1, N, H, W, CI, CO, KS)) return -1;
+  if (CI == 2) return (int64_t)conv_t_nsplit(N, H, W) * conv_t_slab(CO, KS) * 4;
   return (int64_t)conv_wrw_nsplit(N, H, CI, CO, KS) * KS * KS * CO * CI * 4;
 }
 
@@ -2041,6 +2081,41 @@ int siren_conv_wrw(const void* x, const void* dy, int N, int H, int W, int CI, i
   int rc = conv_shape_check(1, N, H, W, CI, CO, KS);
   if (rc) return rc;
   if (!x || !dy || !dw) return fail(SIREN_EINVAL, "conv wrw: null pointer");
+  if (CI == 2) {
+    const int ns = conv_t_nsplit(N, H, W);
+    const int64_t need = (int64_t)ns * conv_t_slab(CO, KS) * 4;
+    if (!ws || ws_bytes < need) return fail(SIREN_ENOSPACE, "conv wrw: workspace %lld < %lld bytes", (long long)ws_bytes, (long long)need);
+    ConvTArgs t;
+    memset(&t, 0, sizeof(t));
+    t.x = (const bf16*)x;
+    t.dy = (const bf16*)dy;
+    t.part = (float*)ws;
+    t.dw = dw;
+    t.N = N;
+    t.H = H;
+    t.W = W;
+    t.CO = CO;
+    t.nsplit = ns;
+    t.chunks_per_split = cdiv((int64_t)N * H * (W / CT_PX), ns);
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 rg((unsigned)cdiv((int64_t)CO * KS * KS * 2, 16));
+#define SIREN_CTW(K)                                                                               \
+  {                                                                                                \
+    switch (CO / 32) {                                                                             \
+      case 1: hipLaunchKernelGGL((conv_t_wrw_kernel<K, 1>), dim3(ns), dim3(256), 0, st, t); break; \
+      case 2: hipLaunchKernelGGL((conv_t_wrw_kernel<K, 2>), dim3(ns), dim3(256), 0, st, t); break; \
+      case 3: hipLaunchKernelGGL((conv_t_wrw_kernel<K, 3>), dim3(ns), dim3(256), 0, st, t); break; \
+      default: hipLaunchKernelGGL((conv_t_wrw_kernel<K, 4>), dim3(ns), dim3(256), 0, st, t); break; \
+    }                                                                                              \
+    if ((rc = check_launch("conv_t_wrw"))) return rc;                                              \
+    hipLaunchKernelGGL((conv_t_wrw_reduce_kernel<K>), rg, dim3(256), 0, st, t);                    \
+  }
+    if (KS == 3) SIREN_CTW(3)
+    else if (KS == 5) SIREN_CTW(5)
+    else SIREN_CTW(7)
+#undef SIREN_CTW
+    return check_launch("conv_t_wrw_reduce");
+  }
   const int nsplit = conv_wrw_nsplit(N, H, CI, CO, KS);
   const int64_t need = (int64_t)nsplit * KS * KS * CO * CI * 4;
   if (!ws || ws_bytes < need) return fail(SIREN_ENOSPACE, "conv wrw: workspace %lld < %lld bytes", (long long)ws_bytes, (long long)need);

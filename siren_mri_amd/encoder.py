@@ -76,8 +76,8 @@ def _native_conv(x, wb):
 
 
 def _native_gen(kind, x, wb):
-    """Whether the generic native kernels (siren_conv_fwd / siren_conv_wrw: 3x3 / 5x5 / 7x7, 64 or
-    128 input channels) take this shape (kind 0 forward, 1 weight gradient)."""
+    """Whether the generic native kernels (siren_conv_fwd / siren_conv_wrw: 3x3 / 5x5 / 7x7, 2, 64
+    or 128 input channels) take this shape (kind 0 forward, 1 weight gradient)."""
     co, ci, k, _ = wb.shape
     n, _, h, w = x.shape
     key = (kind, n, h, w, ci, co, k)
@@ -89,10 +89,10 @@ def _native_gen(kind, x, wb):
 
 def _conv(x, wb, bb, pad, relu=False):
     """Stride-1 'same' convolution, bf16 NHWC out: the native MFMA kernels — the residual blocks'
-    128 -> 128 5x5 shape (siren_conv_fwd_k5), the other 3x3 / 5x5 / 7x7 shapes with 64 or 128
-    input channels (siren_conv_fwd: cnn[0] and its input gradient), bias + ReLU in their epilogue —
-    and MIOpen for the rest (conv_theta's 2 input channels, other widths; relu=True needs a bias on
-    that path and is applied by siren_enc_bias_relu)."""
+    128 -> 128 5x5 shape (siren_conv_fwd_k5), the other 3x3 / 5x5 / 7x7 shapes with 2, 64 or 128
+    input channels (siren_conv_fwd: conv_theta, cnn[0] and its input gradient), bias + ReLU in
+    their epilogue — and MIOpen for the rest (the 1x1, other widths; relu=True needs a bias on that
+    path and is applied by siren_enc_bias_relu)."""
     if _native_conv(x, wb):
         n, _, h, w = x.shape
         y = torch.empty((n, wb.shape[0], h, w), dtype=torch.bfloat16, device=x.device, memory_format=_CL)
@@ -122,9 +122,9 @@ _WGRAD_NATIVE = [True]
 
 def _wgrad(g, x, wb, pad):
     """dL/dW of a stride-1 'same' convolution: the native MFMA kernels for the residual blocks'
-    128 -> 128 5x5 shape (siren_conv_wrw_k5) and the other 3x3 / 5x5 / 7x7 shapes with 64 or 128
-    input channels (siren_conv_wrw), fp32 out in the filter's channels-last layout; MIOpen's
-    weight-gradient convolution otherwise."""
+    128 -> 128 5x5 shape (siren_conv_wrw_k5) and the other 3x3 / 5x5 / 7x7 shapes with 2, 64 or
+    128 input channels (siren_conv_wrw), fp32 out in the filter's channels-last layout; MIOpen's
+    weight-gradient convolution otherwise (the 1x1)."""
     co, ci, k, _ = wb.shape
     n, _, h, w = x.shape
     if _WGRAD_NATIVE[0] and co == ci == 128 and k == 5 and w % 64 == 0:

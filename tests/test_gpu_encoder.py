@@ -4,10 +4,10 @@ modules.py:340-380 / 433-450), and its native passes (siren_encoder.hip) against
 
 Tolerances: on MIOpen's convolutions the node's forward has the autocast chain's roundings, so the
 embedding agrees to fp32 summation order (1e-5); with the native 5x5 kernels (another summation
-order inside each convolution) to the bf16 level (3e-3); parameter gradients agree to the bf16
-level (2e-2 norm-relative; 3e-2 with every 64/128-channel convolution native, cnn[0] and its input
-gradient included: two bf16 paths each ~1-2 % from fp32, measured 2.1e-2 on a residual block's
-weight); against fp32 no further off than the autocast chain (test_fused_node_against_fp32_encoder).
+order inside each convolution) to the bf16 level (6e-3); parameter gradients agree to the bf16
+level (2e-2 norm-relative; with every 2/64/128-channel convolution native, two bf16 paths each a
+few % from fp32: 1e-1, measured 6.9e-2 on conv_theta's weight); against fp32 no further off than
+the autocast chain (test_fused_node_against_fp32_encoder).
 """
 import pytest
 import torch
@@ -36,9 +36,11 @@ def _run(enc, I, ge):
 @pytest.mark.parametrize("blocks,hidden,k", [(2, 128, 7), (1, 64, 5)])
 def test_fused_node_matches_autocast_chain(blocks, hidden, k, native_conv):
     """native_conv=False: the node on MIOpen's convolutions, the chain's own roundings (forward to
-    fp32 summation order, 1e-5). True: the residual blocks' convolutions on the native kernels
+    fp32 summation order, 1e-5). True: every 2/64/128-channel convolution on the native kernels
     (another fp32 summation order inside each convolution, so activations may differ by a bf16
-    rounding step: 3e-3 forward)."""
+    rounding step, compounding over the layers from conv_theta on: measured 3.8e-3 / 4.6e-3
+    forward, bound 6e-3); test_fused_node_against_fp32_encoder checks the native node is no
+    further from fp32 than the chain."""
     from siren_mri_amd import encoder
     enc = _encoder("bf16", blocks=blocks, hidden=hidden, k=k)
     g = torch.Generator().manual_seed(1)
@@ -55,10 +57,13 @@ def test_fused_node_matches_autocast_chain(blocks, hidden, k, native_conv):
             encoder.set_fused(True)
     finally:
         encoder._CONV_NATIVE[0] = encoder._WGRAD_NATIVE[0] = True
-    assert orc.norm_rel(e_f.cpu(), e_c.cpu()) < (3e-3 if native_conv else 1e-5)
+    assert orc.norm_rel(e_f.cpu(), e_c.cpu()) < (6e-3 if native_conv else 1e-5)
     assert g_f.keys() == g_c.keys()
     for n in g_f:
-        assert orc.norm_rel(g_f[n].cpu(), g_c[n].cpu()) < (3e-2 if native_conv else 2e-2), n
+        # native: conv_theta's weight gradient sums the whole network's bf16 backward over every
+        # pixel (chain and node each ~5 % from fp32 there: measured 6.9e-2 between them); the
+        # accuracy bound is test_fused_node_against_fp32_encoder's (<= 1.25 x the chain's error)
+        assert orc.norm_rel(g_f[n].cpu(), g_c[n].cpu()) < (1e-1 if native_conv else 2e-2), n
 
 
 def test_fused_node_against_fp32_encoder():
@@ -250,16 +255,17 @@ def test_conv_forward_kernel_against_fp32(bias, relu):
 
 
 @pytest.mark.parametrize("k,ci,co", [(7, 64, 128), (7, 128, 64), (3, 64, 128), (3, 128, 128), (5, 64, 64),
-                                     (5, 128, 128)])
+                                     (5, 128, 128), (7, 2, 64), (3, 2, 128), (5, 2, 32), (7, 2, 96)])
 @pytest.mark.parametrize("bias,relu", [(False, False), (True, True)])
 def test_generic_conv_forward_kernel_against_fp32(k, ci, co, bias, relu):
     """siren_conv_fwd (round 5: the encoder's other shapes — cnn[0]'s 64 -> 128 7x7, its input
-    gradient 128 -> 64, the 3x3 forms) against the fp64 convolution of the same bf16 operands
-    (then the conv + bias-add chain's bf16 roundings), bit-equal on a rerun."""
+    gradient 128 -> 64, the 3x3 forms; conv_theta's 2 input channels, with a ragged last
+    workgroup of image rows) against the fp64 convolution of the same bf16 operands (then the
+    conv + bias-add chain's bf16 roundings), bit-equal on a rerun."""
     from siren_mri_amd import _native
     import torch.nn.functional as F
     lib = _native.lib()
-    N, H = 2, 6
+    N, H = (2, 5) if ci == 2 else (2, 6)
     assert lib.siren_conv_check(0, N, H, 128, ci, co, k) == 0, _native.last_error()
     g = torch.Generator().manual_seed(k * 1000 + ci + co + bias)
     x = torch.randn(N, ci, H, 128, generator=g).to(torch.bfloat16)
@@ -285,7 +291,7 @@ def test_generic_conv_forward_kernel_against_fp32(k, ci, co, bias, relu):
     assert (d.abs() <= ref.float().abs() * 2 ** -7 + 1e-6).float().mean() > 0.999
 
 
-@pytest.mark.parametrize("k,ci,co", [(7, 64, 128), (3, 128, 64), (5, 64, 128)])
+@pytest.mark.parametrize("k,ci,co", [(7, 64, 128), (3, 128, 64), (5, 64, 128), (7, 2, 64), (3, 2, 128), (5, 2, 96)])
 @pytest.mark.parametrize("N,H,W", [(2, 128, 128), (3, 7, 64)])
 def test_generic_conv_weight_gradient_kernel_against_fp32(k, ci, co, N, H, W):
     """siren_conv_wrw against the fp64 weight gradient of the same bf16 operands, bit-equal on a rerun."""
@@ -309,11 +315,14 @@ def test_generic_conv_weight_gradient_kernel_against_fp32(k, ci, co, N, H, W):
     assert orc.norm_rel(outs[0].cpu(), ref) < 1e-6
 
 
-def test_c4_encoder_has_no_miopen_cnn0():
-    """Configs 4/5's encoder (kernel_size 7): cnn[0] and its gradients run on the native kernels —
-    only conv_theta (2 input channels) still takes MIOpen's."""
+def test_c4_encoder_has_no_miopen_7x7():
+    """Configs 4/5's encoder (kernel_size 7): cnn[0] and its gradients and conv_theta (2 input
+    channels: forward and weight gradient; no input gradient) run on the native kernels."""
     from siren_mri_amd import encoder
     enc = _encoder("bf16", blocks=1, hidden=128, k=7)
+    xi = torch.empty(2, 2, 128, 128, dtype=torch.bfloat16, device=DEV).contiguous(memory_format=torch.channels_last)
+    wt = encoder._w_bf16(enc.conv_theta.weight)
+    assert encoder._native_gen(0, xi, wt) and encoder._native_gen(1, xi, wt)
     x = torch.empty(2, 64, 128, 128, dtype=torch.bfloat16, device=DEV).contiguous(memory_format=torch.channels_last)
     wb = encoder._w_bf16(enc.cnn[0].weight)
     assert encoder._native_gen(0, x, wb) and encoder._native_gen(1, x, wb)

@@ -25,7 +25,7 @@ def main():
     args = bench.parse()
     _native.load_library()
     dev = torch.device("cuda", 0)
-    step, _ = bench.build_step(args, dev, 0, 1)
+    step = bench.build(args.config, args, dev, 0, 1).step
     for _ in range(5):
         step()
     torch.cuda.synchronize()
