@@ -30,6 +30,7 @@ extern "C" {
 /* Arithmetic modes of the layer stack. */
 #define SIREN_PREC_F32  0 /* fp32 operands, exact-fp32 MFMA (v_mfma_f32_32x32x2_f32), libm sin/cos  */
 #define SIREN_PREC_BF16 1 /* bf16 operands, fp32 accumulate, 16-bit phase storage, v_sin/v_cos     */
+#define SIREN_PREC_F64  2 /* IEEE double throughout (siren_mlp64_*: double_precision=True)         */
 
 /* Error codes. */
 #define SIREN_OK 0
@@ -75,6 +76,24 @@ typedef struct siren_mlp_desc {
 
 /* Validates a descriptor; returns SIREN_OK or SIREN_EINVAL (message in siren_last_error). */
 int siren_mlp_check(const siren_mlp_desc* d);
+
+/*
+ * fp64 stack: the reference's double_precision=True training (training.py:56-58, the model cast
+ * to float64 with .double()). prec = SIREN_PREC_F64; weight[l] / bias[l] point to double arrays
+ * and x, y, dy, dW, db, dx are double; any widths (dims 1..65536), shared or batched weights, sine
+ * or linear output layer; no Fourier-feature input. Forward saves Z (the pre-activation, fp64) of
+ * every sine layer in `saved` (siren_mlp64_saved_bytes; NULL for inference); the backward is
+ * first-order (dW, db of every layer, dx when non-NULL), weight-gradient row reductions added
+ * in a fixed split order (deterministic). Replaces FCBlock.forward / its autograd backward in
+ * float64 (modules.py:16-27, 35-38, 92-97).
+ */
+int64_t siren_mlp64_saved_bytes(const siren_mlp_desc* d);
+int64_t siren_mlp64_workspace_bytes(const siren_mlp_desc* d);
+int siren_mlp64_forward(const siren_mlp_desc* d, const double* x, double* y, void* saved, int64_t saved_bytes,
+                        void* workspace, int64_t workspace_bytes, void* stream);
+int siren_mlp64_backward(const siren_mlp_desc* d, const double* x, const double* dy, const void* saved,
+                         int64_t saved_bytes, void* workspace, int64_t workspace_bytes, double* const* dW,
+                         double* const* db, double* dx, void* stream);
 
 /* Bytes of the per-call "saved" buffer (the activations kept between forward and
  * backward: one phase tensor per sine layer). */

@@ -16,6 +16,7 @@ import torch
 MAX_LAYERS = 16
 PREC_F32 = 0
 PREC_BF16 = 1
+PREC_F64 = 2  # float64 tensors (siren_mlp64_*): chosen by dtype, not by the precision string
 PRECISIONS = {"fp32": PREC_F32, "f32": PREC_F32, "float32": PREC_F32,
               "bf16": PREC_BF16, "bfloat16": PREC_BF16}
 
@@ -33,6 +34,10 @@ EXPORTED_SYMBOLS = (
     "siren_mlp_loss_check",
     "siren_mlp_forward_loss",
     "siren_mlp_backward_ex",
+    "siren_mlp64_saved_bytes",
+    "siren_mlp64_workspace_bytes",
+    "siren_mlp64_forward",
+    "siren_mlp64_backward",
     "siren_jvp_saved_bytes",
     "siren_jvp_workspace_bytes",
     "siren_jvp_forward",
@@ -191,6 +196,14 @@ def _declare(lib):
     lib.siren_mlp_forward_loss.restype = ci
     lib.siren_mlp_backward_ex.argtypes = [P, vp, vp, vp, vp, i64, vp, i64, ctypes.POINTER(vp), ctypes.POINTER(vp), vp, vp]
     lib.siren_mlp_backward_ex.restype = ci
+    lib.siren_mlp64_saved_bytes.argtypes = [P]
+    lib.siren_mlp64_saved_bytes.restype = i64
+    lib.siren_mlp64_workspace_bytes.argtypes = [P]
+    lib.siren_mlp64_workspace_bytes.restype = i64
+    lib.siren_mlp64_forward.argtypes = [P, vp, vp, vp, i64, vp, i64, vp]
+    lib.siren_mlp64_forward.restype = ci
+    lib.siren_mlp64_backward.argtypes = [P, vp, vp, vp, i64, vp, i64, ctypes.POINTER(vp), ctypes.POINTER(vp), vp, vp]
+    lib.siren_mlp64_backward.restype = ci
     lib.siren_jvp_saved_bytes.argtypes = [P, ci]
     lib.siren_jvp_saved_bytes.restype = i64
     lib.siren_jvp_workspace_bytes.argtypes = [P, ci]

@@ -19,6 +19,7 @@
 #include "siren_kspace.hip"
 #include "siren_encoder.hip"
 #include "siren_conv.hip"
+#include "siren_f64.hip"
 
 using namespace siren;
 
@@ -1561,7 +1562,212 @@ int jvp_backward_impl(const siren_mlp_desc* d, int order, const float* x, const 
 
 }  // namespace
 
+namespace {
+// ------------------------------------------------------------------ fp64 stack (siren_f64.hip)
+struct F64Layout {
+  int64_t z_off[SIREN_MAX_LAYERS];  // saved Z of each sine layer (-1: linear output layer)
+  int64_t saved_bytes;
+  int64_t h_off[2], dz_off[2], part_off, ws_bytes;
+};
+
+// split of the weight-gradient GEMM's row reduction: ~512 workgroups over the output tiles
+void f64_split(const Geo& g, int M, int N, int64_t& nsplit, int64_t& per) {
+  const int64_t tiles = cdiv(M, 64) * cdiv(N + 1, 64) * g.nb;
+  nsplit = std::max<int64_t>(1, std::min<int64_t>(cdiv(512, tiles), cdiv(g.rows, 64)));
+  per = align_up(cdiv(g.rows, nsplit), 16);
+  nsplit = cdiv(g.rows, per);
+}
+
+F64Layout f64_layout(const siren_mlp_desc* d) {
+  const Geo g = geo_of(d);
+  F64Layout lo;
+  int64_t off = 0, wmax = 0, part = 0;
+  for (int l = 0; l < g.L; ++l) {
+    const bool sine = l + 1 < g.L || !d->outermost_linear;
+    lo.z_off[l] = sine ? off : -1;
+    if (sine) off = align_up(off + g.total * d->dims[l + 1] * 8, 256);
+    wmax = std::max<int64_t>(wmax, std::max(d->dims[l], d->dims[l + 1]));
+    int64_t ns, per;
+    f64_split(g, d->dims[l + 1], d->dims[l], ns, per);
+    part = std::max<int64_t>(part, ns * g.nb * (int64_t)d->dims[l + 1] * (d->dims[l] + 1));
+  }
+  lo.saved_bytes = off;
+  off = 0;
+  for (int k = 0; k < 2; ++k) {
+    lo.h_off[k] = off;
+    off = align_up(off + g.total * wmax * 8, 256);
+  }
+  for (int k = 0; k < 2; ++k) {
+    lo.dz_off[k] = off;
+    off = align_up(off + g.total * wmax * 8, 256);
+  }
+  lo.part_off = off;
+  off = align_up(off + part * 8, 256);
+  lo.ws_bytes = off;
+  return lo;
+}
+
+int f64_check(const siren_mlp_desc* d) {
+  if (!d) return fail(SIREN_EINVAL, "null descriptor");
+  const int L = d->num_layers;
+  if (L < 1 || L > SIREN_MAX_LAYERS) return fail(SIREN_EINVAL, "num_layers=%d outside [1, %d]", L, SIREN_MAX_LAYERS);
+  if (d->prec != SIREN_PREC_F64) return fail(SIREN_EINVAL, "fp64 entry point with precision %d", d->prec);
+  if (d->batch < 1 || d->rows_per_batch < 1) return fail(SIREN_EINVAL, "empty input");
+  if (d->batch > 65535) return fail(SIREN_EINVAL, "batch %lld > 65535", (long long)d->batch);
+  for (int l = 0; l <= L; ++l)
+    if (d->dims[l] < 1 || d->dims[l] > 65536) return fail(SIREN_EINVAL, "dims[%d]=%d unsupported", l, d->dims[l]);
+  for (int l = 0; l < L; ++l)
+    if (!d->weight[l] || !d->bias[l]) return fail(SIREN_EINVAL, "layer %d: null weight/bias", l);
+  if (d->ff_B) return fail(SIREN_EINVAL, "fp64: no fused Fourier-feature input");
+  return SIREN_OK;
+}
+
+template <int TA, int TB, int EPI>
+int f64_launch(const F64Args& a, int64_t z, hipStream_t st) {
+  const dim3 grid((unsigned)cdiv(a.M, 64), (unsigned)cdiv(EPI == F64_DW ? a.N + 1 : a.N, 64), (unsigned)z);
+  hipLaunchKernelGGL((f64_gemm_kernel<TA, TB, EPI>), grid, dim3(256), 0, st, a);
+  return check_launch("f64_gemm");
+}
+
+}  // namespace
+
 extern "C" {
+
+int64_t siren_mlp64_saved_bytes(const siren_mlp_desc* d) {
+  if (f64_check(d)) return -1;
+  return f64_layout(d).saved_bytes;
+}
+
+int64_t siren_mlp64_workspace_bytes(const siren_mlp_desc* d) {
+  if (f64_check(d)) return -1;
+  return f64_layout(d).ws_bytes;
+}
+
+int siren_mlp64_forward(const siren_mlp_desc* d, const double* x, double* y, void* saved, int64_t saved_bytes,
+                        void* workspace, int64_t workspace_bytes, void* stream) {
+  int rc = f64_check(d);
+  if (rc) return rc;
+  if (!x || !y) return fail(SIREN_EINVAL, "fp64 forward: null x / y");
+  const Geo g = geo_of(d);
+  const F64Layout lo = f64_layout(d);
+  if (saved && saved_bytes < lo.saved_bytes) return fail(SIREN_ENOSPACE, "fp64 forward: saved buffer too small");
+  if (!workspace || workspace_bytes < lo.ws_bytes) return fail(SIREN_ENOSPACE, "fp64 forward: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  const double* h = x;
+  for (int l = 0; l < g.L; ++l) {
+    const int K = d->dims[l], N = d->dims[l + 1];
+    const bool last = l + 1 == g.L, sine = !last || !d->outermost_linear;
+    F64Args a;
+    memset(&a, 0, sizeof(a));
+    a.A = h;
+    a.B = (const double*)d->weight[l];
+    a.bias = (const double*)d->bias[l];
+    a.C = last ? y : (double*)(ws + lo.h_off[l & 1]);
+    a.Zs = (saved && sine) ? (double*)((char*)saved + lo.z_off[l]) : nullptr;
+    a.M = g.rows;
+    a.N = N;
+    a.K = K;
+    a.lda = K;
+    a.ldb = K;
+    a.ldc = N;
+    a.a_bs = g.rows * K;
+    a.b_bs = d->weights_batched ? (int64_t)N * K : 0;
+    a.bias_bs = d->weights_batched ? N : 0;
+    a.c_bs = a.zs_bs = g.rows * N;
+    a.nb = (int)g.nb;
+    a.w0 = d->w0;
+    rc = sine ? f64_launch<0, 0, F64_FWD_SINE>(a, g.nb, st) : f64_launch<0, 0, F64_FWD_LIN>(a, g.nb, st);
+    if (rc) return rc;
+    h = a.C;
+  }
+  return SIREN_OK;
+}
+
+int siren_mlp64_backward(const siren_mlp_desc* d, const double* x, const double* dy, const void* saved,
+                         int64_t saved_bytes, void* workspace, int64_t workspace_bytes, double* const* dW,
+                         double* const* db, double* dx, void* stream) {
+  int rc = f64_check(d);
+  if (rc) return rc;
+  if (!x || !dy || !saved || !dW || !db) return fail(SIREN_EINVAL, "fp64 backward: null argument");
+  const Geo g = geo_of(d);
+  const F64Layout lo = f64_layout(d);
+  if (saved_bytes < lo.saved_bytes) return fail(SIREN_ENOSPACE, "fp64 backward: saved buffer too small");
+  if (!workspace || workspace_bytes < lo.ws_bytes) return fail(SIREN_ENOSPACE, "fp64 backward: workspace too small");
+  for (int l = 0; l < g.L; ++l)
+    if (!dW[l] || !db[l]) return fail(SIREN_EINVAL, "fp64 backward: layer %d null dW / db", l);
+  hipStream_t st = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  const char* sv = (const char*)saved;
+  double* part = (double*)(ws + lo.part_off);
+  // dZ of the output layer
+  const double* dz = dy;
+  if (!d->outermost_linear) {
+    const int64_t n = g.total * d->dims[g.L];
+    double* t = (double*)(ws + lo.dz_off[0]);
+    hipLaunchKernelGGL(f64_top_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, dy,
+                       (const double*)(sv + lo.z_off[g.L - 1]), t, n, (double)d->w0);
+    if ((rc = check_launch("f64_top"))) return rc;
+    dz = t;
+  }
+  for (int l = g.L - 1; l >= 0; --l) {
+    const int M = d->dims[l + 1], N = d->dims[l];
+    // [dW | db] = dZ_l^T [H_l | 1], H_l = sin(w0 Z_{l-1}) (x for l = 0)
+    int64_t ns, per;
+    f64_split(g, M, N, ns, per);
+    F64Args w;
+    memset(&w, 0, sizeof(w));
+    w.A = dz;
+    w.B = l == 0 ? x : (const double*)(sv + lo.z_off[l - 1]);
+    w.Zp = l == 0 ? nullptr : w.B;
+    w.C = part;
+    w.M = M;
+    w.N = N;
+    w.K = g.rows;
+    w.lda = M;
+    w.ldb = N;
+    w.ldc = N + 1;
+    w.a_bs = g.rows * M;
+    w.b_bs = g.rows * N;
+    w.c_bs = (int64_t)M * (N + 1);
+    w.k_per_split = per;
+    w.nb = (int)g.nb;
+    w.w0 = d->w0;
+    if ((rc = f64_launch<1, 1, F64_DW>(w, ns * g.nb, st))) return rc;
+    const int64_t nred = g.nb * (int64_t)M * (N + 1);
+    hipLaunchKernelGGL(f64_reduce_kernel, dim3((unsigned)cdiv(nred, 256)), dim3(256), 0, st, (const double*)part,
+                       dW[l], db[l], (int64_t)M, (int64_t)N, (int)g.nb, (int)ns);
+    if ((rc = check_launch("f64_reduce"))) return rc;
+    if (l == 0 && !dx) break;
+    // dH_l = dZ_l W_l; dZ_{l-1} = dH_l w0 cos(w0 Z_{l-1}) (dx for l = 0)
+    F64Args h;
+    memset(&h, 0, sizeof(h));
+    h.A = dz;
+    h.B = (const double*)d->weight[l];
+    h.M = g.rows;
+    h.N = N;
+    h.K = M;
+    h.lda = M;
+    h.ldb = N;
+    h.ldc = N;
+    h.a_bs = g.rows * M;
+    h.b_bs = d->weights_batched ? (int64_t)M * N : 0;
+    h.c_bs = h.zs_bs = g.rows * N;
+    h.nb = (int)g.nb;
+    h.w0 = d->w0;
+    if (l == 0) {
+      h.C = dx;
+      if ((rc = f64_launch<0, 1, F64_DX>(h, g.nb, st))) return rc;
+    } else {
+      h.Zp = (const double*)(sv + lo.z_off[l - 1]);
+      double* out = (double*)(ws + lo.dz_off[(dz == (const double*)(ws + lo.dz_off[0])) ? 1 : 0]);
+      h.C = out;
+      if ((rc = f64_launch<0, 1, F64_DH>(h, g.nb, st))) return rc;
+      dz = out;
+    }
+  }
+  return SIREN_OK;
+}
 
 int siren_mlp_check(const siren_mlp_desc* d) {
   if (!d) return fail(SIREN_EINVAL, "null descriptor");

@@ -20,7 +20,12 @@ formula of sine_mlp_fwd (its Autograd dispatch key) is sine_mlp_bwd; under creat
 per-channel Jacobian of the tangent-stream op (jvp.py), which is itself differentiable, and the
 weight gradients are exact but raise if differentiated again.
 
-No CPU or eager-PyTorch fallback exists: a CPU tensor, a float64 tensor or an unsupported
+float64 inputs and parameters (the reference's double_precision=True with the model cast by
+.double(), training.py:56-58) take the fp64 stack (siren_mlp64_*, csrc/siren_f64.hip) through
+  siren_mri_amd::sine_mlp64_fwd / sine_mlp64_bwd
+whatever `precision` says (first-order gradients; no Fourier-feature input, no fused loss).
+
+No CPU or eager-PyTorch fallback exists: a CPU tensor, a mixed-dtype call or an unsupported
 shape raises.
 """
 from __future__ import annotations
@@ -302,6 +307,164 @@ torch.library.register_fake("siren_mri_amd::sine_mlp_fwd", _sine_mlp_fwd_fake, l
 torch.library.register_fake("siren_mri_amd::sine_mlp_bwd", _sine_mlp_bwd_fake, lib=_LIB)
 
 
+# ---------------------------------------------------------------- fp64 stack (double_precision=True)
+_LIB.define("sine_mlp64_fwd(Tensor x, Tensor[] weights, Tensor[] biases, float w0, bool outermost_linear, "
+            "bool batched, bool keep) -> (Tensor, Tensor)")
+_LIB.define("sine_mlp64_bwd(Tensor dy, Tensor x, Tensor[] weights, Tensor[] biases, Tensor saved, float w0, "
+            "bool outermost_linear, bool batched, bool need_dx) -> (Tensor, Tensor[], Tensor[])")
+
+_SIZES64 = {}
+
+
+def _sizes64(geo: _Geometry, outermost_linear: bool):
+    key = (tuple(geo.dims), geo.batch, geo.rows, geo.batched, outermost_linear)
+    hit = _SIZES64.get(key)
+    if hit is None:
+        L = _native.lib()
+        desc = _native.describe_only(geo.dims, prec=_native.PREC_F64, outermost_linear=outermost_linear,
+                                     weights_batched=geo.batched, batch=geo.batch, rows_per_batch=geo.rows)
+        saved = L.siren_mlp64_saved_bytes(ctypes.byref(desc))
+        if saved < 0:
+            _native.check(-1, "siren_mlp64_saved_bytes")
+        hit = (saved, L.siren_mlp64_workspace_bytes(ctypes.byref(desc)))
+        if len(_SIZES64) > 256:
+            _SIZES64.clear()
+        _SIZES64[key] = hit
+    return hit
+
+
+def _require_f64(x, weights, biases):
+    if x.device.type != "cuda":
+        raise RuntimeError("siren_mri_amd: the SIREN layer stack runs only on an MI355X (HIP) device; got a "
+                           f"{x.device.type} tensor. There is no CPU fallback by design.")
+    for t in list(weights) + list(biases):
+        if t.dtype != torch.float64 or t.device != x.device:
+            raise RuntimeError("siren_mri_amd: a float64 input needs float64 weights and biases on its device "
+                               f"(model.double(), as the reference's double_precision=True); got {t.dtype}")
+
+
+def sine_mlp64_fwd(x: Tensor, weights: List[Tensor], biases: List[Tensor], w0: float, outermost_linear: bool,
+                   batched: bool, keep: bool) -> Tuple[Tensor, Tensor]:
+    """siren_mlp64_forward: y (float64); saved = the pre-activations of the sine layers (empty unless keep)."""
+    _require_f64(x, weights, biases)
+    geo = _geo_of(x, weights, batched)
+    ws = [w.contiguous() for w in weights]
+    bs = [b.contiguous() for b in biases]
+    xc = x.contiguous()
+    dev = x.device
+    desc = _native.make_desc(geo.dims, ws, bs, w0=w0, prec=_native.PREC_F64, outermost_linear=outermost_linear,
+                             weights_batched=geo.batched, batch=geo.batch, rows_per_batch=geo.rows)
+    saved_bytes, ws_bytes = _sizes64(geo, outermost_linear)
+    saved = torch.empty(saved_bytes if keep else 0, dtype=torch.uint8, device=dev)
+    work = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    y = torch.empty(geo.lead_shape + (geo.dims[-1],), dtype=torch.float64, device=dev)
+    rc = _native.lib().siren_mlp64_forward(ctypes.byref(desc), xc.data_ptr(), y.data_ptr(),
+                                           saved.data_ptr() if keep else None, saved_bytes if keep else 0,
+                                           work.data_ptr(), ws_bytes, _native.stream_handle(dev))
+    _native.check(rc, "siren_mlp64_forward")
+    return y, saved
+
+
+def _sine_mlp64_fwd_fake(x, weights, biases, w0, outermost_linear, batched, keep):
+    geo = _geo_of(x, weights, batched)
+    saved_bytes, _ = _sizes64(geo, outermost_linear)
+    return (x.new_empty(geo.lead_shape + (geo.dims[-1],), dtype=torch.float64),
+            x.new_empty((saved_bytes if keep else 0,), dtype=torch.uint8))
+
+
+def sine_mlp64_bwd(dy: Tensor, x: Tensor, weights: List[Tensor], biases: List[Tensor], saved: Tensor, w0: float,
+                   outermost_linear: bool, batched: bool, need_dx: bool) -> Tuple[Tensor, List[Tensor], List[Tensor]]:
+    """siren_mlp64_backward: (dx or an empty tensor, dW per layer, db per layer), all float64."""
+    if saved.numel() == 0:
+        raise RuntimeError("siren_mri_amd: sine_mlp64_bwd needs the saved buffer of a forward run with keep=True")
+    geo = _geo_of(x, weights, batched)
+    ws = [w.contiguous() for w in weights]
+    bs = [b.contiguous() for b in biases]
+    xc = x.contiguous()
+    dev = x.device
+    dyc = dy.contiguous().to(torch.float64)
+    desc = _native.make_desc(geo.dims, ws, bs, w0=w0, prec=_native.PREC_F64, outermost_linear=outermost_linear,
+                             weights_batched=geo.batched, batch=geo.batch, rows_per_batch=geo.rows)
+    saved_bytes, ws_bytes = _sizes64(geo, outermost_linear)
+    work = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    dW = [torch.empty_like(w) for w in ws]
+    db = [torch.empty_like(b) for b in bs]
+    dx = torch.empty_like(xc) if need_dx else xc.new_empty((0,))
+    n = len(ws)
+    VP = ctypes.c_void_p * n
+    rc = _native.lib().siren_mlp64_backward(ctypes.byref(desc), xc.data_ptr(), dyc.data_ptr(), saved.data_ptr(),
+                                            saved_bytes, work.data_ptr(), ws_bytes,
+                                            VP(*[t.data_ptr() for t in dW]), VP(*[t.data_ptr() for t in db]),
+                                            dx.data_ptr() if need_dx else None, _native.stream_handle(dev))
+    _native.check(rc, "siren_mlp64_backward")
+    return dx, dW, db
+
+
+def _sine_mlp64_bwd_fake(dy, x, weights, biases, saved, w0, outermost_linear, batched, need_dx):
+    return (torch.empty_like(x) if need_dx else x.new_empty((0,)),
+            [torch.empty_like(w) for w in weights], [torch.empty_like(b) for b in biases])
+
+
+class _SineMLP64Autograd(torch.autograd.Function):
+    """Autograd formula of sine_mlp64_fwd: its backward is sine_mlp64_bwd (first order)."""
+
+    @staticmethod
+    def forward(ctx, meta, x, *params):
+        w0, outermost_linear, batched, n, keep = meta
+        with torch._C._AutoDispatchBelowAutograd():
+            y, saved = torch.ops.siren_mri_amd.sine_mlp64_fwd(x, list(params[:n]), list(params[n:]), w0,
+                                                              outermost_linear, batched, keep)
+        ctx.meta = meta
+        ctx.save_for_backward(x, saved, *params)
+        ctx.mark_non_differentiable(saved)
+        ctx.set_materialize_grads(False)
+        return y, saved
+
+    @staticmethod
+    def backward(ctx, dy, _dsaved):
+        w0, outermost_linear, batched, n, keep = ctx.meta
+        if dy is None:
+            return (None,) * (2 + 2 * n)
+        if not keep:
+            raise RuntimeError("siren_mri_amd: the SIREN forward ran without keeping activations "
+                               "(grad mode was off); it cannot be differentiated")
+        if torch.is_grad_enabled():
+            raise RuntimeError("siren_mri_amd: second derivatives of the fp64 SIREN stack are not provided "
+                               "(create_graph=True); the fp32 / bf16 stacks provide them")
+        t = ctx.saved_tensors
+        x, saved, ws, bs = t[0], t[1], list(t[2:2 + n]), list(t[2 + n:])
+        need_dx = ctx.needs_input_grad[1]
+        dx, dW, db = torch.ops.siren_mri_amd.sine_mlp64_bwd(dy, x, ws, bs, saved, w0, outermost_linear, batched,
+                                                            need_dx)
+        return (None, dx if need_dx else None, *dW, *db)
+
+
+def _sine_mlp64_fwd_autograd(x, weights, biases, w0, outermost_linear, batched, keep):
+    meta = (w0, outermost_linear, batched, len(weights), keep)
+    return _SineMLP64Autograd.apply(meta, x, *weights, *biases)
+
+
+_LIB.impl("sine_mlp64_fwd", sine_mlp64_fwd, "CUDA")
+_LIB.impl("sine_mlp64_bwd", sine_mlp64_bwd, "CUDA")
+_LIB.impl("sine_mlp64_fwd", _sine_mlp64_fwd_autograd, "Autograd")
+torch.library.register_fake("siren_mri_amd::sine_mlp64_fwd", _sine_mlp64_fwd_fake, lib=_LIB)
+torch.library.register_fake("siren_mri_amd::sine_mlp64_bwd", _sine_mlp64_bwd_fake, lib=_LIB)
+
+
+def _siren_mlp64(x, weights, biases, w0, outermost_linear, return_saved, ff_B):
+    if ff_B is not None:
+        raise RuntimeError("siren_mri_amd: no Fourier-feature input in the fp64 stack (the reference's "
+                           "double_precision=True cannot combine them either: its B is float32)")
+    _require_f64(x, weights, biases)
+    geo = _Geometry(x, weights)
+    ws, bs = list(weights), list(biases)
+    if geo.squeeze_w:
+        ws, bs = [w[0] for w in ws], [b[0] for b in bs]
+    keep = torch.is_grad_enabled() and (x.requires_grad or any(t.requires_grad for t in ws + bs))
+    y, saved = torch.ops.siren_mri_amd.sine_mlp64_fwd(x, ws, bs, float(w0), bool(outermost_linear), geo.batched, keep)
+    return (y, saved) if return_saved else y
+
+
 # ---------------------------------------------------------------- forward with the fused image loss
 def _loss_desc(tgt, k0, mask, hf, noise, weight, y_dc, dy, loss, lws):
     ld = _native.SirenLossDesc()
@@ -497,10 +660,12 @@ def siren_mlp(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence
     coordinates and the stack's input is their Gaussian Fourier features (features.py:21-41):
     formed inside the forward's first layer with a staged image loss (bf16 wide form, no input
     gradient), else materialised by the fourier_features op first."""
-    prec = _native.precision_code(precision or _DEFAULT_PRECISION)
     n = len(weights)
     if len(biases) != n:
         raise ValueError("siren_mlp: weights and biases differ in length")
+    if x.dtype == torch.float64:
+        return _siren_mlp64(x, weights, biases, w0, outermost_linear, return_saved, ff_B)
+    prec = _native.precision_code(precision or _DEFAULT_PRECISION)
     _require_device(x)
     if ff_B is not None:
         y = _fourier_input_forward(x, weights, biases, w0, prec, outermost_linear, return_saved, ff_B)
