@@ -3,8 +3,9 @@ double_precision=True training (training.py:56-58) with the model cast to float6
 fp64 oracle (oracle/siren_oracle.py: FCBlock.forward restated, autograd for the gradients).
 
 Both sides compute in IEEE double with different summation orders, so forward, every dW / db and
-dx agree to ~1e-15 norm-relative (measured 1e-16 - 1.7e-15; bound 1e-13); the 3-step Adam fit through training.train with
-double_precision=True reproduces the oracle's training loop losses to 1e-11.
+dx agree to ~1e-15 norm-relative (measured 1e-16 - 1.7e-15; bound 1e-13); the 3-step Adam fit
+through training.train with double_precision=True reproduces the oracle's training loop losses
+to 1e-11.
 """
 import numpy as np
 import pytest
