@@ -2058,7 +2058,7 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const f32x4 v = {acc[bm][bn][4 * q], acc[bm][bn][4 * q + 1], acc[bm][bn][4 * q + 2], acc[bm][bn][4 * q + 3]};
-        *(f32x4*)(part + ((((wave * 2 + bm) * 4 + bn) * 64 + lane) * 16 + 4 * q)) = v;
+        *(f32x4*)(part + (((((wave * 2 + bm) * 4 + bn) * 4 + q) * 64 + lane) * 4)) = v;
       }
 #else
 #pragma unroll
