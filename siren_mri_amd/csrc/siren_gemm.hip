@@ -2049,18 +2049,6 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
 
   // partial slab: dW (row-major M x N) then db (M)
   float* part = a.part + (int64_t)split * a.split_stride + batch * ((int64_t)M * N + M);
-#ifdef SIREN_SLAB_FRAG_PROBE
-  // timing probe only (wrong slab order): the same 256 KB as 16-byte stores in fragment order
-#pragma unroll
-  for (int bm = 0; bm < 2; ++bm)
-#pragma unroll
-    for (int bn = 0; bn < 4; ++bn)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 v = {acc[bm][bn][4 * q], acc[bm][bn][4 * q + 1], acc[bm][bn][4 * q + 2], acc[bm][bn][4 * q + 3]};
-        *(f32x4*)(part + (((((wave * 2 + bm) * 4 + bn) * 4 + q) * 64 + lane) * 4)) = v;
-      }
-#else
 #pragma unroll
   for (int bm = 0; bm < 2; ++bm)
 #pragma unroll
@@ -2072,7 +2060,6 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
         part[(int64_t)row * N + col] = acc[bm][bn][e];
       }
     }
-#endif
   __syncthreads();
   float* red = (float*)smem;  // [16 row slots][256]
 #pragma unroll
