@@ -328,6 +328,38 @@ int siren_conv_fwd(const void* x, const void* w, const void* bias, int relu, voi
 int64_t siren_conv_wrw_ws_bytes(int N, int H, int W, int CI, int CO, int KS);
 int siren_conv_wrw(const void* x, const void* dy, int N, int H, int W, int CI, int CO, int KS, float* dw, void* ws,
                    int64_t ws_bytes, void* stream);
+/*
+ * HyperNetwork heads (meta_modules.py:11-54; configs 4/5): `heads` ReLU FCBlocks (modules.py:40-119,
+ * nonlinearity='relu', outermost_linear=True) on one shared latent z [rows][in_features]: per head
+ * `depth` Linear + ReLU layers of width `hidden`, then a Linear to out_features[g]. Every head's layer
+ * of one depth is one grouped fp32 GEMM launch (bias and ReLU in its epilogue). weight[g * 5 + d] /
+ * bias[g * 5 + d] are the head's layer d (d = depth: the output layer), nn.Linear layout [out][in].
+ *   forward : out[g] [rows][out_features[g]]; saved (siren_hyper_saved_bytes) keeps the ReLU outputs.
+ *   backward: dW / db of every layer (same [g * 5 + d] indexing, [out][in] / [out]) and dz (the
+ *             latent's gradient, summed over the heads in head order); deterministic.
+ */
+#define SIREN_HYPER_MAXG 32
+#define SIREN_HYPER_MAXD 4
+typedef struct siren_hyper_desc {
+  int32_t heads, depth, rows, in_features, hidden;
+  int32_t out_features[SIREN_HYPER_MAXG];
+  const float* weight[SIREN_HYPER_MAXG * (SIREN_HYPER_MAXD + 1)];
+  const float* bias[SIREN_HYPER_MAXG * (SIREN_HYPER_MAXD + 1)];
+} siren_hyper_desc;
+int64_t siren_hyper_saved_bytes(const siren_hyper_desc* d);
+int64_t siren_hyper_workspace_bytes(const siren_hyper_desc* d);
+int siren_hyper_forward(const siren_hyper_desc* d, const float* z, float* const* out, void* saved, int64_t saved_bytes,
+                        void* stream);
+int siren_hyper_backward(const siren_hyper_desc* d, const float* z, const float* const* dout, const void* saved,
+                         int64_t saved_bytes, void* workspace, int64_t workspace_bytes, float* const* dW,
+                         float* const* db, float* dz, void* stream);
+/* The encoder's per-step operand preparation in one launch: for each of n (<= 32) convolutions,
+ * geom[7 i ..] = {co, ci, k, stride_co, stride_ci, stride_kh, stride_kw} of the fp32 filter w[i]
+ * (any strides); writes wb[i] = its bf16 channels-last copy [co][kh][kw][ci], wf[i] (wf or wf[i]
+ * may be NULL) = the input gradient's bf16 filter [ci][k-1-kh][k-1-kw][co], and bb[i] (bb / bb[i]
+ * may be NULL) = bf16 bias b[i] [co]; round to nearest even (torch's .to(torch.bfloat16)). */
+int siren_enc_prep(int n, const float* const* w, const float* const* b, const int64_t* geom, void* const* wb,
+                   void* const* wf, void* const* bb, void* stream);
 int siren_enc_relu_bwd(const void* g1, const void* g2, const void* y, void* out, float* db, int64_t P, int C, void* ws,
                        int64_t ws_bytes, void* stream);
 int siren_enc_bias_relu(void* y, const void* cb, int64_t P, int C, void* stream);

@@ -38,6 +38,10 @@ EXPORTED_SYMBOLS = (
     "siren_mlp64_workspace_bytes",
     "siren_mlp64_forward",
     "siren_mlp64_backward",
+    "siren_hyper_saved_bytes",
+    "siren_hyper_workspace_bytes",
+    "siren_hyper_forward",
+    "siren_hyper_backward",
     "siren_jvp_saved_bytes",
     "siren_jvp_workspace_bytes",
     "siren_jvp_forward",
@@ -63,6 +67,7 @@ EXPORTED_SYMBOLS = (
     "siren_conv_wrw_ws_bytes",
     "siren_conv_wrw",
     "siren_enc_bias_relu",
+    "siren_enc_prep",
     "siren_enc_relu_bwd",
     "siren_enc_res_fwd",
     "siren_enc_res_bwd",
@@ -131,6 +136,25 @@ class SirenLossDesc(ctypes.Structure):
         ("loss", ctypes.c_void_p),
         ("loss_workspace", ctypes.c_void_p),
         ("loss_workspace_bytes", ctypes.c_int64),
+    ]
+
+
+HYPER_MAXG = 32
+HYPER_MAXD = 4
+
+
+class SirenHyperDesc(ctypes.Structure):
+    """Mirror of ``siren_hyper_desc`` (include/siren_mri_amd.h)."""
+
+    _fields_ = [
+        ("heads", ctypes.c_int32),
+        ("depth", ctypes.c_int32),
+        ("rows", ctypes.c_int32),
+        ("in_features", ctypes.c_int32),
+        ("hidden", ctypes.c_int32),
+        ("out_features", ctypes.c_int32 * HYPER_MAXG),
+        ("weight", ctypes.c_void_p * (HYPER_MAXG * (HYPER_MAXD + 1))),
+        ("bias", ctypes.c_void_p * (HYPER_MAXG * (HYPER_MAXD + 1))),
     ]
 
 
@@ -204,6 +228,19 @@ def _declare(lib):
     lib.siren_mlp64_forward.restype = ci
     lib.siren_mlp64_backward.argtypes = [P, vp, vp, vp, i64, vp, i64, ctypes.POINTER(vp), ctypes.POINTER(vp), vp, vp]
     lib.siren_mlp64_backward.restype = ci
+    HP = ctypes.POINTER(SirenHyperDesc)
+    lib.siren_hyper_saved_bytes.argtypes = [HP]
+    lib.siren_hyper_saved_bytes.restype = i64
+    lib.siren_hyper_workspace_bytes.argtypes = [HP]
+    lib.siren_hyper_workspace_bytes.restype = i64
+    lib.siren_hyper_forward.argtypes = [HP, vp, ctypes.POINTER(vp), vp, i64, vp]
+    lib.siren_hyper_forward.restype = ci
+    lib.siren_hyper_backward.argtypes = [HP, vp, ctypes.POINTER(vp), vp, i64, vp, i64, ctypes.POINTER(vp),
+                                         ctypes.POINTER(vp), vp, vp]
+    lib.siren_hyper_backward.restype = ci
+    lib.siren_enc_prep.argtypes = [ci, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64),
+                                   ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), vp]
+    lib.siren_enc_prep.restype = ci
     lib.siren_jvp_saved_bytes.argtypes = [P, ci]
     lib.siren_jvp_saved_bytes.restype = i64
     lib.siren_jvp_workspace_bytes.argtypes = [P, ci]

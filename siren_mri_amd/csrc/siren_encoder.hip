@@ -338,4 +338,47 @@ __global__ __launch_bounds__(256) void enc_pixfc_bwd_kernel(EncArgs a) {
   enc_block_sum(a, acc, c0, pix, ppi, a.C, a.db, nullptr);
 }
 
+// The encoder's per-step operand preparation in one launch (round 5): every convolution's fp32
+// filter -> its bf16 channels-last copy [co][kh][kw][ci], the flipped / transposed bf16 filter of
+// its input gradient [ci][k - 1 - kh][k - 1 - kw][co] (when asked), and its bias -> bf16; the
+// casts round to nearest even as torch's .to(torch.bfloat16). Replaces ~50 cast / flip / copy
+// launches per C4 step.
+constexpr int ENC_PREP_MAX = 32;
+struct EncPrepSeg {
+  const float* w;
+  const float* b;
+  bf16* wb;
+  bf16* wf;  // or null
+  bf16* bb;  // or null
+  int co, ci, k;
+  int64_t s_co, s_ci, s_kh, s_kw;  // element strides of w
+  int64_t begin;                   // first flat index of this segment (filter elements, then bias)
+};
+struct EncPrepArgs {
+  EncPrepSeg seg[ENC_PREP_MAX];
+  int nseg;
+  int64_t total;
+};
+__global__ __launch_bounds__(256) void enc_prep_kernel(EncPrepArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.total) return;
+  int si = 0;
+  while (si + 1 < a.nseg && i >= a.seg[si + 1].begin) ++si;
+  const EncPrepSeg& g = a.seg[si];
+  const int64_t e = i - g.begin;
+  const int64_t nw = (int64_t)g.co * g.ci * g.k * g.k;
+  if (e < nw) {
+    // e in channels-last order: ((co k + kh) k + kw) ci + ci
+    const int ci = (int)(e % g.ci);
+    const int kw = (int)((e / g.ci) % g.k);
+    const int kh = (int)((e / ((int64_t)g.ci * g.k)) % g.k);
+    const int co = (int)(e / ((int64_t)g.ci * g.k * g.k));
+    const bf16 v = (bf16)g.w[co * g.s_co + ci * g.s_ci + kh * g.s_kh + kw * g.s_kw];
+    g.wb[e] = v;
+    if (g.wf) g.wf[(((int64_t)ci * g.k + (g.k - 1 - kh)) * g.k + (g.k - 1 - kw)) * g.co + co] = v;
+  } else if (g.bb && e < nw + g.co) {
+    g.bb[e - nw] = (bf16)g.b[e - nw];
+  }
+}
+
 }  // namespace siren

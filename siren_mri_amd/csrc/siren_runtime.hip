@@ -20,6 +20,7 @@
 #include "siren_encoder.hip"
 #include "siren_conv.hip"
 #include "siren_f64.hip"
+#include "siren_hyper.hip"
 
 using namespace siren;
 
@@ -1562,6 +1563,259 @@ int jvp_backward_impl(const siren_mlp_desc* d, int order, const float* x, const 
 
 }  // namespace
 
+// ------------------------------------------------------------------ hypernetwork heads
+namespace {
+constexpr int HY_KCH = 512;  // K per split of the wide output layers' input gradient
+
+int hyper_check(const siren_hyper_desc* d) {
+  if (!d) return fail(SIREN_EINVAL, "null hyper descriptor");
+  if (d->heads < 1 || d->heads > SIREN_HYPER_MAXG) return fail(SIREN_EINVAL, "hyper: %d heads (1..%d)", d->heads, SIREN_HYPER_MAXG);
+  if (d->depth < 1 || d->depth > SIREN_HYPER_MAXD) return fail(SIREN_EINVAL, "hyper: depth %d (1..%d)", d->depth, SIREN_HYPER_MAXD);
+  if (d->rows < 1 || d->in_features < 1 || d->hidden < 1) return fail(SIREN_EINVAL, "hyper: empty shape");
+  for (int g = 0; g < d->heads; ++g) {
+    if (d->out_features[g] < 1) return fail(SIREN_EINVAL, "hyper: head %d has no outputs", g);
+    for (int l = 0; l <= d->depth; ++l)
+      if (!d->weight[g * 5 + l] || !d->bias[g * 5 + l]) return fail(SIREN_EINVAL, "hyper: head %d layer %d null", g, l);
+  }
+  return SIREN_OK;
+}
+int64_t hyper_act(const siren_hyper_desc* d) { return (int64_t)d->rows * d->hidden; }
+int hyper_nsplit(int n) { return (n + HY_KCH - 1) / HY_KCH; }
+struct HyperWs {
+  int64_t dz_off[2], part_off[SIREN_HYPER_MAXG], dzg_off, bytes;
+};
+HyperWs hyper_ws(const siren_hyper_desc* d) {
+  HyperWs w;
+  int64_t off = 0;
+  const int64_t act = hyper_act(d) * 4 * d->heads;
+  for (int k = 0; k < 2; ++k) {
+    w.dz_off[k] = off;
+    off = align_up(off + act, 256);
+  }
+  for (int g = 0; g < d->heads; ++g) {
+    w.part_off[g] = off;
+    off = align_up(off + (int64_t)hyper_nsplit(d->out_features[g]) * hyper_act(d) * 4, 256);
+  }
+  w.dzg_off = off;
+  off = align_up(off + (int64_t)d->heads * d->rows * d->in_features * 4, 256);
+  w.bytes = off;
+  return w;
+}
+// tiles of one group (split: the number of K splits of HY_PART); BM 32 tiles (32 x 128) when every
+// group has at most 32 rows, else 64 x 64
+int hy_tiles(int M, int N, int split, int bm) { return (int)(cdiv(M, bm) * cdiv(N, 4096 / bm)) * split; }
+
+template <int TA, int TB, int EPI>
+int hy_launch(HyArgs& a, hipStream_t st) {
+  int bm = 32;
+  for (int g = 0; g < a.ng; ++g)
+    if (a.g[g].M > 32) bm = 64;
+  int t = 0;
+  for (int g = 0; g < a.ng; ++g) {
+    HyGroup& G = a.g[g];
+    G.tile0 = t;
+    const int ns = EPI == HY_PART ? (G.K + G.ksplit - 1) / G.ksplit : 1;
+    t += hy_tiles(G.M, G.N, ns, bm);
+  }
+  a.ntiles = t;
+  if (bm == 32) hipLaunchKernelGGL((hy_gemm_kernel<TA, TB, EPI, 32>), dim3((unsigned)t), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((hy_gemm_kernel<TA, TB, EPI, 64>), dim3((unsigned)t), dim3(256), 0, st, a);
+  return check_launch("hy_gemm");
+}
+}  // namespace
+
+extern "C" {
+
+int64_t siren_hyper_saved_bytes(const siren_hyper_desc* d) {
+  if (hyper_check(d)) return -1;
+  return (int64_t)d->heads * d->depth * hyper_act(d) * 4;
+}
+
+int64_t siren_hyper_workspace_bytes(const siren_hyper_desc* d) {
+  if (hyper_check(d)) return -1;
+  return hyper_ws(d).bytes;
+}
+
+int siren_hyper_forward(const siren_hyper_desc* d, const float* z, float* const* out, void* saved, int64_t saved_bytes,
+                        void* stream) {
+  int rc = hyper_check(d);
+  if (rc) return rc;
+  if (!z || !out || !saved) return fail(SIREN_EINVAL, "hyper forward: null argument");
+  if (saved_bytes < siren_hyper_saved_bytes(d)) return fail(SIREN_ENOSPACE, "hyper forward: saved buffer too small");
+  hipStream_t st = (hipStream_t)stream;
+  const int G = d->heads, D = d->depth, B = d->rows, H = d->hidden;
+  float* hs = (float*)saved;  // H_{l+1}[g] at hs + (g * D + l) * B * H
+  auto hbuf = [&](int g, int l) { return hs + ((int64_t)g * D + l) * B * H; };
+  for (int l = 0; l < D; ++l) {
+    HyArgs a;
+    memset(&a, 0, sizeof(a));
+    a.ng = G;
+    for (int g = 0; g < G; ++g) {
+      HyGroup& q = a.g[g];
+      const int K = l == 0 ? d->in_features : H;
+      q.A = l == 0 ? z : hbuf(g, l - 1);
+      q.lda = K;
+      q.B = d->weight[g * 5 + l];
+      q.ldb = K;
+      q.bias = d->bias[g * 5 + l];
+      q.C = hbuf(g, l);
+      q.ldc = H;
+      q.M = B;
+      q.N = H;
+      q.K = K;
+    }
+    if ((rc = hy_launch<0, 0, HY_BIAS_RELU>(a, st))) return rc;
+  }
+  HyArgs a;
+  memset(&a, 0, sizeof(a));
+  a.ng = G;
+  for (int g = 0; g < G; ++g) {
+    if (!out[g]) return fail(SIREN_EINVAL, "hyper forward: head %d null output", g);
+    HyGroup& q = a.g[g];
+    q.A = hbuf(g, D - 1);
+    q.lda = H;
+    q.B = d->weight[g * 5 + D];
+    q.ldb = H;
+    q.bias = d->bias[g * 5 + D];
+    q.C = out[g];
+    q.ldc = d->out_features[g];
+    q.M = B;
+    q.N = d->out_features[g];
+    q.K = H;
+  }
+  return hy_launch<0, 0, HY_BIAS>(a, st);
+}
+
+int siren_hyper_backward(const siren_hyper_desc* d, const float* z, const float* const* dout, const void* saved,
+                         int64_t saved_bytes, void* workspace, int64_t workspace_bytes, float* const* dW,
+                         float* const* db, float* dz, void* stream) {
+  int rc = hyper_check(d);
+  if (rc) return rc;
+  if (!z || !dout || !saved || !dW || !db) return fail(SIREN_EINVAL, "hyper backward: null argument");
+  if (saved_bytes < siren_hyper_saved_bytes(d)) return fail(SIREN_ENOSPACE, "hyper backward: saved buffer too small");
+  const HyperWs w = hyper_ws(d);
+  if (!workspace || workspace_bytes < w.bytes) return fail(SIREN_ENOSPACE, "hyper backward: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const int G = d->heads, D = d->depth, B = d->rows, H = d->hidden, IN = d->in_features;
+  const float* hs = (const float*)saved;
+  auto hbuf = [&](int g, int l) { return hs + ((int64_t)g * D + l) * B * H; };
+  char* ws = (char*)workspace;
+  auto dzbuf = [&](int k, int g) { return (float*)(ws + w.dz_off[k]) + (int64_t)g * B * H; };
+  for (int g = 0; g < G; ++g)
+    for (int l = 0; l <= D; ++l)
+      if (!dW[g * 5 + l] || !db[g * 5 + l]) return fail(SIREN_EINVAL, "hyper backward: head %d layer %d null grad", g, l);
+  // output layers: [dW | db] = dout^T [H_D | 1]
+  {
+    HyArgs a;
+    memset(&a, 0, sizeof(a));
+    a.ng = G;
+    for (int g = 0; g < G; ++g) {
+      HyGroup& q = a.g[g];
+      q.A = dout[g];
+      q.lda = d->out_features[g];
+      q.B = hbuf(g, D - 1);
+      q.ldb = H;
+      q.C = dW[g * 5 + D];
+      q.ldc = H;
+      q.db = db[g * 5 + D];
+      q.M = d->out_features[g];
+      q.N = H;
+      q.K = B;
+    }
+    if ((rc = hy_launch<1, 1, HY_DWDB>(a, st))) return rc;
+  }
+  // their input gradients dout W over K splits, then dZ_{D-1} = sum * (H_D > 0)
+  {
+    HyArgs a;
+    memset(&a, 0, sizeof(a));
+    a.ng = G;
+    HyPartArgs r;
+    memset(&r, 0, sizeof(r));
+    r.ng = G;
+    r.n = (int64_t)B * H;
+    for (int g = 0; g < G; ++g) {
+      HyGroup& q = a.g[g];
+      q.A = dout[g];
+      q.lda = d->out_features[g];
+      q.B = d->weight[g * 5 + D];
+      q.ldb = H;
+      q.C = (float*)(ws + w.part_off[g]);
+      q.ldc = H;
+      q.M = B;
+      q.N = H;
+      q.K = d->out_features[g];
+      q.ksplit = HY_KCH;
+      r.part[g] = q.C;
+      r.relu_out[g] = hbuf(g, D - 1);
+      r.dz[g] = dzbuf(0, g);
+      r.nsplit[g] = hyper_nsplit(d->out_features[g]);
+    }
+    if ((rc = hy_launch<0, 1, HY_PART>(a, st))) return rc;
+    hipLaunchKernelGGL(hy_part_kernel, dim3((unsigned)cdiv(r.n, 256), (unsigned)G), dim3(256), 0, st, r);
+    if ((rc = check_launch("hy_part"))) return rc;
+  }
+  int cur = 0;
+  for (int l = D - 1; l >= 0; --l) {
+    const int K = l == 0 ? IN : H;
+    HyArgs a;
+    memset(&a, 0, sizeof(a));
+    a.ng = G;
+    for (int g = 0; g < G; ++g) {
+      HyGroup& q = a.g[g];
+      q.A = dzbuf(cur, g);
+      q.lda = H;
+      q.B = l == 0 ? z : hbuf(g, l - 1);
+      q.ldb = K;
+      q.C = dW[g * 5 + l];
+      q.ldc = K;
+      q.db = db[g * 5 + l];
+      q.M = H;
+      q.N = K;
+      q.K = B;
+    }
+    if ((rc = hy_launch<1, 1, HY_DWDB>(a, st))) return rc;
+    if (l == 0 && !dz) break;
+    HyArgs b;
+    memset(&b, 0, sizeof(b));
+    b.ng = G;
+    for (int g = 0; g < G; ++g) {
+      HyGroup& q = b.g[g];
+      q.A = dzbuf(cur, g);
+      q.lda = H;
+      q.B = d->weight[g * 5 + l];
+      q.ldb = K;
+      q.M = B;
+      q.N = K;
+      q.K = H;
+      if (l > 0) {
+        q.aux = hbuf(g, l - 1);
+        q.C = dzbuf(cur ^ 1, g);
+        q.ldc = H;
+      } else {
+        q.C = (float*)(ws + w.dzg_off) + (int64_t)g * B * IN;
+        q.ldc = IN;
+      }
+    }
+    if (l > 0) {
+      if ((rc = hy_launch<0, 1, HY_MASK>(b, st))) return rc;
+      cur ^= 1;
+    } else {
+      if ((rc = hy_launch<0, 1, HY_PLAIN>(b, st))) return rc;
+      HySumArgs sa;
+      memset(&sa, 0, sizeof(sa));
+      sa.ng = G;
+      sa.n = (int64_t)B * IN;
+      sa.out = dz;
+      for (int g = 0; g < G; ++g) sa.src[g] = (const float*)(ws + w.dzg_off) + (int64_t)g * B * IN;
+      hipLaunchKernelGGL(hy_sum_kernel, dim3((unsigned)cdiv(sa.n, 256)), dim3(256), 0, st, sa);
+      if ((rc = check_launch("hy_sum"))) return rc;
+    }
+  }
+  return SIREN_OK;
+}
+
+}  // extern "C"
+
 namespace {
 // ------------------------------------------------------------------ fp64 stack (siren_f64.hip)
 struct F64Layout {
@@ -2353,6 +2607,39 @@ int siren_conv_wrw(const void* x, const void* dy, int N, int H, int W, int CI, i
   else { if (CI == 64) SIREN_CW(7, 64, 4) else SIREN_CW(7, 128, 2) }
 #undef SIREN_CW
   return check_launch("conv_wrw_gen_reduce");
+}
+
+int siren_enc_prep(int n, const float* const* w, const float* const* b, const int64_t* geom, void* const* wb,
+                   void* const* wf, void* const* bb, void* stream) {
+  if (n < 1 || n > ENC_PREP_MAX) return fail(SIREN_EINVAL, "enc_prep: %d filters (1..%d)", n, ENC_PREP_MAX);
+  if (!w || !geom || !wb) return fail(SIREN_EINVAL, "enc_prep: null table");
+  EncPrepArgs a;
+  memset(&a, 0, sizeof(a));
+  a.nseg = n;
+  int64_t t = 0;
+  for (int i = 0; i < n; ++i) {
+    EncPrepSeg& g = a.seg[i];
+    const int64_t* q = geom + 7 * i;
+    g.co = (int)q[0];
+    g.ci = (int)q[1];
+    g.k = (int)q[2];
+    g.s_co = q[3];
+    g.s_ci = q[4];
+    g.s_kh = q[5];
+    g.s_kw = q[6];
+    if (g.co < 1 || g.ci < 1 || g.k < 1) return fail(SIREN_EINVAL, "enc_prep: filter %d shape", i);
+    g.w = w[i];
+    g.b = b ? b[i] : nullptr;
+    g.wb = (bf16*)wb[i];
+    g.wf = wf ? (bf16*)wf[i] : nullptr;
+    g.bb = bb ? (bf16*)bb[i] : nullptr;
+    if (!g.w || !g.wb || (g.bb && !g.b)) return fail(SIREN_EINVAL, "enc_prep: filter %d null pointer", i);
+    g.begin = t;
+    t += (int64_t)g.co * g.ci * g.k * g.k + (g.bb ? g.co : 0);
+  }
+  a.total = t;
+  hipLaunchKernelGGL(enc_prep_kernel, dim3((unsigned)cdiv(t, 256)), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("enc_prep");
 }
 
 int siren_enc_relu_bwd(const void* g1, const void* g2, const void* y, void* out, float* db, int64_t P, int C, void* ws,

@@ -60,6 +60,28 @@ def _w_bf16(w):
     return w.detach().to(torch.bfloat16).contiguous(memory_format=_CL)
 
 
+def _prep_operands(convs, dev, stream):
+    """Every convolution's bf16 channels-last filter, its input gradient's flipped / transposed bf16
+    filter (none for conv_theta: no gradient into the image) and its bf16 bias, in one launch
+    (siren_enc_prep; the casts of _w_bf16 / _w_flip / .to(torch.bfloat16), bit for bit)."""
+    import ctypes
+    n = len(convs)
+    wbs, wfs, bbs, geom = [], [], [], []
+    for i, c in enumerate(convs):
+        co, ci, kh, kw = c.weight.shape
+        wbs.append(torch.empty((co, ci, kh, kw), dtype=torch.bfloat16, device=dev, memory_format=_CL))
+        wfs.append(torch.empty((ci, co, kh, kw), dtype=torch.bfloat16, device=dev, memory_format=_CL) if i else None)
+        bbs.append(torch.empty(co, dtype=torch.bfloat16, device=dev))
+        geom += [co, ci, kh, *c.weight.stride()]
+    VP = ctypes.c_void_p * n
+    _native.check(_native.lib().siren_enc_prep(
+        n, VP(*[c.weight.data_ptr() for c in convs]), VP(*[c.bias.data_ptr() for c in convs]),
+        (ctypes.c_int64 * (7 * n))(*geom), VP(*[t.data_ptr() for t in wbs]),
+        VP(*[t.data_ptr() if t is not None else None for t in wfs]), VP(*[t.data_ptr() for t in bbs]), stream),
+        "siren_enc_prep")
+    return wbs, wfs, bbs
+
+
 def _w_flip(wb):
     """Filter of the input gradient as a forward convolution: W'[ci][co] = W[co][ci] rotated 180."""
     return wb.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL)
@@ -159,8 +181,8 @@ class _EncoderBF16(torch.autograd.Function):
         stream = _native.stream_handle(dev)
         ws = _native.enc_workspace(dev)
         convs = ctx.convs = enc._enc_layers
-        wbs = [_w_bf16(c.weight) for c in convs]
-        bbs = [c.bias.detach().to(torch.bfloat16) for c in convs]
+        wbs, wfs, bbs = _prep_operands(convs, dev, stream)
+        ctx.wfs = wfs
         x0 = I.detach().to(torch.bfloat16).contiguous(memory_format=_CL)
         saved = [x0]
 
@@ -230,7 +252,7 @@ class _EncoderBF16(torch.autograd.Function):
         xin = saved[-1]  # the 1x1 conv's input (the last block's output, or cnn[0]'s)
         pad = convs[k].padding[0]
         gW[k] = _wgrad(ga, xin, wbs[k], pad)
-        g1 = _conv(ga, _w_flip(wbs[k]), None, pad)
+        g1 = _conv(ga, ctx.wfs[k], None, pad)
         g2 = None
         # residual blocks, last to first
         for _ in range(enc._enc_nblocks):
@@ -249,7 +271,7 @@ class _EncoderBF16(torch.autograd.Function):
                                                 gb[k + 1].data_ptr(), P, C, wsp, wsn, stream), "siren_enc_res_bwd")
             pad = convs[k + 1].padding[0]
             gW[k + 1] = _wgrad(ga, h, wbs[k + 1], pad)
-            gh = _conv(ga, _w_flip(wbs[k + 1]), None, pad)
+            gh = _conv(ga, ctx.wfs[k + 1], None, pad)
             ghm = torch.empty_like(h)
             P, C = _plane(h)
             gb[k] = torch.empty(C, dtype=torch.float32, device=dev)
@@ -257,7 +279,7 @@ class _EncoderBF16(torch.autograd.Function):
                                                  P, C, wsp, wsn, stream), "siren_enc_relu_bwd")
             pad = convs[k].padding[0]
             gW[k] = _wgrad(ghm, t, wbs[k], pad)
-            g1 = _conv(ghm, _w_flip(wbs[k]), None, pad)
+            g1 = _conv(ghm, ctx.wfs[k], None, pad)
             g2 = gskip
         # cnn[0] and conv_theta (each followed by a ReLU); no gradient into the image
         for k in (1, 0):
@@ -272,7 +294,7 @@ class _EncoderBF16(torch.autograd.Function):
             pad = convs[k].padding[0]
             gW[k] = _wgrad(gm, xin, wbs[k], pad)
             if k == 1:
-                g1 = _conv(gm, _w_flip(wbs[k]), None, pad)
+                g1 = _conv(gm, ctx.wfs[k], None, pad)
                 g2 = None
         grads = []
         for k, c in enumerate(convs):

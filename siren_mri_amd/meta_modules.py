@@ -7,7 +7,9 @@ SIREN stack batched, per-slice weights (configs 4/5).
 
 The hypo-network is a SingleBVPNet whose forward receives the HyperNetwork's parameter dict
 ({'net.net.i.0.weight': [B, out, in], ...}); the native stack runs all B slices in one call with
-batched weights. The encoder and the HyperNetwork's ReLU MLPs are plain PyTorch-ROCm modules.
+batched weights. The HyperNetwork's heads (one ReLU MLP per hypo-parameter) run as grouped native
+GEMMs on CUDA fp32 (siren_hyper_forward / _backward: every head's layer of one depth in one launch);
+the encoder is ConvImgEncoder (modules.py).
 Deviation (bug 0.5): constructors take no `device=` argument (the reference scripts pass one the
 reference constructor does not accept).
 """
@@ -62,11 +64,117 @@ class HyperNetwork(nn.Module):
             elif "bias" in name:
                 hn.net[-1].apply(hyper_bias_init)
 
+    def _native_layers(self, z):
+        """Per head the Linear layers [hidden..., output] when the grouped native heads take this
+        call (CUDA fp32 latent [B, in], plain ReLU FCBlocks of one hidden width); else None."""
+        if not (z.is_cuda and z.dtype == torch.float32 and z.dim() == 2 and len(self.nets) <= _native_hyper_maxg()):
+            return None
+        heads = []
+        for net in self.nets:
+            if not (isinstance(net, modules.FCBlock) and net.nonlinearity == "relu" and net.outermost_linear):
+                return None
+            lins = [net.net[i][0] for i in range(len(net.net))]
+            if not 2 <= len(lins) <= 5 or any(type(m) is not modules.BatchLinear or m.bias is None for m in lins):
+                return None
+            if any(p.dtype != torch.float32 or p.device != z.device for m in lins for p in (m.weight, m.bias)):
+                return None
+            heads.append(lins)
+        hid = heads[0][0].weight.shape[0]
+        depth = len(heads[0]) - 1
+        for lins in heads:
+            if len(lins) - 1 != depth or lins[0].weight.shape[1] != z.shape[1]:
+                return None
+            if any(m.weight.shape[0] != hid for m in lins[:-1]) or any(m.weight.shape[1] != hid for m in lins[1:]):
+                return None
+        return heads
+
     def forward(self, z):
+        heads = self._native_layers(z)
+        if heads is not None:
+            flat = [t for lins in heads for m in lins for t in (m.weight, m.bias)]
+            outs = _HyperHeads.apply(len(heads), len(heads[0]) - 1, z, *flat)
+            return OrderedDict((name, o.reshape((-1,) + tuple(shape)))
+                               for name, o, shape in zip(self.names, outs, self.param_shapes))
         params = OrderedDict()
         for name, net, shape in zip(self.names, self.nets, self.param_shapes):
             params[name] = net(z).reshape((-1,) + tuple(shape))
         return params
+
+
+def _native_hyper_maxg():
+    from . import _native
+    return _native.HYPER_MAXG
+
+
+class _HyperHeads(torch.autograd.Function):
+    """All heads of a HyperNetwork (meta_modules.py:48-54) in grouped native launches: forward
+    siren_hyper_forward (ReLU outputs kept), backward siren_hyper_backward (every dW / db and the
+    latent's gradient summed over the heads in head order). Same fp32 arithmetic as the per-head
+    Linear + ReLU chain up to summation order."""
+
+    @staticmethod
+    def _desc(G, D, z, params):
+        from . import _native
+        d = _native.SirenHyperDesc()
+        d.heads, d.depth, d.rows, d.in_features = G, D, z.shape[0], z.shape[1]
+        d.hidden = params[0].shape[0]
+        for g in range(G):
+            for l in range(D + 1):
+                W, b = params[2 * (g * (D + 1) + l)], params[2 * (g * (D + 1) + l) + 1]
+                d.weight[g * 5 + l] = W.data_ptr()
+                d.bias[g * 5 + l] = b.data_ptr()
+            d.out_features[g] = params[2 * (g * (D + 1) + D)].shape[0]
+        return d
+
+    @staticmethod
+    def forward(ctx, G, D, z, *params):
+        import ctypes
+        from . import _native
+        lib = _native.lib()
+        zc = z.detach().contiguous()
+        ps = [p.detach().contiguous() for p in params]
+        d = _HyperHeads._desc(G, D, zc, ps)
+        saved = torch.empty(int(lib.siren_hyper_saved_bytes(ctypes.byref(d))) // 4, dtype=torch.float32, device=z.device)
+        outs = [torch.empty(zc.shape[0], d.out_features[g], dtype=torch.float32, device=z.device) for g in range(G)]
+        VP = ctypes.c_void_p * G
+        _native.check(lib.siren_hyper_forward(ctypes.byref(d), zc.data_ptr(), VP(*[o.data_ptr() for o in outs]),
+                                              saved.data_ptr(), saved.numel() * 4, _native.stream_handle(z.device)),
+                      "siren_hyper_forward")
+        ctx.G, ctx.D = G, D
+        ctx.save_for_backward(zc, saved, *ps)
+        ctx.set_materialize_grads(False)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *douts):
+        import ctypes
+        from . import _native
+        if torch.is_grad_enabled():
+            raise RuntimeError("siren_mri_amd: second derivatives of the native HyperNetwork heads are not provided")
+        G, D = ctx.G, ctx.D
+        t = ctx.saved_tensors
+        z, saved, ps = t[0], t[1], list(t[2:])
+        lib = _native.lib()
+        d = _HyperHeads._desc(G, D, z, ps)
+        gs = [g.contiguous() if g is not None else torch.zeros(z.shape[0], d.out_features[i], device=z.device)
+              for i, g in enumerate(douts)]
+        ws = torch.empty(int(lib.siren_hyper_workspace_bytes(ctypes.byref(d))), dtype=torch.uint8, device=z.device)
+        grads = [torch.empty_like(p) for p in ps]
+        NW = G * 5
+        dWp = (ctypes.c_void_p * NW)()
+        dbp = (ctypes.c_void_p * NW)()
+        for g in range(G):
+            for l in range(D + 1):
+                k = 2 * (g * (D + 1) + l)
+                dWp[g * 5 + l] = grads[k].data_ptr()
+                dbp[g * 5 + l] = grads[k + 1].data_ptr()
+        need_z = ctx.needs_input_grad[2]
+        dz = torch.empty_like(z) if need_z else None
+        _native.check(lib.siren_hyper_backward(ctypes.byref(d), z.data_ptr(), (ctypes.c_void_p * G)(*[g.data_ptr() for g in gs]),
+                                               saved.data_ptr(), saved.numel() * 4, ws.data_ptr(), ws.numel(), dWp, dbp,
+                                               dz.data_ptr() if need_z else None, _native.stream_handle(z.device)),
+                      "siren_hyper_backward")
+        return (None, None, dz, *grads)
 
 
 class ConvolutionalNeuralProcessImplicit2DHypernetFourierFeatures(nn.Module):

@@ -328,3 +328,22 @@ def test_c4_encoder_has_no_miopen_7x7():
     assert encoder._native_gen(0, x, wb) and encoder._native_gen(1, x, wb)
     g = torch.empty(2, 128, 128, 128, dtype=torch.bfloat16, device=DEV).contiguous(memory_format=torch.channels_last)
     assert encoder._native_gen(0, g, encoder._w_flip(wb))
+
+
+def test_operand_prep_equals_the_casts():
+    """siren_enc_prep (one launch per step) == _w_bf16 / _w_flip / .to(torch.bfloat16), bit for bit,
+    for every convolution of the encoder (contiguous and channels-last fp32 filters)."""
+    from siren_mri_amd import _native, encoder
+    enc = _encoder("bf16", blocks=1, hidden=128, k=7)
+    convs = enc._layers()
+    convs[1].weight.data = convs[1].weight.data.contiguous(memory_format=torch.channels_last)
+    wbs, wfs, bbs = encoder._prep_operands(convs, DEV, _native.stream_handle(DEV))
+    for i, c in enumerate(convs):
+        ref = encoder._w_bf16(c.weight)
+        assert torch.equal(wbs[i], ref) and wbs[i].is_contiguous(memory_format=torch.channels_last), i
+        assert torch.equal(bbs[i], c.bias.detach().to(torch.bfloat16)), i
+        if i:
+            rf = encoder._w_flip(ref)
+            assert torch.equal(wfs[i], rf) and wfs[i].stride() == rf.stride(), i
+        else:
+            assert wfs[i] is None
