@@ -6,8 +6,8 @@
 // One kernel, hy_gemm_kernel<TA, TB, EPI, BM>, over a table of groups (<= HY_MAXG): workgroup tiles
 // are dealt to groups by a prefix over the groups' tile counts. A 64 x 64 (or, for the heads'
 // <= 32-row batches, 32 x 128) output tile per 256-thread workgroup, 4 x 4 per thread, K in
-// 16-deep LDS stages, fp32 FMA (the reference's fp32 arithmetic; only the summation order differs
-// from the library GEMM). Epilogues:
+// 64-deep LDS stages (a K = 128 layer in two: few dependent load rounds), fp32 FMA (the
+// reference's fp32 arithmetic; only the summation order differs from the library GEMM). Epilogues:
 //   HY_BIAS_RELU  C = relu(A B + bias)            the heads' hidden layers
 //   HY_BIAS       C = A B + bias                  the heads' output layers
 //   HY_DWDB       C = A B, db[m] = sum_k A(m, k) (kept beside the K loop by the first column tile)
@@ -45,7 +45,7 @@ enum { HY_BIAS_RELU = 0, HY_BIAS = 1, HY_DWDB = 2, HY_PART = 3, HY_MASK = 4, HY_
 // per thread: rows tm + (BM / 4) i, columns tn + (BN / 4) j
 template <int TA, int TB, int EPI, int BM>
 __global__ __launch_bounds__(256) void hy_gemm_kernel(HyArgs a) {
-  constexpr int BN = 4096 / BM, BK = 16, SM = BM / 4, SN = BN / 4;
+  constexpr int BN = 4096 / BM, BK = 64, SM = BM / 4, SN = BN / 4;
   static_assert(BM == 32 || BM == 64, "tile");
   __shared__ float As[BK][BM + 1];
   __shared__ float Bs[BK][BN + 1];
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(256) void hy_gemm_kernel(HyArgs a) {
     for (int q = 0; q < BM * BK / 256; ++q) {
       const int e = tid + 256 * q;
       int mm, kk;
-      if (TA == 0) { kk = e & 15; mm = e >> 4; }
+      if (TA == 0) { kk = e % BK; mm = e / BK; }
       else { mm = e % BM; kk = e / BM; }
       const int m = m0 + mm, k = kb + kk;
       float v = 0.f;
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256) void hy_gemm_kernel(HyArgs a) {
     for (int q = 0; q < BN * BK / 256; ++q) {
       const int e = tid + 256 * q;
       int nn, kk;
-      if (TB == 0) { kk = e & 15; nn = e >> 4; }
+      if (TB == 0) { kk = e % BK; nn = e / BK; }
       else { nn = e % BN; kk = e / BN; }
       const int n = n0 + nn, k = kb + kk;
       float v = 0.f;

@@ -1607,9 +1607,14 @@ int hy_tiles(int M, int N, int split, int bm) { return (int)(cdiv(M, bm) * cdiv(
 
 template <int TA, int TB, int EPI>
 int hy_launch(HyArgs& a, hipStream_t st) {
-  int bm = 32;
-  for (int g = 0; g < a.ng; ++g)
-    if (a.g[g].M > 32) bm = 64;
+  // 32 x 128 tiles when every group has <= 32 rows and they still give >= 128 workgroups
+  int bm = 32, t32 = 0;
+  for (int g = 0; g < a.ng; ++g) {
+    const HyGroup& G = a.g[g];
+    if (G.M > 32) bm = 64;
+    t32 += hy_tiles(G.M, G.N, EPI == HY_PART ? (G.K + G.ksplit - 1) / G.ksplit : 1, 32);
+  }
+  if (t32 < 128) bm = 64;
   int t = 0;
   for (int g = 0; g < a.ng; ++g) {
     HyGroup& G = a.g[g];
