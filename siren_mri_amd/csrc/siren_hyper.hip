@@ -6,8 +6,9 @@
 // One kernel, hy_gemm_kernel<TA, TB, EPI, BM>, over a table of groups (<= HY_MAXG): workgroup tiles
 // are dealt to groups by a prefix over the groups' tile counts. A 64 x 64 (or, for the heads'
 // <= 32-row batches, 32 x 128) output tile per 256-thread workgroup, 4 x 4 per thread, K in
-// 64-deep LDS stages (a K = 128 layer in two: few dependent load rounds), fp32 FMA (the
-// reference's fp32 arithmetic; only the summation order differs from the library GEMM). Epilogues:
+// 16-deep LDS stages (64-deep stages measured slower: 232 VGPRs, two workgroups per CU), fp32 FMA
+// (the reference's fp32 arithmetic; only the summation order differs from the library GEMM).
+// Epilogues:
 //   HY_BIAS_RELU  C = relu(A B + bias)            the heads' hidden layers
 //   HY_BIAS       C = A B + bias                  the heads' output layers
 //   HY_DWDB       C = A B, db[m] = sum_k A(m, k) (kept beside the K loop by the first column tile)
@@ -45,7 +46,7 @@ enum { HY_BIAS_RELU = 0, HY_BIAS = 1, HY_DWDB = 2, HY_PART = 3, HY_MASK = 4, HY_
 // per thread: rows tm + (BM / 4) i, columns tn + (BN / 4) j
 template <int TA, int TB, int EPI, int BM>
 __global__ __launch_bounds__(256) void hy_gemm_kernel(HyArgs a) {
-  constexpr int BN = 4096 / BM, BK = 64, SM = BM / 4, SN = BN / 4;
+  constexpr int BN = 4096 / BM, BK = 16, SM = BM / 4, SN = BN / 4;
   static_assert(BM == 32 || BM == 64, "tile");
   __shared__ float As[BK][BM + 1];
   __shared__ float Bs[BK][BN + 1];
