@@ -398,7 +398,9 @@ class ConvImgEncoder(nn.Module):
                     if isinstance(m, nn.Conv2d):
                         m.weight.data = m.weight.data.contiguous(memory_format=torch.channels_last)
                 self._nhwc = True
-            if encoder.fused_enabled() and self._layers() is not None:
+            # the fused node gives no gradient into the image: an image that requires one takes
+            # the autocast chain
+            if encoder.fused_enabled() and self._layers() is not None and not I.requires_grad:
                 return encoder.encoder_bf16(self, I)
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 o = self.relu(self.conv_theta(I.contiguous(memory_format=torch.channels_last)))

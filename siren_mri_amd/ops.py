@@ -277,11 +277,18 @@ def _differentiable_backward(ctx, dy, x, saved, ws, bs, need_dx):
     dx = None
     if need_dx:
         if not outermost_linear or x.shape[-1] > 4:
-            raise RuntimeError(
-                "siren_mri_amd: a differentiable SIREN input gradient (create_graph=True) needs "
-                "outermost_linear=True and in_features <= 4 (the tangent-stream kernels)")
-        J = jacobian_of(x, ws, bs, w0, prec, batched)
-        dx = (J * dy.unsqueeze(-1)).sum(-2)
+            # no tangent-stream form for this stack: the native first-order input gradient, which
+            # raises only if it is differentiated again
+            with torch.no_grad():
+                dx, _, _ = torch.ops.siren_mri_amd.sine_mlp_bwd(dy, x, ws, bs, saved, w0, prec, outermost_linear,
+                                                                batched, True)
+            dx = guard_higher_order([dx], [dy, x, *ws, *bs],
+                                    "siren_mri_amd: a differentiable SIREN input gradient (create_graph=True) "
+                                    "needs outermost_linear=True and in_features <= 4 (the tangent-stream "
+                                    "kernels)")[0]
+        else:
+            J = jacobian_of(x, ws, bs, w0, prec, batched)
+            dx = (J * dy.unsqueeze(-1)).sum(-2)
     need_w = any(ctx.needs_input_grad[2:])
     dW, db = [None] * n, [None] * n
     if need_w:

@@ -347,3 +347,22 @@ def test_operand_prep_equals_the_casts():
             assert torch.equal(wfs[i], rf) and wfs[i].stride() == rf.stride(), i
         else:
             assert wfs[i] is None
+
+
+def test_image_gradient_takes_the_autocast_chain():
+    """An image that requires a gradient goes through the autocast chain (the fused node gives
+    none): a real gradient, the chain's with the node switched off (MIOpen's convolutions are not
+    bit-reproducible run to run: 1e-3)."""
+    from siren_mri_amd import encoder
+    enc = _encoder("bf16", blocks=1, hidden=64, k=5)
+    I = torch.randn(2, 2, 128, 128, generator=torch.Generator().manual_seed(4)).to(DEV).requires_grad_(True)
+    enc(I).square().sum().backward()
+    g_on = I.grad.clone()
+    assert g_on.abs().sum() > 0
+    I.grad = None
+    encoder.set_fused(False)
+    try:
+        enc(I).square().sum().backward()
+    finally:
+        encoder.set_fused(True)
+    assert orc.norm_rel(g_on.cpu(), I.grad.cpu()) < 1e-3

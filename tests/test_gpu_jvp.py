@@ -397,3 +397,22 @@ def test_fused_adjoint_combine_matches_two_launches(order, precision, batched):
     for a, b in zip(g1, gt):
         assert orc.norm_rel(a.cpu(), b.cpu()) < 1e-6
     assert torch.equal(dx1, dxt)
+
+
+def test_create_graph_first_order_dx_without_tangent_form():
+    """create_graph=True on a stack the tangent-stream kernels do not take (a sine output layer):
+    the input gradient is the native first-order one (equal to create_graph=False), and only
+    differentiating it again raises."""
+    from siren_mri_amd.ops import siren_mlp
+    g = torch.Generator().manual_seed(3)
+    ws = [(torch.randn(64, 2, generator=g) * 0.5).to(DEV).requires_grad_(True),
+          (torch.randn(1, 64, generator=g) * 0.1).to(DEV).requires_grad_(True)]
+    bs = [torch.zeros(64, device=DEV).requires_grad_(True), torch.zeros(1, device=DEV).requires_grad_(True)]
+    x = (torch.rand(1, 500, 2, generator=g) * 2 - 1).to(DEV).requires_grad_(True)
+    y = siren_mlp(x, ws, bs, outermost_linear=False)
+    d1 = torch.autograd.grad(y.sum(), x, create_graph=True)[0]
+    y2 = siren_mlp(x, ws, bs, outermost_linear=False)
+    d0 = torch.autograd.grad(y2.sum(), x)[0]
+    assert torch.equal(d1.detach(), d0)
+    with pytest.raises(RuntimeError, match="tangent-stream"):
+        d1.square().sum().backward()
