@@ -158,8 +158,13 @@ class Adam(torch.optim.Adam):
                     self._dev_step[id(group)] = dev
                 key = (float(group["lr"]), float(beta1), float(beta2))
                 tables = self.__dict__.setdefault("_tables", {})
+                # replaced tables / counters stay alive: a hipGraph captured earlier may still
+                # point at them
+                retired = self.__dict__.setdefault("_retired", [])
                 tab = tables.get(id(group))
                 if tab is None or tab[0] != key:
+                    if tab is not None:
+                        retired.append(tab)
                     tab = (key, self._scalar_table(*key, params[0].device))
                     tables[id(group)] = tab
                 tab = tab[1]
@@ -197,8 +202,14 @@ class Adam(torch.optim.Adam):
                         # table form: the launch's workgroups each advance their own counter
                         nblk = lib.siren_adam_num_blocks(ctypes.byref(d))
                         cnt = dev["steps"].get(i0)
-                        if cnt is None or cnt.numel() != nblk:
-                            cnt = torch.full((max(nblk, 1),), dev["t0"], dtype=torch.float64, device=p.device)
+                        if cnt is None or cnt.numel() != max(nblk, 1):
+                            if cnt is None:
+                                cnt = torch.full((max(nblk, 1),), dev["t0"], dtype=torch.float64, device=p.device)
+                            else:
+                                # carry the device count over (no host sync; every workgroup's
+                                # counter holds the same step after a launch)
+                                self._retired.append(cnt)
+                                cnt = cnt[:1].expand(max(nblk, 1)).clone()
                             dev["steps"][i0] = cnt
                         d.dev_steps = cnt.data_ptr()
                         d.dev_table = tab.data_ptr()
