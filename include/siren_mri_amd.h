@@ -360,6 +360,15 @@ int siren_hyper_backward(const siren_hyper_desc* d, const float* z, const float*
  * may be NULL) = bf16 bias b[i] [co]; round to nearest even (torch's .to(torch.bfloat16)). */
 int siren_enc_prep(int n, const float* const* w, const float* const* b, const int64_t* geom, void* const* wb,
                    void* const* wf, void* const* bb, void* stream);
+/* Sum of squares over n (<= 32) fp32 tensors (hypo_weight_loss's sum of torch.sum(w ** 2),
+ * loss_functions.py:279-287) into the device scalar out, deterministic; ws: zeroed once, left
+ * zeroed, siren_sumsq_workspace_bytes(total elements). Backward: dst[i] = 2 g src[i] (g a device
+ * scalar). */
+int64_t siren_sumsq_workspace_bytes(int64_t total);
+int siren_sumsq_forward(int n, const float* const* src, const int64_t* numel, float* out, void* ws, int64_t ws_bytes,
+                        void* stream);
+int siren_sumsq_backward(int n, const float* const* src, const int64_t* numel, const float* g, float* const* dst,
+                         void* stream);
 int siren_enc_relu_bwd(const void* g1, const void* g2, const void* y, void* out, float* db, int64_t P, int C, void* ws,
                        int64_t ws_bytes, void* stream);
 int siren_enc_bias_relu(void* y, const void* cb, int64_t P, int C, void* stream);

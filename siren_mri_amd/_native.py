@@ -68,6 +68,9 @@ EXPORTED_SYMBOLS = (
     "siren_conv_wrw",
     "siren_enc_bias_relu",
     "siren_enc_prep",
+    "siren_sumsq_workspace_bytes",
+    "siren_sumsq_forward",
+    "siren_sumsq_backward",
     "siren_enc_relu_bwd",
     "siren_enc_res_fwd",
     "siren_enc_res_bwd",
@@ -241,6 +244,13 @@ def _declare(lib):
     lib.siren_enc_prep.argtypes = [ci, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64),
                                    ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), vp]
     lib.siren_enc_prep.restype = ci
+    lib.siren_sumsq_workspace_bytes.argtypes = [i64]
+    lib.siren_sumsq_workspace_bytes.restype = i64
+    lib.siren_sumsq_forward.argtypes = [ci, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64), vp, vp, i64, vp]
+    lib.siren_sumsq_forward.restype = ci
+    lib.siren_sumsq_backward.argtypes = [ci, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64), vp,
+                                         ctypes.POINTER(vp), vp]
+    lib.siren_sumsq_backward.restype = ci
     lib.siren_jvp_saved_bytes.argtypes = [P, ci]
     lib.siren_jvp_saved_bytes.restype = i64
     lib.siren_jvp_workspace_bytes.argtypes = [P, ci]

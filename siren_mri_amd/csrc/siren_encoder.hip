@@ -381,4 +381,74 @@ __global__ __launch_bounds__(256) void enc_prep_kernel(EncPrepArgs a) {
   }
 }
 
+// Sum of squares over a list of fp32 tensors (loss_functions.py:279-287 hypo_weight_loss's
+// sum of torch.sum(w ** 2)) and its gradient 2 g w, each one launch over every tensor (round 5;
+// ~45 pow / reduce / add / mul launches per C4 step before). Deterministic: fixed per-thread
+// order, an LDS tree per block, the block partials added in block order by the last block.
+constexpr int SUMSQ_MAX = 32;
+constexpr int SUMSQ_CHUNK = 4096;  // elements per block
+struct SumsqArgs {
+  const float* src[SUMSQ_MAX];
+  float* dst[SUMSQ_MAX];     // backward: 2 g src
+  int64_t begin[SUMSQ_MAX + 1];
+  int n;
+  float* part;               // forward: [blocks] partials
+  unsigned* counter;         // forward: zero between launches (the last block resets it)
+  float* out;                // forward: the sum
+  const float* g;            // backward: upstream gradient (device scalar)
+};
+DEV int sumsq_seg(const SumsqArgs& a, int64_t i) {
+  int s = 0;
+  while (s + 1 < a.n && i >= a.begin[s + 1]) ++s;
+  return s;
+}
+__global__ __launch_bounds__(256) void sumsq_fwd_kernel(SumsqArgs a) {
+  __shared__ float red[256];
+  __shared__ bool last;
+  const int64_t base = (int64_t)blockIdx.x * SUMSQ_CHUNK;
+  float acc = 0.f;
+  for (int k = 0; k < SUMSQ_CHUNK / 256; ++k) {
+    const int64_t i = base + k * 256 + threadIdx.x;
+    if (i < a.begin[a.n]) {
+      const int s = sumsq_seg(a, i);
+      const float v = a.src[s][i - a.begin[s]];
+      acc = fmaf(v, v, acc);
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  // hand-off as enc_block_sum's: a write-through partial, drained, then one relaxed ticket
+  if (threadIdx.x == 0) __hip_atomic_store(a.part + blockIdx.x, red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) last = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  // the last block: thread t adds partials t, t + 256, ... in order, then the same LDS tree
+  float s = 0.f;
+  for (unsigned b = threadIdx.x; b < gridDim.x; b += 256)
+    s += __hip_atomic_load(a.part + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    *a.out = red[0];
+    __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+__global__ __launch_bounds__(256) void sumsq_bwd_kernel(SumsqArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.begin[a.n]) return;
+  const int s = sumsq_seg(a, i);
+  const int64_t e = i - a.begin[s];
+  a.dst[s][e] = 2.f * *a.g * a.src[s][e];
+}
+
 }  // namespace siren

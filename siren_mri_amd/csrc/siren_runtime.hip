@@ -2614,6 +2614,59 @@ int siren_conv_wrw(const void* x, const void* dy, int N, int H, int W, int CI, i
   return check_launch("conv_wrw_gen_reduce");
 }
 
+int64_t siren_sumsq_workspace_bytes(int64_t total) {
+  return 256 + (int64_t)std::max<int64_t>(1, cdiv(total, SUMSQ_CHUNK)) * 4;
+}
+
+namespace {
+int sumsq_setup(SumsqArgs& a, int n, const float* const* src, const int64_t* numel) {
+  if (n < 1 || n > SUMSQ_MAX) return fail(SIREN_EINVAL, "sumsq: %d tensors (1..%d)", n, SUMSQ_MAX);
+  if (!src || !numel) return fail(SIREN_EINVAL, "sumsq: null table");
+  memset(&a, 0, sizeof(a));
+  a.n = n;
+  int64_t t = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!src[i] || numel[i] < 0) return fail(SIREN_EINVAL, "sumsq: tensor %d", i);
+    a.src[i] = src[i];
+    a.begin[i] = t;
+    t += numel[i];
+  }
+  a.begin[n] = t;
+  return SIREN_OK;
+}
+}  // namespace
+
+int siren_sumsq_forward(int n, const float* const* src, const int64_t* numel, float* out, void* ws, int64_t ws_bytes,
+                        void* stream) {
+  SumsqArgs a;
+  int rc = sumsq_setup(a, n, src, numel);
+  if (rc) return rc;
+  if (!out || !ws || ws_bytes < siren_sumsq_workspace_bytes(a.begin[n]))
+    return fail(SIREN_ENOSPACE, "sumsq: workspace (zeroed, siren_sumsq_workspace_bytes) missing or small");
+  a.counter = (unsigned*)ws;
+  a.part = (float*)((char*)ws + 256);
+  a.out = out;
+  const int64_t nb = std::max<int64_t>(1, cdiv(a.begin[n], SUMSQ_CHUNK));
+  hipLaunchKernelGGL(sumsq_fwd_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("sumsq_fwd");
+}
+
+int siren_sumsq_backward(int n, const float* const* src, const int64_t* numel, const float* g, float* const* dst,
+                         void* stream) {
+  SumsqArgs a;
+  int rc = sumsq_setup(a, n, src, numel);
+  if (rc) return rc;
+  if (!g || !dst) return fail(SIREN_EINVAL, "sumsq backward: null argument");
+  for (int i = 0; i < n; ++i) {
+    if (!dst[i]) return fail(SIREN_EINVAL, "sumsq backward: null output %d", i);
+    a.dst[i] = dst[i];
+  }
+  a.g = g;
+  if (a.begin[n] == 0) return SIREN_OK;
+  hipLaunchKernelGGL(sumsq_bwd_kernel, dim3((unsigned)cdiv(a.begin[n], 256)), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("sumsq_bwd");
+}
+
 int siren_enc_prep(int n, const float* const* w, const float* const* b, const int64_t* geom, void* const* wb,
                    void* const* wf, void* const* bb, void* stream) {
   if (n < 1 || n > ENC_PREP_MAX) return fail(SIREN_EINVAL, "enc_prep: %d filters (1..%d)", n, ENC_PREP_MAX);

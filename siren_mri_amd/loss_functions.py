@@ -254,12 +254,65 @@ def latent_loss(model_output):
     return torch.mean(model_output["latent_vec"] ** 2)
 
 
+_SUMSQ_WS = {}
+
+
+def _sumsq_workspace(device, total):
+    """Per-(device, stream) zeroed workspace of siren_sumsq_forward (left zeroed by every launch)."""
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    need = int(_native.lib().siren_sumsq_workspace_bytes(total))
+    ws = _SUMSQ_WS.get(key)
+    if ws is None or ws.numel() < need:
+        ws = torch.zeros(need, dtype=torch.uint8, device=device)
+        _SUMSQ_WS[key] = ws
+    return ws
+
+
+class _SumSquares(torch.autograd.Function):
+    """sum over tensors of torch.sum(w ** 2) in one native launch (siren_sumsq_forward), its
+    gradient 2 g w in one more (siren_sumsq_backward)."""
+
+    @staticmethod
+    def forward(ctx, *ws):
+        import ctypes
+        ts = [w.detach().contiguous() for w in ws]
+        n = len(ts)
+        numel = (ctypes.c_int64 * n)(*[t.numel() for t in ts])
+        out = torch.empty((), dtype=torch.float32, device=ts[0].device)
+        work = _sumsq_workspace(ts[0].device, sum(t.numel() for t in ts))
+        _native.check(_native.lib().siren_sumsq_forward(n, (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts]), numel,
+                                                        out.data_ptr(), work.data_ptr(), work.numel(),
+                                                        _native.stream_handle(ts[0].device)), "siren_sumsq_forward")
+        ctx.save_for_backward(*ts)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        import ctypes
+        if torch.is_grad_enabled():
+            raise RuntimeError("siren_mri_amd: second derivatives of the native hypo_weight_loss are not provided")
+        ts = ctx.saved_tensors
+        n = len(ts)
+        gc = g.detach().reshape(()).to(torch.float32).contiguous()
+        outs = [torch.empty_like(t) for t in ts]
+        _native.check(_native.lib().siren_sumsq_backward(n, (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts]),
+                                                         (ctypes.c_int64 * n)(*[t.numel() for t in ts]), gc.data_ptr(),
+                                                         (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs]),
+                                                         _native.stream_handle(ts[0].device)), "siren_sumsq_backward")
+        return tuple(o if need else None for o, need in zip(outs, ctx.needs_input_grad))
+
+
 def hypo_weight_loss(model_output):
+    """loss_functions.py:279-287: the mean of the squared hypo-parameters; on CUDA fp32 the sum of
+    squares is one native launch (and its gradient one more)."""
+    ws = list(model_output["hypo_params"].values())
+    total = sum(w.numel() for w in ws)
+    if ws and 0 < len(ws) <= 32 and all(w.is_cuda and w.dtype == torch.float32 and w.device == ws[0].device
+                                        for w in ws):
+        return _SumSquares.apply(*ws) * (1 / total)
     weight_sum = 0
-    total = 0
-    for w in model_output["hypo_params"].values():
+    for w in ws:
         weight_sum = weight_sum + torch.sum(w ** 2)
-        total += w.numel()
     return weight_sum * (1 / total)
 
 

@@ -85,3 +85,28 @@ def test_native_heads_deterministic():
     assert torch.equal(a[1], b[1])
     for n in a[2]:
         assert torch.equal(a[2][n], b[2][n]), n
+
+
+def test_hypo_weight_loss_native_sum_of_squares():
+    """hypo_weight_loss (loss_functions.py:279-287) on CUDA fp32: the native sum of squares and its
+    gradient against the fp64 torch formula (1e-6), deterministic, ragged tensor sizes."""
+    from siren_mri_amd import loss_functions
+    g = torch.Generator().manual_seed(5)
+    shapes = [(32, 256, 16), (32, 256), (32, 256, 256), (32, 2, 256), (32, 2), (7, 1001)]
+    ws = [torch.randn(s, generator=g).to(DEV).requires_grad_(True) for s in shapes]
+    out = {"hypo_params": {f"p{i}": w for i, w in enumerate(ws)}}
+    l1 = loss_functions.hypo_weight_loss(out)
+    l1.backward()
+    g1 = [w.grad.clone() for w in ws]
+    for w in ws:
+        w.grad = None
+    l2 = loss_functions.hypo_weight_loss(out)
+    l2.backward()
+    assert torch.equal(l1, l2) and all(torch.equal(a, w.grad) for a, w in zip(g1, ws))
+    wd = [w.detach().double().cpu().requires_grad_(True) for w in ws]
+    total = sum(w.numel() for w in wd)
+    ref = sum((w ** 2).sum() for w in wd) / total
+    ref.backward()
+    assert abs(l1.item() - ref.item()) <= 1e-6 * abs(ref.item())
+    for a, w in zip(g1, wd):
+        assert orc.norm_rel(a.cpu(), w.grad) < 1e-6
