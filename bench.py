@@ -86,7 +86,7 @@ KCLASS_SYMBOL = {
              14: "siren::pair_ring_bf16_kernel<2, true, true, 0, 2>"},
     "fp32": {1: "siren::nt_f32_kernel<0, 256>", 2: "siren::nt_f32_kernel<1, 256>", 3: "siren::tn_dw_kernel<0, false, false>"},
 }
-CONFIG_DEFAULT_STEPS = {"m": (50, 10), "c1": (50, 10), "c2": (50, 10), "c3": (20, 5), "c4": (10, 3),
+CONFIG_DEFAULT_STEPS = {"m": (50, 10), "c1": (50, 10), "c2": (50, 10), "c3": (20, 5), "c4": (10, 3), "c4_fp32": (5, 2),
                         "m_fp32": (10, 3), "m_shard8": (50, 10)}
 C4 = dict(num_fourier_features=8, kl_weight=2.78e-8, fw_weight=6.4e-6, lr=5.57e-5, fourier_features_scale=21,
           latent_dim=128, hidden_features_hyper=128, hidden_layers_hyper=2, hidden_layers=3, hidden_features=256,
@@ -98,7 +98,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=None)
     p.add_argument("--warmup", type=int, default=None)
-    p.add_argument("--config", default="m", choices=["m", "c1", "c2", "c3", "c4", "m_fp32", "m_shard8"])
+    p.add_argument("--config", default="m", choices=["m", "c1", "c2", "c3", "c4", "c4_fp32", "m_fp32", "m_shard8"])
     p.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     p.add_argument("--precision", default=None, choices=["bf16", "fp32"],
                    help="SIREN arithmetic (default: bf16, fp32 for c3)")
@@ -115,7 +115,7 @@ def parse():
     a.steps = st if a.steps is None else a.steps
     a.warmup = wu if a.warmup is None else a.warmup
     if a.precision is None:
-        a.precision = "fp32" if a.config in ("c3", "m_fp32") else "bf16"
+        a.precision = "fp32" if a.config in ("c3", "m_fp32", "c4_fp32") else "bf16"
     if a.no_graph:
         a.timing = "eager"
     return a
@@ -323,11 +323,12 @@ def build_c4(args, dev, rank, world, precision, encoder_precision="bf16"):
                     "synthetic k-space (IRData slices x flips/rotations + seeded ellipses, fftshift(fft2)), "
                     "seeded CS-Cartesian masks, FF B = randn(2, 8) * 21 (seed 0)",
                     {"optimizer": opt, "encoder_flops_per_step": enc, "encoder_precision": encoder_precision,
-                     "model": model, "inp": inp, "conv_algorithms": "MIOpen find (torch.backends.cudnn.benchmark)"})
+                     "model": model, "inp": inp, "ff": ff, "loss_fn": loss_fn,
+                     "conv_algorithms": "MIOpen find (torch.backends.cudnn.benchmark)"})
 
 
 def build(cfg, args, dev, rank, world, precision=None):
-    precision = precision or ("fp32" if cfg in ("c3", "m_fp32") else args.precision)
+    precision = precision or ("fp32" if cfg in ("c3", "m_fp32", "c4_fp32") else args.precision)
     if cfg in ("m", "c1", "c2"):
         return build_fit(cfg, args, dev, rank, world, precision)
     if cfg == "m_fp32":  # the metric fit in the reference's arithmetic (fp32 operands, exact-fp32 MFMA)
@@ -336,6 +337,8 @@ def build(cfg, args, dev, rank, world, precision=None):
         return build_fit("m", args, dev, rank, world, precision, shard_of=8)
     if cfg == "c3":
         return build_c3(args, dev, rank, world, precision)
+    if cfg == "c4_fp32":  # config 4 in the reference's arithmetic: fp32 encoder (MIOpen) and fp32 SIREN
+        return build_c4(args, dev, rank, world, "fp32", encoder_precision="fp32")
     return build_c4(args, dev, rank, world, precision)
 
 
@@ -716,22 +719,23 @@ def measure(cfg, args, dev, rank, world, with_kernels=True):
             traffic = None
         nbytes = kernel_bytes(wl, dom)
         mfma_frac = flops / avg_s / peak
-        hbm_frac = nbytes / avg_s / HBM_PEAK if nbytes else None
-        # the binding ceiling of the roofline model: HBM when the launch's arithmetic intensity
-        # (algorithmic FLOPs / algorithmic bytes) is below the ridge point peak / HBM bandwidth
-        ai = flops / nbytes if nbytes else None
-        hbm_bound = ai is not None and ai < peak / HBM_PEAK
+        # the path is a dense contraction (~12 B of algorithmic I/O per coordinate,
+        # ~1e5 FLOP/B), so the roofline that bounds it is the MFMA peak and `frac` is the dominant
+        # kernel's algorithmic FLOPs / its launch time / the dense peak. The bytes the design itself
+        # stores between kernels (phase codes, dZ planes) are NOT algorithmic: their HBM rate is
+        # reported under a separate key only, never as `frac`.
+        design_hbm_frac = nbytes / avg_s / HBM_PEAK if nbytes else None
         res["roofline"] = {
-            "bound": "hbm" if hbm_bound else "mfma", "kernel": KCLASS_NAMES[dom],
+            "bound": "mfma", "kernel": KCLASS_NAMES[dom],
             "kernel_symbol": KCLASS_SYMBOL.get(wl.precision, {}).get(dom),
-            "achieved": round(nbytes / avg_s / 1e9, 1) if hbm_bound else round(flops / avg_s / 1e12, 2),
-            "peak": HBM_PEAK / 1e9 if hbm_bound else round(peak / 1e12, 1),
-            "unit": "GB/s" if hbm_bound else "TFLOP/s",
-            "frac": round(hbm_frac if hbm_bound else mfma_frac, 4),
-            "mfma_frac": round(mfma_frac, 4), "hbm_frac": round(hbm_frac, 4) if hbm_frac else None,
-            "arithmetic_intensity_flop_per_byte": round(ai, 1) if ai else None,
-            "ridge_flop_per_byte": round(peak / HBM_PEAK, 1),
-            "bytes_per_launch": nbytes, "flops_per_launch": flops,
+            "achieved": round(flops / avg_s / 1e12, 2), "peak": round(peak / 1e12, 1), "unit": "TFLOP/s",
+            "frac": round(mfma_frac, 4),
+            "basis": "SURVEY.md §8(d): algorithmic FLOPs per launch / HIP-event launch time / dense MFMA peak",
+            "design_bytes_per_launch": nbytes,
+            "hbm_frac_of_design_bytes": round(design_hbm_frac, 4) if design_hbm_frac else None,
+            "design_bytes_note": "bytes the design materialises between kernels (phase codes, dZ planes), "
+                                 "each read once / written once, over 8 TB/s; not algorithmic I/O",
+            "flops_per_launch": flops,
             "avg_launch_ms": round(kt.avg_ms, 4), "launches": kt.launches,
             "timing": "HIP event pairs on the launch stream around every launch of the kernel over a timed "
                       "region of K eager steps" + (" (the reported value is the hipGraph region's)" if graph else ""),
@@ -836,10 +840,10 @@ def main():
     if world == 1 and not args.no_other_configs and args.config == "m":
         oargs = argparse.Namespace(**vars(args))
         others = {}
-        for cfg in ("c1", "c2", "c3", "c4", "m_fp32", "m_shard8"):
+        for cfg in ("c1", "c2", "c3", "c4", "c4_fp32", "m_fp32", "m_shard8"):
             oargs.steps, oargs.warmup = CONFIG_DEFAULT_STEPS[cfg]
             try:
-                r, owl, _, _ = measure(cfg, oargs, dev, rank, world, with_kernels=(cfg != "c4"))
+                r, owl, _, _ = measure(cfg, oargs, dev, rank, world, with_kernels=not cfg.startswith("c4"))
                 others[cfg] = r
                 del owl
             except Exception as e:  # noqa: BLE001 - a failing side config must not lose the metric line

@@ -86,11 +86,19 @@ DEV float cos_f32(float x) {
   return ((q + 1) & 2) ? -v : v;
 }
 
+// Range of Fourier-feature arguments (2 pi z, radians) over which both feature paths use
+// sincos_poly: the FMA Cody-Waite reduction stays within 7e-8 absolute of sin / cos of the fp32
+// argument up to 1e6 (measured against fp64; tests/test_gpu_fourier_input.py pins it).
+constexpr float kFFPolyRange = 1.0e6f;
+
 // Fourier feature f of a row (features.py:21-41): z = sum_c x[c] B[c][k] (fma chain from 0), k = f
 // mod m, sin(2 pi z) for f < m, cos(2 pi z) for m <= f < 2m, 0 past 2m — bit-identical to
 // siren_kspace.hip fourier_kernel (the same chain, argument and sincos_poly), so features formed
-// here equal the materialised ones. Arguments stay inside the Cody-Waite range for any |x| <= 1
-// coordinates and |B| entries below ~4000 (no far path here).
+// here equal the materialised ones. There is no far-range path in the register forward (a call
+// there would cost the kernel its register budget): the host takes the fused path only when
+// 2 pi max_k sum_c |B[c][k]| < kFFPolyRange (coordinates in [-1, 1]; features.py), and an
+// argument past the range anyway (coordinates outside [-1, 1]) yields NaN, never a silently
+// different feature.
 DEV float ff_feature(const float* xr, const float* B, int cin, int m, int f) {
   if (f >= 2 * m) return 0.f;
   const bool cosine = f >= m;
@@ -101,10 +109,11 @@ DEV float ff_feature(const float* xr, const float* B, int cin, int m, int f) {
     if (c < cin) z = fmaf(xr[c], B[c * m + k], z);
   float sn, cs;
   int q;
-  sincos_poly(__fmul_rn(6.2831854820251465f, z), sn, cs, q);
+  const float arg = __fmul_rn(6.2831854820251465f, z);
+  sincos_poly(arg, sn, cs, q);
   q += cosine ? 1 : 0;  // cos x = sin(x + pi / 2): one quadrant on
   const float v = (q & 1) ? cs : sn;
-  return (q & 2) ? -v : v;
+  return __builtin_fabsf(arg) < kFFPolyRange ? ((q & 2) ? -v : v) : __builtin_nanf("");
 }
 
 template <> struct Prec<kPrecF32> {

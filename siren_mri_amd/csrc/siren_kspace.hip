@@ -164,7 +164,7 @@ __global__ __launch_bounds__(KS_THREADS) void fourier_kernel(FourierArgs a) {
     // the features the register forward forms in its first layer from the raw coordinates are then
     // bit-identical to these, so the fused and the materialised paths compute the same network
     float sv, cv;
-    if (__builtin_expect(__builtin_fabsf(arg) < 1.0e5f, 1)) {
+    if (__builtin_expect(__builtin_fabsf(arg) < kFFPolyRange, 1)) {
       float sn, cs;
       int qd;
       sincos_poly(arg, sn, cs, qd);

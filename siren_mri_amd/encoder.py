@@ -48,7 +48,7 @@ def _ok_channels(c: int) -> bool:
 
 def supported(enc) -> bool:
     """The layer structure this node takes (ConvImgEncoder as modules.py builds it)."""
-    convs = [enc.conv_theta] + [m for m in enc.cnn if isinstance(m, torch.nn.Conv2d)]
+    convs = [m for m in enc.modules() if isinstance(m, torch.nn.Conv2d)]  # the residual blocks' too
     if not all(c.stride == (1, 1) and c.dilation == (1, 1) and c.groups == 1 and c.bias is not None
                and c.kernel_size[0] == c.kernel_size[1] and c.kernel_size[0] % 2 == 1
                and c.padding == (c.kernel_size[0] // 2,) * 2 for c in convs):
@@ -58,6 +58,9 @@ def supported(enc) -> bool:
 
 def _w_bf16(w):
     return w.detach().to(torch.bfloat16).contiguous(memory_format=_CL)
+
+
+ENC_PREP_MAX = 32  # filters per siren_enc_prep launch (csrc/siren_encoder.hip)
 
 
 def _prep_operands(convs, dev, stream):
@@ -73,12 +76,16 @@ def _prep_operands(convs, dev, stream):
         wfs.append(torch.empty((ci, co, kh, kw), dtype=torch.bfloat16, device=dev, memory_format=_CL) if i else None)
         bbs.append(torch.empty(co, dtype=torch.bfloat16, device=dev))
         geom += [co, ci, kh, *c.weight.stride()]
-    VP = ctypes.c_void_p * n
-    _native.check(_native.lib().siren_enc_prep(
-        n, VP(*[c.weight.data_ptr() for c in convs]), VP(*[c.bias.data_ptr() for c in convs]),
-        (ctypes.c_int64 * (7 * n))(*geom), VP(*[t.data_ptr() for t in wbs]),
-        VP(*[t.data_ptr() if t is not None else None for t in wfs]), VP(*[t.data_ptr() for t in bbs]), stream),
-        "siren_enc_prep")
+    # one launch per ENC_PREP_MAX filters (an encoder with more than 14 residual blocks has more
+    # than 32 convolutions)
+    for a in range(0, n, ENC_PREP_MAX):
+        b = min(n, a + ENC_PREP_MAX)
+        VP = ctypes.c_void_p * (b - a)
+        _native.check(_native.lib().siren_enc_prep(
+            b - a, VP(*[c.weight.data_ptr() for c in convs[a:b]]), VP(*[c.bias.data_ptr() for c in convs[a:b]]),
+            (ctypes.c_int64 * (7 * (b - a)))(*geom[7 * a:7 * b]), VP(*[t.data_ptr() for t in wbs[a:b]]),
+            VP(*[t.data_ptr() if t is not None else None for t in wfs[a:b]]), VP(*[t.data_ptr() for t in bbs[a:b]]),
+            stream), "siren_enc_prep")
     return wbs, wfs, bbs
 
 

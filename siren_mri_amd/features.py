@@ -81,6 +81,7 @@ class GaussianFourierFeatureTransform(torch.nn.Module):
         self._mapping_size = mapping_size_spatial
         B = torch.randn((num_input_channels, mapping_size_spatial)) * scale if loaded_B is None else loaded_B
         self.register_buffer("_B_spatial", B.detach().clone(), persistent=False)
+        self._fused_ok = _fused_range_ok(self._B_spatial)
         if device is not None:
             self.to(device)
 
@@ -100,8 +101,8 @@ class GaussianFourierFeatureTransform(torch.nn.Module):
         from . import fusion
         x = model_input["coords"]
         inner = getattr(model, "module", model)  # (a DistributedDataParallel wrapper)
-        if (FUSED_INPUT and getattr(inner, "fourier_input", False) and fusion.enabled() and x.is_cuda
-                and x.dtype == torch.float32 and not x.requires_grad):
+        if (FUSED_INPUT and self._fused_ok and getattr(inner, "fourier_input", False) and fusion.enabled()
+                and x.is_cuda and x.dtype == torch.float32 and not x.requires_grad):
             model_input["fourier_B"] = self._B_spatial.to(x.device, x.dtype)
         else:
             model_input["coords"] = self(x)
@@ -118,3 +119,18 @@ class GaussianFourierFeatureTransform(torch.nn.Module):
 
     def set_B(self, B):
         self._B_spatial = B.detach().clone().to(self._B_spatial.device)
+        self._fused_ok = _fused_range_ok(self._B_spatial)
+
+
+# |2 pi x B| bound below which the kernels' Fourier-feature sin / cos (siren_common.h ff_feature,
+# fourier_kernel: Cody-Waite + minimax) are accurate (kFFPolyRange): the in-kernel transform is
+# used only when it holds for coordinates in [-1, 1] (get_mgrid's range); larger B entries take
+# the materialised op, whose kernel calls the far-range sin / cos past it
+FF_POLY_RANGE = 1.0e6
+
+
+def _fused_range_ok(B):
+    """Whether 2 pi max_k sum_c |B[c][k]| < FF_POLY_RANGE (computed once per B, on set)."""
+    if B.numel() == 0:
+        return True
+    return float(2 * np.pi * B.detach().abs().sum(0).max()) < FF_POLY_RANGE

@@ -283,15 +283,16 @@ class _SumSquares(torch.autograd.Function):
         _native.check(_native.lib().siren_sumsq_forward(n, (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts]), numel,
                                                         out.data_ptr(), work.data_ptr(), work.numel(),
                                                         _native.stream_handle(ts[0].device)), "siren_sumsq_forward")
-        ctx.save_for_backward(*ts)
+        ctx.save_for_backward(*ws)  # the inputs: a create_graph backward differentiates through them
         return out
 
     @staticmethod
     def backward(ctx, g):
         import ctypes
         if torch.is_grad_enabled():
-            raise RuntimeError("siren_mri_amd: second derivatives of the native hypo_weight_loss are not provided")
-        ts = ctx.saved_tensors
+            # create_graph=True: the exact gradient 2 g w in differentiable PyTorch
+            return tuple(2 * g * w if need else None for w, need in zip(ctx.saved_tensors, ctx.needs_input_grad))
+        ts = [w.detach().contiguous() for w in ctx.saved_tensors]
         n = len(ts)
         gc = g.detach().reshape(()).to(torch.float32).contiguous()
         outs = [torch.empty_like(t) for t in ts]

@@ -141,19 +141,43 @@ class _HyperHeads(torch.autograd.Function):
                                               saved.data_ptr(), saved.numel() * 4, _native.stream_handle(z.device)),
                       "siren_hyper_forward")
         ctx.G, ctx.D = G, D
-        ctx.save_for_backward(zc, saved, *ps)
+        # the inputs themselves are saved (not detached copies) so that a create_graph backward can
+        # differentiate through them
+        ctx.save_for_backward(z, saved, *params)
         ctx.set_materialize_grads(False)
         return tuple(outs)
+
+    @staticmethod
+    def _eager_backward(G, D, z, params, douts, needs):
+        """create_graph=True: the per-head Linear + ReLU chain of the reference (meta_modules.py:
+        48-54 through modules.FCBlock), recomputed in differentiable PyTorch and differentiated with
+        the graph kept, so higher derivatives exist."""
+        with torch.enable_grad():
+            outs, wrt = [], [z] + list(params)
+            for g in range(G):
+                h = z
+                for l in range(D + 1):
+                    W, b = params[2 * (g * (D + 1) + l)], params[2 * (g * (D + 1) + l) + 1]
+                    h = torch.nn.functional.linear(h, W, b)
+                    if l < D:
+                        h = torch.relu(h)
+                outs.append(h)
+            pairs = [(o, g) for o, g in zip(outs, douts) if g is not None]
+            want = [t for t, n in zip(wrt, needs) if n]
+            got = iter(torch.autograd.grad([o for o, _ in pairs], want, [g for _, g in pairs], create_graph=True,
+                                           allow_unused=True) if pairs and want else [None] * len(want))
+            res = [next(got) if n else None for n in needs]
+        return (None, None, *res)
 
     @staticmethod
     def backward(ctx, *douts):
         import ctypes
         from . import _native
-        if torch.is_grad_enabled():
-            raise RuntimeError("siren_mri_amd: second derivatives of the native HyperNetwork heads are not provided")
         G, D = ctx.G, ctx.D
         t = ctx.saved_tensors
-        z, saved, ps = t[0], t[1], list(t[2:])
+        if torch.is_grad_enabled():
+            return _HyperHeads._eager_backward(G, D, t[0], list(t[2:]), douts, ctx.needs_input_grad[2:])
+        z, saved, ps = t[0].detach().contiguous(), t[1], [p.detach().contiguous() for p in t[2:]]
         lib = _native.lib()
         d = _HyperHeads._desc(G, D, z, ps)
         gs = [g.contiguous() if g is not None else torch.zeros(z.shape[0], d.out_features[i], device=z.device)

@@ -275,13 +275,17 @@ def _differentiable_backward(ctx, dy, x, saved, ws, bs, need_dx):
     from .jvp import guard_higher_order, jacobian_of
     w0, prec, outermost_linear, batched, n, keep = ctx.meta
     dx = None
+    need_w = any(ctx.needs_input_grad[2:])
+    dW, db = [None] * n, [None] * n
     if need_dx:
         if not outermost_linear or x.shape[-1] > 4:
             # no tangent-stream form for this stack: the native first-order input gradient, which
-            # raises only if it is differentiated again
+            # raises only if it is differentiated again; the same launch's dW / db are
+            # kept when the weights need gradients (one native backward, not two)
             with torch.no_grad():
-                dx, _, _ = torch.ops.siren_mri_amd.sine_mlp_bwd(dy, x, ws, bs, saved, w0, prec, outermost_linear,
-                                                                batched, True)
+                dx, dW, db = torch.ops.siren_mri_amd.sine_mlp_bwd(dy, x, ws, bs, saved, w0, prec, outermost_linear,
+                                                                  batched, True)
+            dW, db = list(dW), list(db)
             dx = guard_higher_order([dx], [dy, x, *ws, *bs],
                                     "siren_mri_amd: a differentiable SIREN input gradient (create_graph=True) "
                                     "needs outermost_linear=True and in_features <= 4 (the tangent-stream "
@@ -289,12 +293,11 @@ def _differentiable_backward(ctx, dy, x, saved, ws, bs, need_dx):
         else:
             J = jacobian_of(x, ws, bs, w0, prec, batched)
             dx = (J * dy.unsqueeze(-1)).sum(-2)
-    need_w = any(ctx.needs_input_grad[2:])
-    dW, db = [None] * n, [None] * n
     if need_w:
-        with torch.no_grad():
-            _, dW, db = torch.ops.siren_mri_amd.sine_mlp_bwd(dy, x, ws, bs, saved, w0, prec, outermost_linear,
-                                                             batched, False)
+        if dW[0] is None:
+            with torch.no_grad():
+                _, dW, db = torch.ops.siren_mri_amd.sine_mlp_bwd(dy, x, ws, bs, saved, w0, prec, outermost_linear,
+                                                                 batched, False)
         wb = guard_higher_order([*dW, *db], [dy, x, *ws, *bs],
                                 "siren_mri_amd: second derivatives of the SIREN's weight gradients are not "
                                 "provided (derivatives of its input gradient are)")

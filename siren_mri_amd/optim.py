@@ -42,25 +42,85 @@ class Adam(torch.optim.Adam):
     # steps use siren_adam_scalars (the same expressions computed on the device)
     _TABLE_MAX = 1 << 22
 
+    _bias_cache: dict = {}
+
+    @classmethod
+    def _bias_corrections(cls, beta1, beta2):
+        """(1 - beta1^t, sqrt(1 - beta2^t)) for t = 1 .. the step where both reach 1 in double, as
+        float64 arrays (the eager path's expressions, evaluated once per betas), or None when that
+        takes more than _TABLE_MAX steps. The table's length depends on the betas only."""
+        import numpy as np
+        key = (float(beta1), float(beta2), cls._TABLE_MAX)
+        if key not in cls._bias_cache:
+            bc1s, sq2s = [], []
+            t = 1
+            while True:
+                bc1 = 1 - beta1 ** t
+                bc2 = 1 - beta2 ** t
+                bc1s.append(bc1)
+                sq2s.append(bc2 ** 0.5)
+                if (bc1 == 1.0 and bc2 == 1.0) or t >= cls._TABLE_MAX:
+                    break
+                t += 1
+            done = bc1 == 1.0 and bc2 == 1.0
+            cls._bias_cache[key] = (np.array(bc1s), np.array(sq2s)) if done else None
+        return cls._bias_cache[key]
+
+    @classmethod
+    def _scalar_rows(cls, lr, beta1, beta2):
+        """Host rows {step_size, bias_correction2_sqrt} of steps 1, 2, ... (float32), or None."""
+        import numpy as np
+        bc = cls._bias_corrections(beta1, beta2)
+        if bc is None:
+            return None
+        bc1, sq2 = bc
+        # (lr / bc1) * -1 elementwise in double: the same IEEE division as the eager expression
+        return torch.from_numpy(np.stack([(lr / bc1) * -1, sq2], axis=1).astype(np.float32))
+
     @classmethod
     def _scalar_table(cls, lr, beta1, beta2, device):
-        import numpy as np
-        rows = []
-        t = 1
-        while True:
-            bc1 = 1 - beta1 ** t
-            bc2 = 1 - beta2 ** t
-            rows.append(((lr / bc1) * -1, bc2 ** 0.5))
-            if (bc1 == 1.0 and bc2 == 1.0) or t >= cls._TABLE_MAX:
-                break
-            t += 1
-        if not (bc1 == 1.0 and bc2 == 1.0):
-            return None
-        return torch.from_numpy(np.array(rows, dtype=np.float32)).to(device)
+        rows = cls._scalar_rows(lr, beta1, beta2)
+        return None if rows is None else rows.to(device)
 
     def enable_graph_mode(self):
         self._graph_mode = True
         self._dev_step = {}
+
+    def _group_table(self, group, device):
+        """The group's device step-scalar table for its current (lr, betas), or None (computed
+        form). A table replaced by a betas change stays alive until release_graph_buffers(): a
+        hipGraph captured earlier may still point at it. An lr change keeps the table
+        (its length depends on the betas only) and rewrites it in place, so an lr schedule
+        allocates nothing and a captured graph replays the new lr."""
+        lr_now, betas = float(group["lr"]), tuple(float(b) for b in group["betas"])
+        tables = self.__dict__.setdefault("_tables", {})
+        retired = self.__dict__.setdefault("_retired", [])
+        ent = tables.get(id(group))
+        if ent is None or ent[0] != betas:
+            if ent is not None:
+                retired.append(ent[2])
+            ent = [betas, lr_now, self._scalar_table(lr_now, *betas, device)]
+            tables[id(group)] = ent
+        elif ent[1] != lr_now:
+            if ent[2] is not None:
+                ent[2].copy_(self._scalar_rows(lr_now, *betas))
+            ent[1] = lr_now
+        return ent[2]
+
+    def update_graph_scalars(self):
+        """Graph mode: bring every group's step-scalar table to its current lr without stepping
+        (an lr scheduler between replays of a captured step; an eager step() does it itself).
+        The table form only: the computed form bakes lr into the captured launch."""
+        for group in self.param_groups:
+            ent = self.__dict__.get("_tables", {}).get(id(group))
+            if ent is not None and ent[2] is not None:
+                self._group_table(group, ent[2].device)
+
+    def release_graph_buffers(self):
+        """Drop the step-scalar tables and step counters replaced by a betas change or a new
+        parameter count. Call it once no hipGraph captured before the change will be replayed
+        again (a captured launch keeps pointing at the buffers it was captured with)."""
+        self.__dict__.get("_retired", []).clear()
 
     def sync_graph_steps(self):
         for group in self.param_groups:
@@ -156,18 +216,7 @@ class Adam(torch.optim.Adam):
                     #  "t": the group counter and "scalars" (computed form)}
                     dev = {"t0": next(iter(by_step)) - 1, "steps": {}}
                     self._dev_step[id(group)] = dev
-                key = (float(group["lr"]), float(beta1), float(beta2))
-                tables = self.__dict__.setdefault("_tables", {})
-                # replaced tables / counters stay alive: a hipGraph captured earlier may still
-                # point at them
-                retired = self.__dict__.setdefault("_retired", [])
-                tab = tables.get(id(group))
-                if tab is None or tab[0] != key:
-                    if tab is not None:
-                        retired.append(tab)
-                    tab = (key, self._scalar_table(*key, params[0].device))
-                    tables[id(group)] = tab
-                tab = tab[1]
+                tab = self._group_table(group, params[0].device)
                 if tab is None:
                     if "t" not in dev:
                         dev["t"] = torch.full((1,), dev["t0"], dtype=torch.float64, device=params[0].device)

@@ -140,3 +140,44 @@ def test_siren_mlp_ff_input_with_coordinate_gradient():  # (the default path: ma
         fusion.clear()
     y.sum().backward()
     assert x.grad is not None and torch.isfinite(x.grad).all()
+
+
+@pytest.mark.parametrize("scale", [21.0, 3.0e3, 4.0e4])
+def test_fourier_features_op_against_fp64_over_the_argument_range(scale):
+    """the materialised op (and so the fused path, bit-identical to it) forms sin / cos
+    with the Cody-Waite + minimax sincos_poly below kFFPolyRange (1e6 rad). Checked against fp64
+    sin / cos of the SAME fp32 argument (fma chain x.B from 0, then fl(2 pi) z, emulated here in
+    fp64 with one rounding per step) over grid coordinates in [-1, 1] and B scales from the configs'
+    21 up to arguments of ~1e6: abs error <= 2e-7. The host's fused-path gate
+    (features._fused_range_ok) admits the scales whose arguments stay inside the range."""
+    import numpy as np
+    from siren_mri_amd import dataio, features
+    g = torch.Generator().manual_seed(3)
+    B = torch.randn(2, 8, generator=g) * scale
+    x = dataio.get_mgrid(128)[None]
+    out = features.fourier_features(x.to(DEV), B.to(DEV)).cpu().double().numpy()[0]
+    f32 = np.float32
+    xn, Bn = x[0].numpy(), B.numpy()
+    z = f32(np.float64(xn[:, :1]) * np.float64(Bn[0][None]))  # fma(x0, B0, 0): one rounding
+    z = f32(np.float64(xn[:, 1:2]) * np.float64(Bn[1][None]) + np.float64(z))
+    arg = np.float64(f32(np.float64(f32(2 * np.pi)) * np.float64(z)))
+    err_s = np.abs(out[:, :8] - np.sin(arg)).max()
+    err_c = np.abs(out[:, 8:] - np.cos(arg)).max()
+    print(f"\n[fourier_features vs fp64] scale {scale}: max |arg| {np.abs(arg).max():.3g}, "
+          f"sin err {err_s:.2e}, cos err {err_c:.2e}")
+    assert err_s <= 2e-7 and err_c <= 2e-7
+    inside = 2 * np.pi * np.abs(Bn).sum(0).max() < features.FF_POLY_RANGE
+    assert features._fused_range_ok(B) == inside
+    assert features.GaussianFourierFeatureTransform(2, 8, loaded_B=B)._fused_ok == inside
+
+
+def test_fused_fourier_gate_rejects_out_of_range_B():
+    """A B whose arguments could leave the in-kernel range on [-1, 1] coordinates is handed to the
+    model materialised (the op's kernel takes the far-range sin / cos past 1e6), never fused."""
+    from siren_mri_amd import features
+    ff = features.GaussianFourierFeatureTransform(2, 8, loaded_B=torch.full((2, 8), 1.0e5), device=DEV)
+
+    class M(torch.nn.Module):
+        fourier_input = True
+    mi = ff.model_input(M(), {"coords": torch.zeros(1, 4, 2, device=DEV)})
+    assert "fourier_B" not in mi and mi["coords"].shape == (1, 4, 16)

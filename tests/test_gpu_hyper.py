@@ -110,3 +110,57 @@ def test_hypo_weight_loss_native_sum_of_squares():
     assert abs(l1.item() - ref.item()) <= 1e-6 * abs(ref.item())
     for a, w in zip(g1, wd):
         assert orc.norm_rel(a.cpu(), w.grad) < 1e-6
+
+
+def test_create_graph_through_native_heads_and_sum_of_squares():
+    """torch.autograd.grad(..., create_graph=True) over the native heads and the native
+    hypo_weight_loss works as it did with the plain PyTorch modules (the heads recompute the
+    per-head Linear + ReLU chain differentiably; the sum of squares' gradient is 2 g w): the first
+    derivatives equal the chain's, and a second derivative (of the gradient norm) equals the
+    chain's to fp32 summation order."""
+    from siren_mri_amd import loss_functions, meta_modules
+    hn = _hyper(2, hyper_hidden=32, latent=16)
+    g = torch.Generator().manual_seed(5)
+    z0 = torch.randn(4, 16, generator=g).to(DEV)
+
+    def second(native):
+        z = z0.clone().requires_grad_(True)
+        saved = meta_modules.HyperNetwork._native_layers
+        if not native:
+            meta_modules.HyperNetwork._native_layers = lambda self, z: None
+        try:
+            if native:
+                assert hn._native_layers(z) is not None
+            hp = hn(z)
+            loss = loss_functions.hypo_weight_loss({"hypo_params": hp})
+            (gz,) = torch.autograd.grad(loss, [z], create_graph=True)
+            (ggz,) = torch.autograd.grad((gz ** 2).sum(), [z])
+        finally:
+            meta_modules.HyperNetwork._native_layers = saved
+        return loss.detach(), gz.detach(), ggz
+    l_n, g_n, gg_n = second(True)
+    l_c, g_c, gg_c = second(False)
+    assert float(l_n) == pytest.approx(float(l_c), rel=1e-5)
+    assert orc.norm_rel(g_n.cpu(), g_c.cpu()) < 1e-5
+    assert orc.norm_rel(gg_n.cpu(), gg_c.cpu()) < 1e-4
+
+
+def test_encoder_with_more_than_32_convolutions():
+    """an encoder with 15 residual blocks (33 convolutions) takes the operand prep in
+    launches of at most 32 filters; its forward equals the same node's per-convolution casts."""
+    from siren_mri_amd import encoder, modules
+    torch.manual_seed(0)
+    enc = modules.ConvImgEncoder(2, (32, 32), hidden_size=64, kernel_size=3, num_conv_res_blocks=15,
+                                 precision="bf16").to(DEV)
+    convs = enc._layers()
+    assert convs is not None and len(convs) > 32
+    wbs, wfs, bbs = encoder._prep_operands(convs, DEV, torch.cuda.current_stream().cuda_stream)
+    for i, c in enumerate(convs):
+        assert torch.equal(wbs[i], encoder._w_bf16(c.weight))
+        assert torch.equal(bbs[i], c.bias.detach().to(torch.bfloat16))
+        if i:
+            assert torch.equal(wfs[i], encoder._w_flip(wbs[i]))
+    I = torch.randn(2, 2, 32, 32, device=DEV)
+    e = enc(I)
+    e.sum().backward()
+    assert torch.isfinite(e).all() and all(torch.isfinite(p.grad).all() for p in enc.parameters())

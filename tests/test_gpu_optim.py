@@ -85,3 +85,40 @@ def test_adam_graph_mode_replay_matches_eager(sizes, form, monkeypatch):
     o_g.sync_graph_steps()
     # the capture itself does not step: 1 eager + 5 replays = 6 steps, like the eager optimizer
     assert float(o_g.state[p_g[0]]["step"]) == 6.0
+
+
+def test_adam_graph_mode_lr_schedule_rewrites_table_in_place():
+    """an lr change in graph mode rewrites the step-scalar table in place (its length
+    depends on the betas only): nothing is retired or allocated per lr value, and a hipGraph
+    captured before the change replays the NEW lr, as the eager optimizer does."""
+    from siren_mri_amd.optim import Adam
+    g = torch.Generator().manual_seed(2)
+    init = torch.randn(4096, generator=g)
+    grads = [torch.randn(4096, generator=g).to(DEV) for _ in range(6)]
+    lrs = [1e-2, 1e-2, 5e-3, 2.5e-3, 1e-3, 1e-3]
+    p_e = torch.nn.Parameter(init.clone().to(DEV))
+    o_e = Adam([p_e], lr=lrs[0])
+    for lr, gr in zip(lrs, grads):
+        o_e.param_groups[0]["lr"] = lr
+        p_e.grad = gr.clone()
+        o_e.step()
+    p_g = torch.nn.Parameter(init.clone().to(DEV))
+    o_g = Adam([p_g], lr=lrs[0])
+    o_g.enable_graph_mode()
+    buf = torch.empty(4096, device=DEV)
+    p_g.grad = buf
+    buf.copy_(grads[0])
+    o_g.step()
+    table = o_g._tables[id(o_g.param_groups[0])][2]
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        o_g.step()
+    for lr, gr in zip(lrs[1:], grads[1:]):
+        o_g.param_groups[0]["lr"] = lr  # a scheduler's per-step lr
+        o_g.update_graph_scalars()
+        buf.copy_(gr)
+        graph.replay()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(p_g.detach(), p_e.detach(), rtol=1e-6, atol=1e-7)
+    assert o_g._tables[id(o_g.param_groups[0])][2] is table
+    assert not o_g.__dict__.get("_retired")
