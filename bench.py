@@ -52,6 +52,7 @@ import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+T_START = time.perf_counter()
 
 PEAK = {"bf16": 2.5e15, "fp32": 157.3e12}  # dense MFMA (MI355X_MICROARCH.md; no sparsity)
 HBM_PEAK = 8.0e12
@@ -842,6 +843,7 @@ def main():
         others = {}
         for cfg in ("c1", "c2", "c3", "c4", "c4_fp32", "m_fp32", "m_shard8"):
             oargs.steps, oargs.warmup = CONFIG_DEFAULT_STEPS[cfg]
+            print(f"bench: config {cfg} ({time.perf_counter() - T_START:.0f} s)", file=sys.stderr, flush=True)
             try:
                 r, owl, _, _ = measure(cfg, oargs, dev, rank, world, with_kernels=not cfg.startswith("c4"))
                 others[cfg] = r

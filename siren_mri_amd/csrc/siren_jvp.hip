@@ -1180,6 +1180,188 @@ __global__ __launch_bounds__(512) void jvp_adj_kernel(JAdjArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// The tangent streams of a hidden layer, STACKED BY ROW (replaces jvp_nt_kernel<JMODE_FWD> when the
+// primal stream is given and there is no Laplacian stream): U_l^k = (w0 cos(P_{l-1}) U_{l-1}^k) W_l^T
+// for all C tangent streams of the same 64 rows in one workgroup, so each operand element's
+// phase is loaded and its cosine formed ONCE for the C streams (jvp_nt_kernel's stacked rows hold
+// the streams of a row in different tiles: C loads and C cosines per element) — the layout of
+// jvp_adj_kernel: 8 waves, wave (wm, wn) owns rows 32 wm .. + 31 of EVERY stream and features
+// 64 wn .. + 63; K chunks of 32 staged through LDS (fp32 rows padded to 33 words / bf16 to 40),
+// the next chunk's raw phases, tangents and weights in registers during this chunk's MFMAs.
+// Same products as jvp_nt_kernel (w0 * cos(p) * u, rounded to the operand type) and the same K
+// order, so the tangents are bit-identical to the stacked-row kernel's.
+struct JTanArgs {
+  const void* P;   // [B][N][K] phase_t of layer l - 1
+  const float* U;  // [B][Su][N][K] tangents of layer l - 1 (streams 0..C-1 used)
+  const void* W;   // [nb_w][Nout][K] op_t: W_l
+  float* Uout;     // [B][Su][N][Nout] tangents of layer l
+  int64_t N;
+  int Su;
+  int64_t w_bstride;
+  int K, Nout;
+  float w0;
+};
+
+template <int PREC, int C>
+__global__ __launch_bounds__(512) void jvp_tan_kernel(JTanArgs a) {
+  using PT = Prec<PREC>;
+  using phase_t = typename PT::phase_t;
+  using op_t = typename PT::op_t;
+  constexpr bool BF = PREC == kPrecBF16;
+  constexpr int ROW = JNTLds<PREC>::ROW;
+  __shared__ __attribute__((aligned(16))) op_t As[C * JADJ_ROWS * ROW];
+  __shared__ __attribute__((aligned(16))) op_t Bs[JADJ_BN * ROW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int64_t b = blockIdx.y;
+  const int64_t N = a.N;
+  const int64_t n0 = (int64_t)blockIdx.x * JADJ_ROWS;
+  const int K = a.K;
+  const int64_t plane = N * (int64_t)K;
+  const op_t* W = (const op_t*)a.W + b * a.w_bstride;
+  const phase_t* Pg = (const phase_t*)a.P + b * plane;
+  const float* Ug = a.U + b * (int64_t)a.Su * plane;
+
+  f32x16 acc[C][2];
+#pragma unroll
+  for (int s = 0; s < C; ++s)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[s][j][e] = 0.f;
+
+  // A chunk: 64 rows x 32 k in units of 4 -> one unit per thread (row tid >> 3, k 4 (tid & 7)),
+  // the same unit in every stream; B chunk: 256 x 32 -> 4 units per thread.
+  const int ar = tid >> 3, akq = (tid & 7) * 4;
+  const int64_t an = n0 + ar;
+  const bool arow = an < N;
+  phase_t praw[4];
+  float uraw[C][4];
+  float breg[4][4];
+  auto load = [&](int k0) {
+    if (arow) {
+      const int64_t idx = an * K + k0 + akq;
+      if constexpr (BF) {
+        const u16x4 pv = *(const u16x4*)(Pg + idx);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) praw[e] = pv[e];
+      } else {
+        const f32x4 pv = *(const f32x4*)(Pg + idx);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) praw[e] = pv[e];
+      }
+#pragma unroll
+      for (int s = 0; s < C; ++s) {
+        const f32x4 uv = *(const f32x4*)(Ug + (int64_t)s * plane + idx);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) uraw[s][e] = uv[e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        praw[e] = 0;
+#pragma unroll
+        for (int s = 0; s < C; ++s) uraw[s][e] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int u = tid + 512 * q;
+      const int c = u >> 3, k = k0 + (u & 7) * 4;
+      if (c < a.Nout) {
+        if constexpr (BF) {
+          const bf16x4 v = *(const bf16x4*)(W + (int64_t)c * K + k);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) breg[q][e] = (float)v[e];
+        } else {
+          const f32x4 v = *(const f32x4*)((const float*)W + (int64_t)c * K + k);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) breg[q][e] = v[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) breg[q][e] = 0.f;
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float wc = a.w0 * PT::cosp(praw[e]);  // one cosine for the C streams
+#pragma unroll
+      for (int s = 0; s < C; ++s) As[(s * JADJ_ROWS + ar) * ROW + akq + e] = from_f32<op_t>(wc * uraw[s][e]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int u = tid + 512 * q;
+      const int c = u >> 3, kq = (u & 7) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Bs[c * ROW + kq + e] = from_f32<op_t>(breg[q][e]);
+    }
+  };
+
+  const int r32 = lane & 31, h = lane >> 5;
+  const int nk = K / JNT_KC;
+  load(0);
+  for (int kc = 0; kc < nk; ++kc) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (kc + 1 < nk) load((kc + 1) * JNT_KC);
+    if constexpr (BF) {
+#pragma unroll
+      for (int ks = 0; ks < JNT_KC / 16; ++ks) {
+        bf16x8 af[C], bfr[2];
+#pragma unroll
+        for (int s = 0; s < C; ++s)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) af[s][e] = As[(s * JADJ_ROWS + 32 * wm + r32) * ROW + ks * 16 + h * 8 + e];
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bfr[bn][e] = Bs[(64 * wn + 32 * bn + r32) * ROW + ks * 16 + h * 8 + e];
+#pragma unroll
+        for (int s = 0; s < C; ++s)
+#pragma unroll
+          for (int bn = 0; bn < 2; ++bn)
+            acc[s][bn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bfr[bn], acc[s][bn], 0, 0, 0);
+      }
+    } else {
+#pragma unroll 4
+      for (int ks = 0; ks < JNT_KC / 2; ++ks) {
+        float af[C], bfr[2];
+#pragma unroll
+        for (int s = 0; s < C; ++s) af[s] = As[(s * JADJ_ROWS + 32 * wm + r32) * ROW + 2 * ks + h];
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn) bfr[bn] = Bs[(64 * wn + 32 * bn + r32) * ROW + 2 * ks + h];
+#pragma unroll
+        for (int s = 0; s < C; ++s)
+#pragma unroll
+          for (int bn = 0; bn < 2; ++bn)
+            acc[s][bn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bfr[bn], acc[s][bn], 0, 0, 0);
+      }
+    }
+  }
+
+  // U_l^k [n][f] = acc (pre-activation tangents: no bias); a lane's 16 elements of a tile are 16
+  // rows of one column, the 32 lanes of a half-wave 32 consecutive columns (128-byte rows)
+  const int64_t oplane = N * (int64_t)a.Nout;
+  float* Uo = a.Uout + b * (int64_t)a.Su * oplane;
+#pragma unroll
+  for (int bn = 0; bn < 2; ++bn) {
+    const int f = 64 * wn + 32 * bn + r32;
+    if (f >= a.Nout) continue;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int64_t n = n0 + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (n >= N) continue;
+#pragma unroll
+      for (int s = 0; s < C; ++s) Uo[(int64_t)s * oplane + n * a.Nout + f] = acc[s][bn][e];
+    }
+  }
+}
+
 // First layer adjoint: dW0[f][c] = sum_n a_bar[n][f] x[n][c] + sum_n u_bar^c[n][f] (c < C),
 // db0[f] = sum_n a_bar[n][f], dx[n][c] = sum_f a_bar[n][f] W0[f][c]. Thread per feature column;
 // dx via a separate pass (jvp_first_dx_kernel).

@@ -101,6 +101,7 @@ int g_pair_roles = 3;      // debug timing: which pair_ring roles run (results a
 bool g_dx_stagger = false;  // middle/top input-gradient ring: staggered wave halves (measured slower: +5-9 us/step)
 bool g_tail_reduce = true;  // a pair launch reduces the previous pair launch's slabs (no reduce launch)
 bool g_jvp_adj = true;
+bool g_jvp_tan = true;      // tangent streams of a hidden layer stacked by row (jvp_tan_kernel)
 bool g_jvp_tn2 = true;      // fp32 analytic-derivative weight gradients on jvp_tn2_kernel      // analytic-derivative backward: adjoint GEMM + combine in one launch (jvp_adj_kernel)
 // pair_ring role split, input-gradient workgroups per 32 of the grid, per pair kind (middle, top,
 // bottom); 16 = the paired mapping (npair + npair, same tiles on one XCD)
@@ -1338,6 +1339,32 @@ int jvp_forward_impl(const siren_mlp_desc* d, int order, const float* x, float* 
     a.K = d->dims[l];
     a.Nout = d->dims[l + 1];
     a.w0 = d->w0;
+    if (PREC == kPrecF32 && primal && !a.lap && g_jvp_tan && jl.C >= 1 && jl.C <= 4 && a.Nout <= JADJ_BN &&
+        a.K % JNT_KC == 0) {
+      // the tangent streams only, stacked by row: one phase load and cosine per element
+      JTanArgs t;
+      t.P = a.P;
+      t.U = a.U;
+      t.W = a.W;
+      t.Uout = a.Uout;
+      t.N = g.rows;
+      t.Su = jl.Su;
+      t.w_bstride = a.w_bstride;
+      t.K = a.K;
+      t.Nout = a.Nout;
+      t.w0 = a.w0;
+      const dim3 tg((unsigned)cdiv(g.rows, JADJ_ROWS), (unsigned)g.nb);
+      // (fp32 only: the primal stream is given by the fp32 forward alone, jvp_primal_check)
+      constexpr int TP = kPrecF32;
+      switch (jl.C) {
+        case 1: hipLaunchKernelGGL((jvp_tan_kernel<TP, 1>), tg, dim3(512), 0, st, t); break;
+        case 2: hipLaunchKernelGGL((jvp_tan_kernel<TP, 2>), tg, dim3(512), 0, st, t); break;
+        case 3: hipLaunchKernelGGL((jvp_tan_kernel<TP, 3>), tg, dim3(512), 0, st, t); break;
+        default: hipLaunchKernelGGL((jvp_tan_kernel<TP, 4>), tg, dim3(512), 0, st, t); break;
+      }
+      if ((rc = check_launch("jvp_tan"))) return rc;
+      continue;
+    }
     dim3 grid((unsigned)cdiv((int64_t)jl.S * g.rows - a.srow0, JNT_BM), (unsigned)cdiv(a.Nout, JNT_BN), (unsigned)g.nb);
     if (a.lap) hipLaunchKernelGGL((jvp_nt_kernel<PREC, JMODE_FWD, true>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((jvp_nt_kernel<PREC, JMODE_FWD>), grid, dim3(256), 0, st, a);
@@ -3019,6 +3046,10 @@ int siren_config_set(const char* key, int64_t value) {
     g_jvp_adj = value != 0;
     return SIREN_OK;
   }
+  if (key && strcmp(key, "jvp_tan") == 0 && (value == 0 || value == 1)) {
+    g_jvp_tan = value != 0;
+    return SIREN_OK;
+  }
   if (key && strcmp(key, "jvp_tn2") == 0 && (value == 0 || value == 1)) {
     g_jvp_tn2 = value != 0;
     return SIREN_OK;
@@ -3058,6 +3089,7 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "pair_tail_reduce") == 0) return g_tail_reduce ? 1 : 0;
   if (key && strcmp(key, "jvp_adj") == 0) return g_jvp_adj ? 1 : 0;
   if (key && strcmp(key, "jvp_tn2") == 0) return g_jvp_tn2 ? 1 : 0;
+  if (key && strcmp(key, "jvp_tan") == 0) return g_jvp_tan ? 1 : 0;
   if (key && strcmp(key, "dx_stagger") == 0) return g_dx_stagger ? 1 : 0;
   if (key && strcmp(key, "pair_ring") == 0) return g_pair_ring ? 1 : 0;
   if (key && strcmp(key, "debug_keep_p0") == 0) return g_keep_p0 ? 1 : 0;

@@ -9,9 +9,11 @@ so `state_dict`s and HyperNetwork parameter dicts interoperate with the referenc
 
 What changes is where the work runs: an FCBlock with nonlinearity='sine' executes its whole
 [BatchLinear -> Sine] stack as ONE native gfx950 forward call and ONE native backward call
-(siren_mri_amd.ops.siren_mlp, libsiren_mri_amd.so). There is no CPU/eager fallback for it: on a
-CPU tensor it raises. Non-sine FCBlocks (the HyperNetwork's ReLU MLPs) and the conv encoder are
-not on the SIREN hot path and run as ordinary PyTorch(-ROCm) modules.
+(siren_mri_amd.ops.siren_mlp, libsiren_mri_amd.so). A CUDA tensor never falls back to anything
+else (the ops raise if the library is missing). A CPU tensor — config 1 "on CPU (plumbing, no
+GPU)" — runs the stack as plain PyTorch ops on the host (cpu_stack.py), selected by device only.
+Non-sine FCBlocks (the HyperNetwork's ReLU MLPs) and the conv encoder are not on the SIREN hot
+path and run as ordinary PyTorch(-ROCm) modules.
 
 Deliberate deviations from the reference:
   * ImageDownsampling keeps `sidelength` as a device-agnostic buffer instead of calling
@@ -309,7 +311,8 @@ class SingleBVPNet(MetaModule):
             coords = self.image_downsampling(coords)
         output = self.net(coords, get_subdict(params, "net"))
         out = {"model_in": coords_org, "model_out": output}
-        if self.net.nonlinearity == "sine" and not self.image_downsampling.downsample:
+        if self.net.nonlinearity == "sine" and not self.image_downsampling.downsample and output.is_cuda:
+            # (on a CPU device the stack's autograd graph gives the derivatives, as in the reference)
             from .diff_operators import register_siren_output
             register_siren_output(output, coords_org, self.net, get_subdict(params, "net"))
         return out

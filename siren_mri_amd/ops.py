@@ -673,6 +673,16 @@ def siren_mlp(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence
     n = len(weights)
     if len(biases) != n:
         raise ValueError("siren_mlp: weights and biases differ in length")
+    if x.device.type == "cpu":
+        # a CPU tensor: the stack as plain PyTorch ops on the host (config 1 "on CPU", cpu_stack.py);
+        # CUDA tensors never come here — they take the native kernels or raise
+        if return_saved:
+            raise RuntimeError("siren_mri_amd: return_saved needs the native (GPU) stack")
+        from . import cpu_stack
+        if ff_B is not None:
+            from .features import fourier_features
+            x = fourier_features(x, ff_B)
+        return cpu_stack.sine_stack(x, weights, biases, float(w0), outermost_linear)
     if x.dtype == torch.float64:
         return _siren_mlp64(x, weights, biases, w0, outermost_linear, return_saved, ff_B)
     prec = _native.precision_code(precision or _DEFAULT_PRECISION)

@@ -40,10 +40,45 @@ def test_meta_named_parameters_order_and_subdict():
     assert meta.get_subdict(None, "net") is None
 
 
-def test_sine_forward_on_cpu_raises_no_fallback():
-    m = modules.SingleBVPNet(type="sine", hidden_features=32, num_hidden_layers=1)
-    with pytest.raises(RuntimeError, match="no CPU fallback"):
-        m({"coords": dataio.get_mgrid(4)[None]})
+def test_sine_forward_on_cpu_is_the_cpu_device_path():
+    """A CPU tensor runs the stack as plain PyTorch ops on the host (cpu_stack.py, config 1 "on
+    CPU"): the REFERENCE's recorded forward (shared and batched params), gradient and laplace
+    (forward.npz) through the package's own modules and diff_operators."""
+    d = load("forward.npz")
+    m = modules.SingleBVPNet(type="sine", hidden_features=64, num_hidden_layers=2)
+    m.load_state_dict({k[len("param/"):]: torch.from_numpy(d[k]) for k in d.files if k.startswith("param/")})
+    out = m({"coords": torch.from_numpy(d["coords"])})
+    assert orc.norm_rel(out["model_out"].detach(), torch.from_numpy(d["model_out"])) < 1e-5
+    g = diff_operators.gradient(out["model_out"], out["model_in"])
+    assert orc.norm_rel(g.detach(), torch.from_numpy(d["gradient"])) < 1e-5
+    lap = diff_operators.laplace(out["model_out"], out["model_in"])
+    assert orc.norm_rel(lap.detach(), torch.from_numpy(d["laplace"])) < 1e-4
+    params = {k: torch.stack([v, v * 1.05]) for k, v in m.state_dict().items()}
+    outb = m({"coords": torch.from_numpy(d["coords"]).repeat(2, 1, 1)}, params=params)
+    assert orc.norm_rel(outb["model_out"].detach(), torch.from_numpy(d["batched_out"])) < 1e-5
+    from siren_mri_amd import cpu_stack
+    with pytest.raises(RuntimeError, match="CPU tensors only"):
+        cpu_stack.sine_stack(torch.zeros(1, 2, device="meta"), [], [], 30.0)
+
+
+def test_config1_fit_on_cpu_reproduces_reference_trajectory(tmp_path):
+    """Config 1 on a GPU-less host (VERDICT r5 missing 2): experiment_scripts/train_img.py's fit —
+    SingleBVPNet 2-256-256-1 (num_hidden_layers=1) on the 64^2 cameraman, image_mse, Adam 1e-4 —
+    through the package's own modules on CPU tensors reproduces the reference's recorded 10-step
+    training.train trajectory (train_c1.npz: losses and final parameters)."""
+    d = load("train_c1.npz")
+    model = modules.SingleBVPNet(type="sine", hidden_features=256, num_hidden_layers=1, sidelength=(64, 64))
+    model.load_state_dict({k[len("init/"):]: torch.from_numpy(d[k]) for k in d.files if k.startswith("init/")})
+    loader = [({"coords": dataio.get_mgrid(64)[None]}, {"img": torch.from_numpy(d["img"])})]
+    loss_fn = lambda o, g: loss_functions.image_mse(None, o, g, high_freq=False)  # noqa: E731
+    training.train(model, loader, epochs=10, lr=1e-4, steps_til_summary=1000, epochs_til_checkpoint=1000,
+                   model_dir=str(tmp_path / "run"), loss_fn=loss_fn, summary_fn=lambda *a, **k: None)
+    losses = np.loadtxt(tmp_path / "run" / "checkpoints" / "train_losses_final.txt")
+    np.testing.assert_allclose(losses, d["losses"], rtol=1e-5)
+    sd = model.state_dict()
+    for i in range(3):
+        k = f"net.net.{i}.0.weight"
+        assert orc.norm_rel(sd[k], torch.from_numpy(d["final/" + k])) < 1e-5
 
 
 def test_relu_fcblock_runs_in_torch():

@@ -62,6 +62,8 @@ def _run(precision, encoder_precision, monkeypatch, val):
                                                           dataio.lin2img(vgt["img"], (res, res)))))
                 rec[s] = dict(val_loss=vloss, psnr=ref_psnr, image_psnr=_image_psnr(y, vgt["img"], res))
         losses.append(wl.step().detach())
+        if s % 25 == 0 or s < 3:  # progress (a silent GPU command is taken to be hung)
+            print(f"  [{precision}/{encoder_precision}] step {s}", flush=True)
     torch.cuda.synchronize()
     return init, [float(v) for v in torch.stack(losses).cpu()], rec
 

@@ -416,3 +416,55 @@ def test_create_graph_first_order_dx_without_tangent_form():
     assert torch.equal(d1.detach(), d0)
     with pytest.raises(RuntimeError, match="tangent-stream"):
         d1.square().sum().backward()
+
+
+@pytest.mark.parametrize("order,inp", [("gradient", 2), ("gradient", 1), ("gradient", 3), ("jacobian", 2)])
+@pytest.mark.parametrize("batched", [False, True])
+def test_row_stacked_tangents_match_stream_stacked(order, inp, batched):
+    """jvp_tan_kernel (the hidden layers' tangent streams stacked by ROW: one phase load and one
+    cosine per operand element for the C streams; option jvp_tan, default on, fp32 with the
+    forward's primal) against jvp_nt_kernel's stream-stacked rows: the same operand products and
+    the same K order, so the values and every gradient are bit-identical. Ragged rows (41^2, not
+    a multiple of the 64-row tile); 1..3 input dimensions."""
+    from siren_mri_amd import _native, jvp
+    from siren_mri_amd.meta import get_subdict
+    out = 2 if order == "jacobian" else 1
+    m = _model(256, 3, 35, "fp32", out=out, inp=inp)
+    B = 2 if batched else 1
+    g = torch.Generator().manual_seed(7)
+    coords = (torch.rand(B, 41 * 41, inp, generator=g) * 2 - 1).to(DEV)
+    params = None
+    if batched:
+        params = {k: torch.stack([v * (1 + 0.03 * i) for i in range(B)]).requires_grad_(True)
+                  for k, v in m.state_dict().items()}
+    fn = {"gradient": jvp.siren_gradient, "jacobian": jvp.siren_jacobian}[order]
+    res = []
+    assert _native.get_option("jvp_tan") == 1
+    for tan in (1, 0):
+        _native.set_option("jvp_tan", tan)
+        try:
+            m.zero_grad(set_to_none=True)
+            if params is not None:
+                for p in params.values():
+                    p.grad = None
+            x = coords.clone().requires_grad_(True)
+            o = m({"coords": x}, params=params)
+            primal = getattr(o["model_out"], "_siren_primal", None)
+            assert primal is not None
+            sub = get_subdict(params, "net") if params is not None else None
+            val = fn(o["model_in"], m.net, sub, primal=primal)
+            torch.manual_seed(5)
+            w = torch.randn_like(val)
+            (val * w).sum().backward()
+            torch.cuda.synchronize()
+            grads = [p.grad.clone() for p in (params.values() if params is not None else m.parameters())
+                     if p.grad is not None]
+            res.append((val.detach().clone(), grads, o["model_in"].grad.clone()))
+        finally:
+            _native.set_option("jvp_tan", 1)
+    (v1, g1, dx1), (v0, g0, dx0) = res
+    assert torch.equal(v1, v0)
+    assert len(g1) == len(g0) > 0
+    for a, b in zip(g1, g0):
+        assert torch.equal(a, b)
+    assert torch.equal(dx1, dx0)
