@@ -307,6 +307,18 @@ int64_t siren_conv_wrw_workspace_bytes(int N, int H, int W);
  * the encoder's MIOpen forward / input-gradient convolutions for this shape. */
 int siren_conv_fwd_k5(const void* x, const void* w, const void* bias, int relu, void* y, int N, int H, int W, int C,
                       void* stream);
+/* The input gradient of a residual-block convolution (siren_conv_fwd_k5 on the flipped, transposed
+ * filter wf) with the encoder's next backward pass in its epilogue (replaces siren_conv_fwd_k5 +
+ * siren_enc_relu_bwd / siren_enc_res_bwd; the arithmetic of those passes element for element):
+ *   mode 1: out = bf16((g [+ g2]) * (m > 0)), db = channel sums of out        (a ReLU's backward)
+ *   mode 2: out = bf16((g + g2) * (m > 0)) (skip gradient), out2 = out * (bf16(pa + cb) > 0),
+ *           db = channel sums of out2                     (Conv2dResBlock's tail, modules.py:433-450)
+ * with g = bf16(conv(dy, wf)). ws: N * H / 2 * 128 floats of partial sums (reduced in a fixed order
+ * by a second launch: deterministic). Replaces the autograd ReLU / add backward of
+ * modules.py:372-380,446-450 under the fused bf16 encoder node. */
+int siren_conv_dgrad_k5_fused(int mode, const void* dy, const void* wf, const void* g2, const void* m, const void* pa,
+                              const void* cb, void* out, void* out2, float* db, int N, int H, int W, int C, void* ws,
+                              int64_t ws_bytes, void* stream);
 int siren_conv_wrw_k5(const void* x, const void* dy, int N, int H, int W, int C, float* dw, void* ws, int64_t ws_bytes,
                       void* stream);
 /* The encoder's other convolution shapes (round 5; ConvImgEncoder's cnn[0], modules.py:351 — 64 ->

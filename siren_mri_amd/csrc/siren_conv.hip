@@ -238,8 +238,27 @@ struct ConvFArgs {
   bf16* y;           // [N][H][128][128]
   int N, H;
   int relu;          // with bias: y = relu(bf16(bf16(acc) + bias))
+  // gradient epilogues (EPI > 0, the input-gradient convolutions of the conv encoder's backward):
+  const bf16* g2;    // second gradient summand, or null
+  const bf16* m;     // mask source (> 0 keeps the element)
+  const bf16* pa;    // EPI_RES: the block's second convolution output a (bias-free)
+  const bf16* cb;    // EPI_RES: that convolution's bias
+  bf16* y2;          // EPI_RES: second output plane (ga)
+  float* part;       // [blocks][128] per-workgroup channel sums of the gradient the bias takes
 };
 
+// Epilogues of conv_fwd_k5_kernel. The input gradient of a ReLU'd convolution, g = bf16(acc), is
+// consumed at once by an elementwise pass in the encoder's backward (siren_encoder.hip); these
+// forms run that pass on the tile while it is in LDS, so g never goes to HBM and the pass's launch
+// and plane traffic are gone (enc_relu_bwd_kernel / enc_res_bwd_kernel arithmetic, element for
+// element; the channel sums are per-workgroup partials reduced in a fixed order by
+// conv_chan_reduce_kernel, deterministic):
+//   EPI_RELU: y = bf16((g [+ g2]) [m > 0]);                 part = sums of y
+//   EPI_RES : s = g + g2; y = bf16(s [m > 0]) (the skip gradient);
+//             y2 = y [bf16(pa + cb) > 0] (the block's pre-activation gradient); part = sums of y2
+constexpr int EPI_PLAIN = 0, EPI_RELU = 1, EPI_RES = 2;
+
+template <int EPI>
 __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
   __shared__ __attribute__((aligned(16))) char smem_cf[2 * CF_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -392,13 +411,87 @@ __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
   __syncthreads();
   // the pair's 64 KB as 16-byte buffer stores, each followed by its 2 wait states (siren_common.h
   // store_b128_ws2)
-  const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.y + ((int64_t)n * a.H + h0) * CF_W * CW_C, 2 * CF_W * CW_C * 2);
+  const int64_t pair0 = ((int64_t)n * a.H + h0) * CF_W * CW_C;  // the pair's first element
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.y + pair0, 2 * CF_W * CW_C * 2);
+  if constexpr (EPI == EPI_PLAIN) {
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int q = tid + 512 * k;        // 16-byte piece: pixel q / 16, channels 8 (q % 16)
-    const int px = q >> 4, pc = q & 15;
-    store_b128_ws2(*(const u32x4_t*)(ot + px * OROW + 16 * pc), ry, (uint32_t)(q * 16), 0);
+    for (int k = 0; k < 8; ++k) {
+      const int q = tid + 512 * k;        // 16-byte piece: pixel q / 16, channels 8 (q % 16)
+      const int px = q >> 4, pc = q & 15;
+      store_b128_ws2(*(const u32x4_t*)(ot + px * OROW + 16 * pc), ry, (uint32_t)(q * 16), 0);
+    }
+  } else {
+    // a thread's 8 pieces share its 8 channels (pc = tid % 16); every operand piece of the 8 is
+    // loaded before the first is used (one memory latency for the epilogue)
+    const int pc = tid & 15;
+    bf16x8 mv[8], gv[8], av[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t off = pair0 + (int64_t)(tid + 512 * k) * 8;
+      mv[k] = *(const bf16x8*)(a.m + off);
+      if (a.g2) gv[k] = *(const bf16x8*)(a.g2 + off);
+      if constexpr (EPI == EPI_RES) av[k] = *(const bf16x8*)(a.pa + off);
+    }
+    float cbv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cbv[e] = EPI == EPI_RES ? (float)a.cb[8 * pc + e] : 0.f;
+    const __amdgpu_buffer_rsrc_t ry2 =
+        make_rsrc(EPI == EPI_RES ? a.y2 + pair0 : a.y + pair0, 2 * CF_W * CW_C * 2);
+    float sum[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sum[e] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = tid + 512 * k;
+      const int px = q >> 4;
+      const bf16x8 gt = *(const bf16x8*)(ot + px * OROW + 16 * pc);
+      bf16x8 o, o2;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float g = (float)gt[e];
+        if (a.g2) g += (float)gv[k][e];
+        o[e] = (bf16)((float)mv[k][e] > 0.f ? g : 0.f);
+        if constexpr (EPI == EPI_RES) {
+          const float pre = (float)(bf16)((float)av[k][e] + cbv[e]);  // bf16(a + cb), enc_res_bwd's
+          o2[e] = pre > 0.f ? o[e] : (bf16)0.f;
+          sum[e] += (float)o2[e];
+        } else {
+          sum[e] += (float)o[e];
+        }
+      }
+      store_b128_ws2(__builtin_bit_cast(u32x4_t, o), ry, (uint32_t)(q * 16), 0);
+      if constexpr (EPI == EPI_RES) store_b128_ws2(__builtin_bit_cast(u32x4_t, o2), ry2, (uint32_t)(q * 16), 0);
+    }
+    // the workgroup's channel sums: [32 pixel slots][128 channels] in LDS (the tile's reads are done
+    // after the barrier), then rows added in slot order
+    __syncthreads();
+    float* red = (float*)smem_cf;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[(tid >> 4) * CW_C + 8 * pc + e] = sum[e];
+    __syncthreads();
+    if (tid < CW_C) {
+      float t = 0.f;
+#pragma unroll 8
+      for (int r = 0; r < 32; ++r) t += red[r * CW_C + tid];
+      a.part[(int64_t)blockIdx.x * CW_C + tid] = t;
+    }
   }
+}
+
+// db[c] = sum over the workgroups' partial rows part[b][c], b in order: one workgroup per channel,
+// thread t adds rows t, t + 256, ... (all loads in flight), then a fixed-order tree in LDS.
+__global__ __launch_bounds__(256) void conv_chan_reduce_kernel(const float* part, int nblk, float* db) {
+  __shared__ float red[256];
+  const int c = blockIdx.x, t = threadIdx.x;
+  float s = 0.f;
+  for (int b = t; b < nblk; b += 256) s += part[(int64_t)b * CW_C + c];
+  red[t] = s;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (t < w) red[t] += red[t + w];
+    __syncthreads();
+  }
+  if (t == 0) db[c] = red[0];
 }
 
 }  // namespace siren

@@ -2456,8 +2456,43 @@ int siren_conv_fwd_k5(const void* x, const void* w, const void* bias, int relu, 
   a.N = N;
   a.H = H;
   a.relu = relu ? 1 : 0;
-  hipLaunchKernelGGL(conv_fwd_k5_kernel, dim3((unsigned)(N * (H / 2))), dim3(512), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(conv_fwd_k5_kernel<EPI_PLAIN>, dim3((unsigned)(N * (H / 2))), dim3(512), 0, (hipStream_t)stream, a);
   return check_launch("conv_fwd_k5");
+}
+
+int siren_conv_dgrad_k5_fused(int mode, const void* dy, const void* wf, const void* g2, const void* m, const void* pa,
+                              const void* cb, void* out, void* out2, float* db, int N, int H, int W, int C, void* ws,
+                              int64_t ws_bytes, void* stream) {
+  if (C != CW_C || W != CF_W || N < 1 || H < 2 || H % 2 != 0)
+    return fail(SIREN_EINVAL, "conv_dgrad_k5_fused: needs C = %d, W = %d and H even (C = %d, N = %d, H = %d, W = %d)",
+                CW_C, CF_W, C, N, H, W);
+  if (mode != 1 && mode != 2) return fail(SIREN_EINVAL, "conv_dgrad_k5_fused: mode %d (1 relu, 2 residual tail)", mode);
+  if (!dy || !wf || !m || !out || !db || (mode == 2 && (!g2 || !pa || !cb || !out2)))
+    return fail(SIREN_EINVAL, "conv_dgrad_k5_fused: null pointer");
+  const int64_t nblk = (int64_t)N * (H / 2);
+  if (!ws || ws_bytes < nblk * CW_C * 4)
+    return fail(SIREN_ENOSPACE, "conv_dgrad_k5_fused: workspace %lld < %lld bytes", (long long)ws_bytes,
+                (long long)(nblk * CW_C * 4));
+  ConvFArgs a;
+  memset(&a, 0, sizeof(a));
+  a.x = (const bf16*)dy;
+  a.w = (const bf16*)wf;
+  a.y = (bf16*)out;
+  a.N = N;
+  a.H = H;
+  a.g2 = (const bf16*)g2;
+  a.m = (const bf16*)m;
+  a.pa = (const bf16*)pa;
+  a.cb = (const bf16*)cb;
+  a.y2 = (bf16*)out2;
+  a.part = (float*)ws;
+  hipStream_t st = (hipStream_t)stream;
+  if (mode == 1) hipLaunchKernelGGL(conv_fwd_k5_kernel<EPI_RELU>, dim3((unsigned)nblk), dim3(512), 0, st, a);
+  else hipLaunchKernelGGL(conv_fwd_k5_kernel<EPI_RES>, dim3((unsigned)nblk), dim3(512), 0, st, a);
+  int rc = check_launch("conv_dgrad_k5_fused");
+  if (rc) return rc;
+  hipLaunchKernelGGL(conv_chan_reduce_kernel, dim3(CW_C), dim3(256), 0, st, (const float*)ws, (int)nblk, db);
+  return check_launch("conv_chan_reduce");
 }
 
 }  // extern "C"

@@ -146,6 +146,34 @@ def _conv(x, wb, bb, pad, relu=False):
     return y
 
 
+# the encoder's backward passes in the input-gradient convolutions' epilogues (siren_conv_dgrad_k5_fused)
+_EPI_FUSED = [True]
+
+
+def _epilogue_ok(dy, wf):
+    """The native 5x5 kernel takes this input gradient and the encoder workspace holds its
+    per-workgroup channel sums (N H / 2 rows of 128)."""
+    if not (_EPI_FUSED[0] and _native_conv(dy, wf)):
+        return False
+    n, _, h, _ = dy.shape
+    return n * (h // 2) * 128 * 4 <= _native.enc_workspace(dy.device).numel()
+
+
+def _dgrad_fused(mode, dy, wf, g2, m, pa, cb, db, ws):
+    """The input gradient conv(dy, wf) with the next backward pass in its epilogue: mode 1 the ReLU
+    backward (out = (g [+ g2]) (m > 0)), mode 2 the residual tail's (skip gradient out, and
+    out2 = out (bf16(pa + cb) > 0)); db receives the channel sums (see siren_conv_dgrad_k5_fused)."""
+    n, _, h, w = dy.shape
+    out = torch.empty_like(m)
+    out2 = torch.empty_like(m) if mode == 2 else None
+    _native.check(_native.lib().siren_conv_dgrad_k5_fused(
+        mode, dy.data_ptr(), wf.data_ptr(), g2.data_ptr() if g2 is not None else None, m.data_ptr(),
+        pa.data_ptr() if pa is not None else None, cb.data_ptr() if cb is not None else None, out.data_ptr(),
+        out2.data_ptr() if out2 is not None else None, db.data_ptr(), n, h, w, wf.shape[1], ws.data_ptr(),
+        ws.numel(), _native.stream_handle(dy.device)), "siren_conv_dgrad_k5_fused")
+    return out, out2
+
+
 _WGRAD_NATIVE = [True]
 
 
@@ -261,6 +289,14 @@ class _EncoderBF16(torch.autograd.Function):
         gW[k] = _wgrad(ga, xin, wbs[k], pad)
         g1 = _conv(ga, ctx.wfs[k], None, pad)
         g2 = None
+        # an input-gradient convolution not yet run: (its input, filter, padding); the pass that
+        # consumes its output runs in its epilogue where the native 5x5 kernel takes it
+        # (siren_conv_dgrad_k5_fused), else g1 is formed and the pass runs on its own
+        pending = None
+
+        def form_g1():
+            return _conv(pending[0], pending[1], None, pending[2]) if pending is not None else g1
+
         # residual blocks, last to first
         for _ in range(enc._enc_nblocks):
             k -= 2
@@ -269,35 +305,48 @@ class _EncoderBF16(torch.autograd.Function):
             h = saved.pop()
             t = saved[-1]  # the block's input
             P, C = _plane(a)
-            gskip = torch.empty_like(a)
-            ga = torch.empty_like(a)
             gb[k + 1] = torch.empty(C, dtype=torch.float32, device=dev)
-            _native.check(lib.siren_enc_res_bwd(g1.data_ptr(), g2.data_ptr() if g2 is not None else None,
-                                                out.data_ptr(), a.data_ptr(), bbs[k + 1].data_ptr(), gskip.data_ptr(),
-                                                ga.data_ptr(),
-                                                gb[k + 1].data_ptr(), P, C, wsp, wsn, stream), "siren_enc_res_bwd")
+            if pending is not None and g2 is not None and _epilogue_ok(pending[0], pending[1]):
+                gskip, ga = _dgrad_fused(2, pending[0], pending[1], g2, out, a, bbs[k + 1], gb[k + 1], ws)
+            else:
+                g1 = form_g1()
+                gskip = torch.empty_like(a)
+                ga = torch.empty_like(a)
+                _native.check(lib.siren_enc_res_bwd(g1.data_ptr(), g2.data_ptr() if g2 is not None else None,
+                                                    out.data_ptr(), a.data_ptr(), bbs[k + 1].data_ptr(),
+                                                    gskip.data_ptr(), ga.data_ptr(), gb[k + 1].data_ptr(), P, C, wsp,
+                                                    wsn, stream), "siren_enc_res_bwd")
+            pending = None
             pad = convs[k + 1].padding[0]
             gW[k + 1] = _wgrad(ga, h, wbs[k + 1], pad)
-            gh = _conv(ga, ctx.wfs[k + 1], None, pad)
-            ghm = torch.empty_like(h)
             P, C = _plane(h)
             gb[k] = torch.empty(C, dtype=torch.float32, device=dev)
-            _native.check(lib.siren_enc_relu_bwd(gh.data_ptr(), None, h.data_ptr(), ghm.data_ptr(), gb[k].data_ptr(),
-                                                 P, C, wsp, wsn, stream), "siren_enc_relu_bwd")
+            if _epilogue_ok(ga, ctx.wfs[k + 1]):
+                ghm, _ = _dgrad_fused(1, ga, ctx.wfs[k + 1], None, h, None, None, gb[k], ws)
+            else:
+                gh = _conv(ga, ctx.wfs[k + 1], None, pad)
+                ghm = torch.empty_like(h)
+                _native.check(lib.siren_enc_relu_bwd(gh.data_ptr(), None, h.data_ptr(), ghm.data_ptr(),
+                                                     gb[k].data_ptr(), P, C, wsp, wsn, stream), "siren_enc_relu_bwd")
             pad = convs[k].padding[0]
             gW[k] = _wgrad(ghm, t, wbs[k], pad)
-            g1 = _conv(ghm, ctx.wfs[k], None, pad)
+            pending = (ghm, ctx.wfs[k], pad)
             g2 = gskip
         # cnn[0] and conv_theta (each followed by a ReLU); no gradient into the image
         for k in (1, 0):
             y = saved.pop()
             xin = saved[-1]
             P, C = _plane(y)
-            gm = torch.empty_like(y)
             gb[k] = torch.empty(C, dtype=torch.float32, device=dev)
-            _native.check(lib.siren_enc_relu_bwd(g1.data_ptr(), g2.data_ptr() if g2 is not None else None,
-                                                 y.data_ptr(), gm.data_ptr(), gb[k].data_ptr(), P, C, wsp, wsn,
-                                                 stream), "siren_enc_relu_bwd")
+            if pending is not None and _epilogue_ok(pending[0], pending[1]):
+                gm, _ = _dgrad_fused(1, pending[0], pending[1], g2, y, None, None, gb[k], ws)
+            else:
+                g1 = form_g1()
+                gm = torch.empty_like(y)
+                _native.check(lib.siren_enc_relu_bwd(g1.data_ptr(), g2.data_ptr() if g2 is not None else None,
+                                                     y.data_ptr(), gm.data_ptr(), gb[k].data_ptr(), P, C, wsp, wsn,
+                                                     stream), "siren_enc_relu_bwd")
+            pending = None
             pad = convs[k].padding[0]
             gW[k] = _wgrad(gm, xin, wbs[k], pad)
             if k == 1:

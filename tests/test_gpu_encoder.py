@@ -366,3 +366,36 @@ def test_image_gradient_takes_the_autocast_chain():
     finally:
         encoder.set_fused(True)
     assert orc.norm_rel(g_on.cpu(), I.grad.cpu()) < 1e-3
+
+
+@pytest.mark.parametrize("blocks,k", [(5, 7), (2, 3)])
+def test_fused_dgrad_epilogues_match_the_passes(blocks, k):
+    """The encoder's ReLU and residual-tail backward passes in the 5x5 input-gradient convolution's
+    epilogue (siren_conv_dgrad_k5_fused, encoder._EPI_FUSED) against the separate passes
+    (enc_relu_bwd / enc_res_bwd after siren_conv_fwd_k5): the same arithmetic element for element,
+    so every weight gradient is bit-identical; the bias gradients are channel sums in another fixed
+    order (1e-6). Run twice: deterministic."""
+    from siren_mri_amd import encoder
+    enc = _encoder("bf16", blocks=blocks, k=k, seed=4)
+    g = torch.Generator().manual_seed(5)
+    I = torch.randn(4, 2, 128, 128, generator=g).to(DEV)
+    ge = torch.randn(4, 128, generator=g).to(DEV)
+    assert enc._layers() is not None
+    res = []
+    for fused in (True, True, False):
+        encoder._EPI_FUSED[0] = fused
+        try:
+            res.append(_run(enc, I, ge))
+        finally:
+            encoder._EPI_FUSED[0] = True
+    (e1, g1), (e1b, g1b), (e0, g0) = res
+    assert torch.equal(e1, e0)
+    shapes = dict((n, p.shape) for n, p in enc.named_parameters())
+    for n in g1:
+        native_w = len(shapes[n]) == 4 and shapes[n][-1] > 1  # (the 1x1's weight gradient is MIOpen's)
+        if native_w:
+            assert torch.equal(g1[n], g1b[n]), n  # run to run
+            assert torch.equal(g1[n], g0[n]), n
+        else:
+            assert orc.norm_rel(g1[n].cpu(), g1b[n].cpu()) < 1e-6, n
+            assert orc.norm_rel(g1[n].cpu(), g0[n].cpu()) < 1e-6, n
