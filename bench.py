@@ -270,9 +270,10 @@ def c4_batch(dev, n_slices, seed=0):
 
 
 def build_c4(args, dev, rank, world, precision, encoder_precision="bf16"):
-    # MIOpen's find (autotuned) convolution algorithms for the encoder: its few conv shapes are
-    # searched once during the warm-up steps
-    torch.backends.cudnn.benchmark = True
+    # MIOpen's find (autotuned) convolution algorithms for the bf16 encoder's 1x1 convolution: searched
+    # once during the warm-up steps. The fp32 encoder (c4_fp32: every convolution on MIOpen) takes
+    # MIOpen's immediate-mode choice: a find over its fp32 shapes runs for minutes
+    torch.backends.cudnn.benchmark = encoder_precision == "bf16"
     from functools import partial
     from siren_mri_amd import fusion, loss_functions, meta_modules, training
     from siren_mri_amd.features import GaussianFourierFeatureTransform
@@ -325,7 +326,8 @@ def build_c4(args, dev, rank, world, precision, encoder_precision="bf16"):
                     "seeded CS-Cartesian masks, FF B = randn(2, 8) * 21 (seed 0)",
                     {"optimizer": opt, "encoder_flops_per_step": enc, "encoder_precision": encoder_precision,
                      "model": model, "inp": inp, "ff": ff, "loss_fn": loss_fn,
-                     "conv_algorithms": "MIOpen find (torch.backends.cudnn.benchmark)"})
+                     "conv_algorithms": ("MIOpen find (torch.backends.cudnn.benchmark)" if encoder_precision == "bf16"
+                                         else "MIOpen immediate mode")})
 
 
 def build(cfg, args, dev, rank, world, precision=None):

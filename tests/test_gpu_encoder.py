@@ -396,6 +396,11 @@ def test_fused_dgrad_epilogues_match_the_passes(blocks, k):
         if native_w:
             assert torch.equal(g1[n], g1b[n]), n  # run to run
             assert torch.equal(g1[n], g0[n]), n
+        elif len(shapes[n]) == 4:
+            # the 1x1 convolution's weight gradient: MIOpen's, not bit-reproducible run to run
+            # (measured 6e-6 between two identical calls); its input is bit-identical in all runs
+            assert orc.norm_rel(g1[n].cpu(), g1b[n].cpu()) < 1e-4, n
+            assert orc.norm_rel(g1[n].cpu(), g0[n].cpu()) < 1e-4, n
         else:
             assert orc.norm_rel(g1[n].cpu(), g1b[n].cpu()) < 1e-6, n
             assert orc.norm_rel(g1[n].cpu(), g0[n].cpu()) < 1e-6, n
