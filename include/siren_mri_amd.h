@@ -307,6 +307,12 @@ int64_t siren_conv_wrw_workspace_bytes(int N, int H, int W);
  * the encoder's MIOpen forward / input-gradient convolutions for this shape. */
 int siren_conv_fwd_k5(const void* x, const void* w, const void* bias, int relu, void* y, int N, int H, int W, int C,
                       void* stream);
+/* A residual block's second convolution with the block's tail in its epilogue (replaces
+ * siren_conv_fwd_k5 + siren_enc_res_fwd, element for element): a_out = bf16(conv(x, w)) (bias-free,
+ * kept for the backward), out = relu(bf16(relu(bf16(a_out + cb)) + t)), t the block input
+ * (Conv2dResBlock.forward, modules.py:446-450). */
+int siren_conv_fwd_k5_res(const void* x, const void* w, const void* cb, const void* t, void* a_out, void* out, int N,
+                          int H, int W, int C, void* stream);
 /* The input gradient of a residual-block convolution (siren_conv_fwd_k5 on the flipped, transposed
  * filter wf) with the encoder's next backward pass in its epilogue (replaces siren_conv_fwd_k5 +
  * siren_enc_relu_bwd / siren_enc_res_bwd; the arithmetic of those passes element for element):

@@ -63,6 +63,7 @@ EXPORTED_SYMBOLS = (
     "siren_conv_wrw_k5",
     "siren_conv_fwd_k5",
     "siren_conv_dgrad_k5_fused",
+    "siren_conv_fwd_k5_res",
     "siren_conv_check",
     "siren_conv_fwd",
     "siren_conv_wrw_ws_bytes",
@@ -296,6 +297,8 @@ def _declare(lib):
     lib.siren_conv_fwd_k5.restype = ci
     lib.siren_conv_dgrad_k5_fused.argtypes = [ci, vp, vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, vp, i64, vp]
     lib.siren_conv_dgrad_k5_fused.restype = ci
+    lib.siren_conv_fwd_k5_res.argtypes = [vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, vp]
+    lib.siren_conv_fwd_k5_res.restype = ci
     lib.siren_conv_check.argtypes = [ci, ci, ci, ci, ci, ci, ci]
     lib.siren_conv_check.restype = ci
     lib.siren_conv_fwd.argtypes = [vp, vp, vp, ci, vp, ci, ci, ci, ci, ci, ci, vp]

@@ -256,7 +256,10 @@ struct ConvFArgs {
 //   EPI_RELU: y = bf16((g [+ g2]) [m > 0]);                 part = sums of y
 //   EPI_RES : s = g + g2; y = bf16(s [m > 0]) (the skip gradient);
 //             y2 = y [bf16(pa + cb) > 0] (the block's pre-activation gradient); part = sums of y2
-constexpr int EPI_PLAIN = 0, EPI_RELU = 1, EPI_RES = 2;
+//   EPI_RESFWD (the forward of Conv2dResBlock's tail, enc_res_fwd_kernel's arithmetic): y = a =
+//             bf16(acc) (kept for the backward), y2 = relu(bf16(relu(bf16(a + cb)) + g2)), g2 the
+//             block input
+constexpr int EPI_PLAIN = 0, EPI_RELU = 1, EPI_RES = 2, EPI_RESFWD = 3;
 
 template <int EPI>
 __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
@@ -419,6 +422,30 @@ __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
       const int q = tid + 512 * k;        // 16-byte piece: pixel q / 16, channels 8 (q % 16)
       const int px = q >> 4, pc = q & 15;
       store_b128_ws2(*(const u32x4_t*)(ot + px * OROW + 16 * pc), ry, (uint32_t)(q * 16), 0);
+    }
+  } else if constexpr (EPI == EPI_RESFWD) {
+    const int pc = tid & 15;
+    bf16x8 xv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) xv[k] = *(const bf16x8*)(a.g2 + pair0 + (int64_t)(tid + 512 * k) * 8);
+    float cbv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cbv[e] = (float)a.cb[8 * pc + e];
+    const __amdgpu_buffer_rsrc_t ry2 = make_rsrc(a.y2 + pair0, 2 * CF_W * CW_C * 2);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = tid + 512 * k;
+      const int px = q >> 4;
+      const bf16x8 av = *(const bf16x8*)(ot + px * OROW + 16 * pc);
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = (float)(bf16)((float)av[e] + cbv[e]);
+        const float s = (float)(bf16)(fmaxf(v, 0.f) + (float)xv[k][e]);
+        o[e] = (bf16)fmaxf(s, 0.f);
+      }
+      store_b128_ws2(__builtin_bit_cast(u32x4_t, av), ry, (uint32_t)(q * 16), 0);
+      store_b128_ws2(__builtin_bit_cast(u32x4_t, o), ry2, (uint32_t)(q * 16), 0);
     }
   } else {
     // a thread's 8 pieces share its 8 channels (pc = tid % 16); every operand piece of the 8 is

@@ -2460,6 +2460,26 @@ int siren_conv_fwd_k5(const void* x, const void* w, const void* bias, int relu, 
   return check_launch("conv_fwd_k5");
 }
 
+int siren_conv_fwd_k5_res(const void* x, const void* w, const void* cb, const void* t, void* a_out, void* out, int N,
+                          int H, int W, int C, void* stream) {
+  if (C != CW_C || W != CF_W || N < 1 || H < 2 || H % 2 != 0)
+    return fail(SIREN_EINVAL, "conv_fwd_k5_res: needs C = %d, W = %d and H even (C = %d, N = %d, H = %d, W = %d)", CW_C,
+                CF_W, C, N, H, W);
+  if (!x || !w || !cb || !t || !a_out || !out) return fail(SIREN_EINVAL, "conv_fwd_k5_res: null pointer");
+  ConvFArgs a;
+  memset(&a, 0, sizeof(a));
+  a.x = (const bf16*)x;
+  a.w = (const bf16*)w;
+  a.y = (bf16*)a_out;
+  a.N = N;
+  a.H = H;
+  a.g2 = (const bf16*)t;
+  a.cb = (const bf16*)cb;
+  a.y2 = (bf16*)out;
+  hipLaunchKernelGGL(conv_fwd_k5_kernel<EPI_RESFWD>, dim3((unsigned)(N * (H / 2))), dim3(512), 0, (hipStream_t)stream, a);
+  return check_launch("conv_fwd_k5_res");
+}
+
 int siren_conv_dgrad_k5_fused(int mode, const void* dy, const void* wf, const void* g2, const void* m, const void* pa,
                               const void* cb, void* out, void* out2, float* db, int N, int H, int W, int C, void* ws,
                               int64_t ws_bytes, void* stream) {

@@ -230,11 +230,20 @@ class _EncoderBF16(torch.autograd.Function):
         k = 2
         for _ in range(enc._enc_nblocks):
             h = _conv(t, wbs[k], bbs[k], convs[k].padding[0], relu=True)
-            a = _conv(h, wbs[k + 1], None, convs[k + 1].padding[0])  # bias added in the tail pass
-            out = torch.empty_like(a)
-            P, C = _plane(a)
-            _native.check(lib.siren_enc_res_fwd(a.data_ptr(), bbs[k + 1].data_ptr(), t.data_ptr(), out.data_ptr(), P,
-                                                C, stream), "siren_enc_res_fwd")
+            if _EPI_FUSED[0] and _native_conv(h, wbs[k + 1]):
+                # the block's tail in the second convolution's epilogue (siren_conv_fwd_k5_res)
+                a = torch.empty_like(h)
+                out = torch.empty_like(h)
+                n_, _, h_, w_ = h.shape
+                _native.check(lib.siren_conv_fwd_k5_res(h.data_ptr(), wbs[k + 1].data_ptr(), bbs[k + 1].data_ptr(),
+                                                        t.data_ptr(), a.data_ptr(), out.data_ptr(), n_, h_, w_,
+                                                        h.shape[1], stream), "siren_conv_fwd_k5_res")
+            else:
+                a = _conv(h, wbs[k + 1], None, convs[k + 1].padding[0])  # bias added in the tail pass
+                out = torch.empty_like(a)
+                P, C = _plane(a)
+                _native.check(lib.siren_enc_res_fwd(a.data_ptr(), bbs[k + 1].data_ptr(), t.data_ptr(), out.data_ptr(),
+                                                    P, C, stream), "siren_enc_res_fwd")
             saved += [h, a, out]
             t = out
             k += 2
