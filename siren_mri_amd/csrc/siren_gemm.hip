@@ -1780,16 +1780,9 @@ constexpr int dw_ring_lds_bytes() {
 // r_end arrive as zeros (dZ = 0: no contribution to dW, db or the output-layer sums) and no lane
 // ever tests a row bound. Per chunk and lane, VALU work is the convert pass alone: every LDS
 // address is a per-lane base fixed at entry plus the stage base plus an immediate offset.
-// SIREN_TOP_DW_FACT 1: the top layer's weight-gradient role with one output takes the per-feature
-// factor W_L w0 out of its GEMM (see the convert pass); 0: dZ_top formed in full, as the input-
-// gradient role does
-#ifndef SIREN_TOP_DW_FACT
-#define SIREN_TOP_DW_FACT 0
-#endif
 template <int RECC = 0, int TOPO = 0>
 DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const int64_t r_end, const int64_t split) {
   using PT = Prec<kPrecBF16>;
-  constexpr bool TOP_FACT = SIREN_TOP_DW_FACT && TOPO == 1;
   constexpr int M = 256, N = 256, KC = 32, S = RING_S;
   constexpr int X_BYTES = RECC > 0 ? KC * RECC * 4 : 0;
   constexpr int G_BYTES = TOPO > 0 ? KC * TOPO * 4 : 0;
@@ -1936,36 +1929,23 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
 #pragma unroll
       for (int o = 0; o < TOP_MAXO; ++o) gg[o] = o < TOPO ? gt[o] * dys : 0.f;
       bf16x8 dz;
-      if constexpr (TOP_FACT) {
-        // one output: dZ_top = gg (W_L w0) cos(P_top); the per-feature factor W_L w0 is taken out
-        // of the GEMM (dW_top rows and db_top are scaled by it once, after the rows): the MFMA
-        // operand is bf16(gg cos(P_top)) and db sums the unrounded products
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float pc = gg[0] * PT::cosp(pt[e]);
-          dz[e] = (bf16)pc;
-          dbacc[e] += pc;
-          tdw[0][e] = fmaf(gg[0], PT::sinp(pt[e]), tdw[0][e]);
-        }
-      } else {
+      for (int e = 0; e < 8; ++e) {
+        float dh = gg[0] * twl[0][e];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float dh = gg[0] * twl[0][e];
+        for (int o = 1; o < TO; ++o) dh = fmaf(gg[o], twl[o][e], dh);
+        dz[e] = (bf16)(dh * PT::cosp(pt[e]));
+        const float sv = PT::sinp(pt[e]);
 #pragma unroll
-          for (int o = 1; o < TO; ++o) dh = fmaf(gg[o], twl[o][e], dh);
-          dz[e] = (bf16)(dh * PT::cosp(pt[e]));
-          const float sv = PT::sinp(pt[e]);
-#pragma unroll
-          for (int o = 0; o < TO; ++o) tdw[o][e] = fmaf(gg[o], sv, tdw[o][e]);
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) dbacc[e] += (float)dz[e];
+        for (int o = 0; o < TO; ++o) tdw[o][e] = fmaf(gg[o], sv, tdw[o][e]);
       }
       *(bf16x8*)(Db + off) = dz;
       if (cth == 0) {
 #pragma unroll
         for (int o = 0; o < TO; ++o) tdb[o] += gg[o];
       }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dbacc[e] += (float)dz[e];
     } else {
       const bf16x8 dv = *(const bf16x8*)(Db + off);
 #pragma unroll
@@ -2069,7 +2049,6 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
 
   // partial slab: dW (row-major M x N) then db (M)
   float* part = a.part + (int64_t)split * a.split_stride + batch * ((int64_t)M * N + M);
-  const float* wlrow = TOPO > 0 ? a.top.WL + batch * a.top.wl_bstride : nullptr;
 #pragma unroll
   for (int bm = 0; bm < 2; ++bm)
 #pragma unroll
@@ -2078,15 +2057,13 @@ DEV void dw_ring_body(const TNArgs& a, char* smem, const int64_t r_begin, const 
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int row = 64 * wm + 32 * bm + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-        float v = acc[bm][bn][e];
-        if constexpr (TOPO > 0 && TOP_FACT) v *= wlrow[row] * a.w0;  // the factored-out W_L w0
-        part[(int64_t)row * N + col] = v;
+        part[(int64_t)row * N + col] = acc[bm][bn][e];
       }
     }
   __syncthreads();
   float* red = (float*)smem;  // [16 row slots][256]
 #pragma unroll
-  for (int e = 0; e < 8; ++e) red[rth * 256 + 8 * cth + e] = (TOPO > 0 && TOP_FACT) ? dbacc[e] * twl[0][e] : dbacc[e];
+  for (int e = 0; e < 8; ++e) red[rth * 256 + 8 * cth + e] = dbacc[e];
   __syncthreads();
   if (tid < 256) {
     float sum = 0.f;

@@ -404,3 +404,4 @@ def test_fused_dgrad_epilogues_match_the_passes(blocks, k):
         else:
             assert orc.norm_rel(g1[n].cpu(), g1b[n].cpu()) < 1e-6, n
             assert orc.norm_rel(g1[n].cpu(), g0[n].cpu()) < 1e-6, n
+
