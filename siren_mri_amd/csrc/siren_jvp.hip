@@ -1192,23 +1192,35 @@ __global__ __launch_bounds__(512) void jvp_adj_kernel(JAdjArgs a) {
 // Same products as jvp_nt_kernel (w0 * cos(p) * u, rounded to the operand type) and the same K
 // order, so the tangents are bit-identical to the stacked-row kernel's.
 struct JTanArgs {
-  const void* P;   // [B][N][K] phase_t of layer l - 1
-  const float* U;  // [B][Su][N][K] tangents of layer l - 1 (streams 0..C-1 used)
-  const void* W;   // [nb_w][Nout][K] op_t: W_l
-  float* Uout;     // [B][Su][N][Nout] tangents of layer l
+  const void* P;   // [B][N][K] phase_t of layer l - 1 (RB_DX: the phases of layer l - 1 are the
+                   // epilogue's [B][N][Nout])
+  const float* U;  // JT_TAN: [B][Su][N][K] tangents of layer l - 1 (streams 0..C-1 used);
+                   // JT_DX: [B][N][K] the incoming gradient dZ_l
+  const void* W;   // [nb_w][Nout][K] op_t: W_l (JT_DX: W_l^T)
+  const float* bias;  // JT_FWD: [nb_w][Nout] b_l
+  float* Uout;     // JT_TAN: [B][Su][N][Nout] tangents of layer l; JT_FWD: phases P_l [B][N][Nout];
+                   // JT_DX: dZ_{l-1} [B][N][Nout]
   int64_t N;
   int Su;
-  int64_t w_bstride;
+  int64_t w_bstride, b_bstride;
   int K, Nout;
   float w0;
 };
 
-template <int PREC, int C>
+// Modes of jvp_tan_kernel. JT_TAN: C tangent streams of the same 64 rows (above). The same tile
+// serves the fp32 stack's plain hidden layers with the C "streams" taken as C consecutive 64-row
+// blocks of one plane (nt_f32_kernel's products, K order and epilogues):
+//   JT_FWD: P_l = w0 (sin(P_{l-1}) W_l^T + b_l)                     (modules.py:25-26,38)
+//   JT_DX : dZ_{l-1} = (dZ_l W_l) cos(P_{l-1}) w0                    (the Sine's backward)
+constexpr int JT_TAN = 0, JT_FWD = 1, JT_DX = 2;
+
+template <int PREC, int C, int MODE = JT_TAN>
 __global__ __launch_bounds__(512) void jvp_tan_kernel(JTanArgs a) {
   using PT = Prec<PREC>;
   using phase_t = typename PT::phase_t;
   using op_t = typename PT::op_t;
   constexpr bool BF = PREC == kPrecBF16;
+  constexpr bool STREAMS = MODE == JT_TAN;  // C planes of the same rows, or C row blocks of one plane
   constexpr int ROW = JNTLds<PREC>::ROW;
   __shared__ __attribute__((aligned(16))) op_t As[C * JADJ_ROWS * ROW];
   __shared__ __attribute__((aligned(16))) op_t Bs[JADJ_BN * ROW];
@@ -1216,12 +1228,12 @@ __global__ __launch_bounds__(512) void jvp_tan_kernel(JTanArgs a) {
   const int wm = wave >> 2, wn = wave & 3;
   const int64_t b = blockIdx.y;
   const int64_t N = a.N;
-  const int64_t n0 = (int64_t)blockIdx.x * JADJ_ROWS;
+  const int64_t n0 = (int64_t)blockIdx.x * JADJ_ROWS * (STREAMS ? 1 : C);
   const int K = a.K;
   const int64_t plane = N * (int64_t)K;
   const op_t* W = (const op_t*)a.W + b * a.w_bstride;
   const phase_t* Pg = (const phase_t*)a.P + b * plane;
-  const float* Ug = a.U + b * (int64_t)a.Su * plane;
+  const float* Ug = a.U + b * (int64_t)(MODE == JT_TAN ? a.Su : 1) * plane;
 
   f32x16 acc[C][2];
 #pragma unroll
@@ -1231,38 +1243,40 @@ __global__ __launch_bounds__(512) void jvp_tan_kernel(JTanArgs a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[s][j][e] = 0.f;
 
-  // A chunk: 64 rows x 32 k in units of 4 -> one unit per thread (row tid >> 3, k 4 (tid & 7)),
-  // the same unit in every stream; B chunk: 256 x 32 -> 4 units per thread.
+  // A chunk: 64 rows x 32 k in units of 4 -> one unit per thread (row tid >> 3, k 4 (tid & 7)) in
+  // each of the C streams / row blocks; B chunk: 256 x 32 -> 4 units per thread.
   const int ar = tid >> 3, akq = (tid & 7) * 4;
-  const int64_t an = n0 + ar;
-  const bool arow = an < N;
-  phase_t praw[4];
+  auto arow = [&](int s) -> int64_t { return n0 + (STREAMS ? 0 : JADJ_ROWS * s) + ar; };
+  phase_t praw[STREAMS ? 1 : C][4];
   float uraw[C][4];
   float breg[4][4];
   auto load = [&](int k0) {
-    if (arow) {
+#pragma unroll
+    for (int s = 0; s < C; ++s) {
+      const int64_t an = arow(s);
+      const bool ok = an < N;
       const int64_t idx = an * K + k0 + akq;
-      if constexpr (BF) {
-        const u16x4 pv = *(const u16x4*)(Pg + idx);
+      if constexpr (MODE == JT_DX) {
+        const f32x4 v = ok ? *(const f32x4*)(Ug + idx) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) praw[e] = pv[e];
+        for (int e = 0; e < 4; ++e) uraw[s][e] = v[e];
       } else {
-        const f32x4 pv = *(const f32x4*)(Pg + idx);
+        if (MODE == JT_FWD || s == 0) {
+          if constexpr (BF) {
+            const u16x4 pv = ok ? *(const u16x4*)(Pg + idx) : u16x4{0, 0, 0, 0};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) praw[e] = pv[e];
-      }
+            for (int e = 0; e < 4; ++e) praw[STREAMS ? 0 : s][e] = pv[e];
+          } else {
+            const f32x4 pv = ok ? *(const f32x4*)(Pg + idx) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < C; ++s) {
-        const f32x4 uv = *(const f32x4*)(Ug + (int64_t)s * plane + idx);
+            for (int e = 0; e < 4; ++e) praw[STREAMS ? 0 : s][e] = pv[e];
+          }
+        }
+        if constexpr (MODE == JT_TAN) {
+          const f32x4 uv = ok ? *(const f32x4*)(Ug + (int64_t)s * plane + idx) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) uraw[s][e] = uv[e];
-      }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        praw[e] = 0;
-#pragma unroll
-        for (int s = 0; s < C; ++s) uraw[s][e] = 0.f;
+          for (int e = 0; e < 4; ++e) uraw[s][e] = uv[e];
+        }
       }
     }
 #pragma unroll
@@ -1286,11 +1300,20 @@ __global__ __launch_bounds__(512) void jvp_tan_kernel(JTanArgs a) {
     }
   };
   auto store = [&]() {
+    if constexpr (MODE == JT_TAN) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float wc = a.w0 * PT::cosp(praw[e]);  // one cosine for the C streams
+      for (int e = 0; e < 4; ++e) {
+        const float wc = a.w0 * PT::cosp(praw[0][e]);  // one cosine for the C streams
 #pragma unroll
-      for (int s = 0; s < C; ++s) As[(s * JADJ_ROWS + ar) * ROW + akq + e] = from_f32<op_t>(wc * uraw[s][e]);
+        for (int s = 0; s < C; ++s) As[(s * JADJ_ROWS + ar) * ROW + akq + e] = from_f32<op_t>(wc * uraw[s][e]);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < C; ++s)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          As[(s * JADJ_ROWS + ar) * ROW + akq + e] =
+              from_f32<op_t>(MODE == JT_FWD ? PT::sinp(praw[STREAMS ? 0 : s][e]) : uraw[s][e]);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1344,20 +1367,38 @@ __global__ __launch_bounds__(512) void jvp_tan_kernel(JTanArgs a) {
     }
   }
 
-  // U_l^k [n][f] = acc (pre-activation tangents: no bias); a lane's 16 elements of a tile are 16
-  // rows of one column, the 32 lanes of a half-wave 32 consecutive columns (128-byte rows)
+  // Epilogue. A lane's 16 elements of a tile are 16 rows of one column, the 32 lanes of a
+  // half-wave 32 consecutive columns (128-byte rows). JT_TAN: U_l^k = acc (pre-activation tangents:
+  // no bias); JT_FWD: P_l = w0 (acc + b); JT_DX: dZ_{l-1} = (acc cos(P_{l-1})) w0, the block's 16
+  // phases loaded before the first is used.
   const int64_t oplane = N * (int64_t)a.Nout;
-  float* Uo = a.Uout + b * (int64_t)a.Su * oplane;
+  float* Uo = a.Uout + b * (int64_t)(MODE == JT_TAN ? a.Su : 1) * oplane;
+  const phase_t* Po = (const phase_t*)a.P + b * oplane;  // JT_DX: P_{l-1} [N][Nout]
 #pragma unroll
   for (int bn = 0; bn < 2; ++bn) {
     const int f = 64 * wn + 32 * bn + r32;
     if (f >= a.Nout) continue;
+    float bcol = 0.f;
+    if constexpr (MODE == JT_FWD) bcol = a.bias[b * a.b_bstride + f];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int64_t n = n0 + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
-      if (n >= N) continue;
+    for (int s = 0; s < C; ++s) {
+      phase_t pv[16];
+      if constexpr (MODE == JT_DX) {
 #pragma unroll
-      for (int s = 0; s < C; ++s) Uo[(int64_t)s * oplane + n * a.Nout + f] = acc[s][bn][e];
+        for (int e = 0; e < 16; ++e) {
+          const int64_t n = arow(s) - ar + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+          pv[e] = Po[(n < N ? n : N - 1) * a.Nout + f];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int64_t n = arow(s) - ar + 32 * wm + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (n >= N) continue;
+        float v = acc[s][bn][e];
+        if constexpr (MODE == JT_FWD) v = PT::encz(v, bcol, a.w0);
+        if constexpr (MODE == JT_DX) v = (v * PT::cosp(pv[e])) * a.w0;
+        Uo[(STREAMS ? (int64_t)s * oplane : 0) + n * a.Nout + f] = v;
+      }
     }
   }
 }

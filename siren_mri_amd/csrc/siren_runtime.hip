@@ -102,6 +102,7 @@ bool g_dx_stagger = false;  // middle/top input-gradient ring: staggered wave ha
 bool g_tail_reduce = true;  // a pair launch reduces the previous pair launch's slabs (no reduce launch)
 bool g_jvp_adj = true;
 bool g_jvp_tan = true;      // tangent streams of a hidden layer stacked by row (jvp_tan_kernel)
+bool g_f32_rows = true;     // fp32 hidden layers' forward / input gradient on the row-stacked tile
 bool g_jvp_tn2 = true;      // fp32 analytic-derivative weight gradients on jvp_tn2_kernel      // analytic-derivative backward: adjoint GEMM + combine in one launch (jvp_adj_kernel)
 // pair_ring role split, input-gradient workgroups per 32 of the grid, per pair kind (middle, top,
 // bottom); 16 = the paired mapping (npair + npair, same tiles on one XCD)
@@ -194,6 +195,9 @@ int64_t pair_count(const Geo& g) {
   return std::min<int64_t>(np, align_up(ntiles, 8));
 }
 
+Split jtn2_split(const Geo& g, int64_t stacked_rows, int N);
+bool jvp_tn2_ok(int M, int N);
+
 struct Layout {
   // saved
   int64_t saved_off[SIREN_MAX_LAYERS];
@@ -276,6 +280,7 @@ Layout layout_of(const siren_mlp_desc* d) {
     part = std::max(part, s.nsplit * split_stride(g, (int64_t)M * N + M));
     part = std::max(part, dw_ring_split(g).nsplit * split_stride(g, (int64_t)M * N + M));
     part = std::max(part, pair_count(g) * split_stride(g, (int64_t)M * N + M));
+    part = std::max(part, jtn2_split(g, g.rows, N).nsplit * split_stride(g, (int64_t)M * N + M));
   }
   {
     const Split s = valu_split(g);
@@ -522,6 +527,33 @@ int launch_dx_ring_bot(const NTArgs& a, int64_t nb, int C, bool dxout, bool rec,
 template <int PREC, int MODE, bool TOP = false, bool BOT = false>
 int launch_nt(const NTArgs& a, int64_t nb, int kclass, hipStream_t st) {
   const int kmax = a.K <= 256 ? 256 : 512;
+  if constexpr (PREC == kPrecF32 && (MODE == MODE_FWD || MODE == MODE_DX) && !TOP && !BOT) {
+    // fp32 hidden layers on the row-stacked tile (jvp_tan_kernel JT_FWD / JT_DX: 128 rows x all
+    // 256 output features per workgroup, 8 waves; nt_f32_kernel's products, K order and epilogues)
+    if (g_f32_rows && a.K % JNT_KC == 0 && a.K <= 512 && a.N <= JADJ_BN && a.lda == a.K &&
+        (MODE == MODE_FWD || a.Paux)) {
+      JTanArgs t;
+      memset(&t, 0, sizeof(t));
+      t.P = MODE == MODE_FWD ? a.A : a.Paux;
+      t.U = MODE == MODE_DX ? (const float*)a.A : nullptr;
+      t.W = a.W;
+      t.bias = a.bias;
+      t.Uout = (float*)a.C;
+      t.N = a.rows_per_batch;
+      t.Su = 1;
+      t.w_bstride = a.w_bstride;
+      t.b_bstride = a.bias_bstride;
+      t.K = a.K;
+      t.Nout = a.N;
+      t.w0 = a.w0;
+      const dim3 grid((unsigned)cdiv(a.rows_per_batch, 2 * JADJ_ROWS), (unsigned)nb);
+      tmark_begin(kclass, st);
+      if constexpr (MODE == MODE_FWD) hipLaunchKernelGGL((jvp_tan_kernel<kPrecF32, 2, JT_FWD>), grid, dim3(512), 0, st, t);
+      else hipLaunchKernelGGL((jvp_tan_kernel<kPrecF32, 2, JT_DX>), grid, dim3(512), 0, st, t);
+      tmark_end(kclass, st);
+      return check_launch(MODE == MODE_FWD ? "f32 rows fwd" : "f32 rows dx");
+    }
+  }
   if constexpr (PREC == kPrecBF16 && MODE == MODE_DX && !TOP && !BOT) {
     if (g_dx_ring && a.K == 256 && a.N == 256) {
       tmark_begin(SIREN_KCLASS_DX_RING, st);
@@ -1040,6 +1072,7 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
     const bool ring = rec1 || ring_t || (PREC == kPrecBF16 && g_dw_ring && !is_top && M == 256 && N == 256);
     {
       const Split s = ring ? dw_ring_split(g) : tn_split(g, M, N);
+      int64_t nsplit_used = s.nsplit;
       TNArgs a;
       memset(&a, 0, sizeof(a));
       a.D = ws + lo.dz_off[cur];
@@ -1081,12 +1114,34 @@ int backward_impl(const siren_mlp_desc* d, const float* x, const float* dy, cons
           hipLaunchKernelGGL((dw_ring_bf16_kernel<0>), rg, dim3(512), 0, st, a);
         else if (is_top) hipLaunchKernelGGL((tn_dw_kernel<PREC, false, true>), grid, dim3(256), 0, st, a);
         else hipLaunchKernelGGL((tn_dw_kernel<PREC, false>), grid, dim3(256), 0, st, a);
+      } else if (g_f32_rows && jvp_tn2_ok(M, N)) {
+        // fp32: jvp_tn2_kernel over the primal stream alone (S = 1: X = sin(P_{l-1}), D = dZ_l):
+        // all 256 dW rows per workgroup, so each X element is formed once per launch
+        JTNArgs j;
+        memset(&j, 0, sizeof(j));
+        const Split s2 = jtn2_split(g, g.rows, N);
+        j.D = a.D;
+        j.P = a.P;
+        j.U = nullptr;
+        j.part = part;
+        j.N = g.rows;
+        j.rows_per_split = s2.rows_per_split;
+        j.split_stride = a.split_stride;
+        j.S = 1;
+        j.Su = 0;
+        j.C = 0;
+        j.M = M;
+        j.Kin = N;
+        j.w0 = d->w0;
+        nsplit_used = s2.nsplit;
+        hipLaunchKernelGGL((jvp_tn2_kernel<false>), dim3((unsigned)cdiv(N, JTN2_BN), (unsigned)s2.nsplit, (unsigned)g.nb),
+                           dim3(512), 0, st, j);
       } else {
         hipLaunchKernelGGL((tn_dw_kernel<PREC, false>), grid, dim3(256), 0, st, a);
       }
       tmark_end(kcls, st);
       if ((rc = check_launch("tn_dw"))) return rc;
-      if ((rc = launch_reduce(part, s.nsplit, a.split_stride, g.nb, (int64_t)M * N + M,
+      if ((rc = launch_reduce(part, nsplit_used, a.split_stride, g.nb, (int64_t)M * N + M,
                               (int64_t)M * N, dW[l], db[l], st)))
         return rc;
       if (is_top &&
@@ -3101,6 +3156,10 @@ int siren_config_set(const char* key, int64_t value) {
     g_jvp_adj = value != 0;
     return SIREN_OK;
   }
+  if (key && strcmp(key, "f32_rows") == 0 && (value == 0 || value == 1)) {
+    g_f32_rows = value != 0;
+    return SIREN_OK;
+  }
   if (key && strcmp(key, "jvp_tan") == 0 && (value == 0 || value == 1)) {
     g_jvp_tan = value != 0;
     return SIREN_OK;
@@ -3145,6 +3204,7 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "jvp_adj") == 0) return g_jvp_adj ? 1 : 0;
   if (key && strcmp(key, "jvp_tn2") == 0) return g_jvp_tn2 ? 1 : 0;
   if (key && strcmp(key, "jvp_tan") == 0) return g_jvp_tan ? 1 : 0;
+  if (key && strcmp(key, "f32_rows") == 0) return g_f32_rows ? 1 : 0;
   if (key && strcmp(key, "dx_stagger") == 0) return g_dx_stagger ? 1 : 0;
   if (key && strcmp(key, "pair_ring") == 0) return g_pair_ring ? 1 : 0;
   if (key && strcmp(key, "debug_keep_p0") == 0) return g_keep_p0 ? 1 : 0;

@@ -206,12 +206,60 @@ def test_metric_size_fp32_forward():
     assert orc.norm_rel(y.cpu(), y_ref) <= 1e-5
 
 
-def test_cpu_tensor_raises():
+def test_device_selects_the_path(monkeypatch):
+    """A CPU tensor takes the host path (cpu_stack.py, config 1 on a GPU-less host); a CUDA tensor
+    takes the native kernels and never reaches the host path (the GPU-side result is checked
+    against the oracle elsewhere; here the host path is made to raise while the CUDA call runs)."""
+    from siren_mri_amd import cpu_stack
     from siren_mri_amd.ops import siren_mlp
     dims = orc.siren_dims(2, 64, 1, 1)
     params = orc.siren_init(dims, seed=0)
-    with pytest.raises(RuntimeError, match="no CPU fallback"):
-        siren_mlp(torch.zeros(1, 4, 2), [W for W, _ in params], [b for _, b in params])
+    x = orc.get_mgrid(6)[None]
+    y_cpu = siren_mlp(x, [W for W, _ in params], [b for _, b in params])
+    assert y_cpu.device.type == "cpu"
+    assert orc.norm_rel(y_cpu, orc.siren_forward(x, params)) < 1e-6
+
+    def refuse(*a, **k):
+        raise AssertionError("a CUDA tensor reached the host path")
+    monkeypatch.setattr(cpu_stack, "sine_stack", refuse)
+    y = siren_mlp(x.to(DEV), [W.to(DEV) for W, _ in params], [b.to(DEV) for _, b in params], precision="fp32")
+    assert y.is_cuda and orc.norm_rel(y.cpu(), y_cpu) < 1e-5
+
+
+@pytest.mark.parametrize("hidden,nh,B", [(256, 3, 1), (128, 2, 2), (512, 1, 1), (64, 2, 3)])
+def test_fp32_row_stacked_layers_equal_nt_f32(hidden, nh, B):
+    """The fp32 hidden layers' forward and input gradient on the row-stacked tile (jvp_tan_kernel
+    JT_FWD / JT_DX, option f32_rows, default on) against nt_f32_kernel: the same products, K order
+    and epilogues, so y and dx are bit-identical; the 256-wide layers' weight gradients (jvp_tn2
+    over the primal stream, under the same option) split the row sum differently from tn_dw_kernel:
+    fp32 rounding level (1e-6). Ragged rows (37^2), shared and batched weights, hidden 64 .. 512."""
+    from siren_mri_amd import _native
+    from siren_mri_amd.ops import siren_mlp
+    dims = orc.siren_dims(2, hidden, nh, 1)
+    params = orc.siren_init(dims, seed=hidden + nh)
+    g = torch.Generator().manual_seed(9)
+    x = (torch.rand(B, 37 * 37, 2, generator=g) * 2 - 1).to(DEV)
+    lw = torch.randn(B, 37 * 37, 1, generator=g).to(DEV)
+    ws0 = [(W if B == 1 else torch.stack([W * (1 + 0.02 * i) for i in range(B)])).to(DEV) for W, _ in params]
+    bs0 = [(b if B == 1 else torch.stack([b * (1 + 0.02 * i) for i in range(B)])).to(DEV) for _, b in params]
+    res = []
+    assert _native.get_option("f32_rows") == 1
+    for rows in (1, 0):
+        _native.set_option("f32_rows", rows)
+        try:
+            ws = [w.clone().requires_grad_(True) for w in ws0]
+            bs = [b.clone().requires_grad_(True) for b in bs0]
+            xd = x.clone().requires_grad_(True)
+            y = siren_mlp(xd, ws, bs, precision="fp32")
+            (y * lw).sum().backward()
+            torch.cuda.synchronize()
+            res.append((y.detach(), xd.grad, [w.grad for w in ws], [b.grad for b in bs]))
+        finally:
+            _native.set_option("f32_rows", 1)
+    (y1, dx1, dw1, db1), (y0, dx0, dw0, db0) = res
+    assert torch.equal(y1, y0) and torch.equal(dx1, dx0)
+    for a_, b_ in zip(dw1 + db1, dw0 + db0):
+        assert orc.norm_rel(a_.cpu(), b_.cpu()) < 1e-6
 
 
 @pytest.mark.parametrize("nh", [1, 3])
