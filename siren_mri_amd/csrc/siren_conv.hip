@@ -55,10 +55,10 @@ __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cb = wave & 1, ib = wave >> 1;
   const int nrows = a.N * a.H;
-  const int64_t r0 = (int64_t)split * a.rows_per_split;
-  const int64_t r1 = r0 + a.rows_per_split < nrows ? r0 + a.rows_per_split : nrows;
+  const int r0 = split * (int)a.rows_per_split;
+  const int r1 = r0 + (int)a.rows_per_split < nrows ? r0 + (int)a.rows_per_split : nrows;
   const int nch = a.W / CW_PX;
-  const int64_t T = r1 > r0 ? (r1 - r0) * nch : 0;
+  const int T = r1 > r0 ? (r1 - r0) * nch : 0;
 
   f32x16 acc[CW_K];
 #pragma unroll
@@ -70,13 +70,23 @@ __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
   // pieces p = tid + 512 i (row p / 16, piece p % 16; zeros outside the image)
   // (two register sets, selected at compile time: the loop below is unrolled by two, since a
   // run-time set index became indexed register moves)
+  // chunks are loaded in order, so the loader keeps a cursor (image n, row h, first pixel px0)
+  // advanced one chunk per load: no per-chunk 64-bit division on the scalar unit (the divisions of
+  // the chunk index made SALU instructions outnumber VALU ones 1.7 : 1 in the PMC counters)
+  int cn = r0 / a.H, ch_row = r0 - (r0 / a.H) * a.H, cpx = 0;
   u32x4_t dv[2], xv[2][CW_NXL];
   const u32x4_t zero = {0u, 0u, 0u, 0u};
-  auto load = [&](int64_t t, auto set_c) {
+  auto load = [&](auto set_c) {
     constexpr int set = decltype(set_c)::value;
-    const int64_t r = r0 + t / nch;
-    const int px0 = (int)(t % nch) * CW_PX;
-    const int n = (int)(r / a.H), h = (int)(r % a.H);
+    const int n = cn, h = ch_row, px0 = cpx;
+    cpx += CW_PX;
+    if (cpx == a.W) {
+      cpx = 0;
+      if (++ch_row == a.H) {
+        ch_row = 0;
+        ++cn;
+      }
+    }
     const int xr = h + kh - CW_K / 2;
     const bool rowok = xr >= 0 && xr < a.H;
     dv[set] = *(const u32x4_t*)(a.dy + (((int64_t)n * a.H + h) * a.W + px0 + (tid >> 3)) * CW_C + 64 * ch +
@@ -115,20 +125,22 @@ __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
   if (T > 0) {
-    load(0, S0{});
+    load(S0{});
     stage(S0{}, 0);
   }
-  if (T > 1) load(1, S1{});
+  if (T > 1) load(S1{});
   __syncthreads();
+  int bcur = 0;  // t % CW_NB
   // iteration t: chunk t + 1 (register set (t + 1) & 1) to LDS, chunk t + 2's loads into set t & 1,
   // chunk t's MFMAs
-  auto iter = [&](int64_t t, auto par_c) {
+  auto iter = [&](int t, auto par_c) {
     constexpr int par = decltype(par_c)::value;  // t & 1
     using SN = std::integral_constant<int, par ^ 1>;
     using SC = std::integral_constant<int, par>;
-    if (t + 1 < T) stage(SN{}, (int)((t + 1) % CW_NB));
-    if (t + 2 < T) load(t + 2, SC{});
-    const int buf = (int)(t % CW_NB);
+    const int buf = bcur;
+    bcur = bcur == CW_NB - 1 ? 0 : bcur + 1;
+    if (t + 1 < T) stage(SN{}, bcur);
+    if (t + 2 < T) load(SC{});
     const uint32_t db = dbase + buf * DSTAGE, xb = xbase + buf * XSTAGE;
     // K step ks's 12 fragment reads are issued before step ks - 1's MFMAs (a wait for the older 12
     // then covers step ks - 1 exactly: lgkmcnt(12))
@@ -167,7 +179,7 @@ __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
 #undef SIREN_CW_RD
     __syncthreads();
   };
-  for (int64_t t = 0; t < T; t += 2) {
+  for (int t = 0; t < T; t += 2) {
     iter(t, S0{});
     if (t + 1 < T) iter(t + 1, S1{});
   }
@@ -224,10 +236,13 @@ constexpr int CF_W = 128;                    // image width (pixels per row), fi
 constexpr int CF_HALO = CF_W + CW_K - 1;     // 132
 constexpr int CF_CC = 32;                    // input channels per stage
 constexpr int CF_ROWB = 80;                  // bytes per LDS row (32 bf16 + 16 pad)
-constexpr int CF_XB = 2 * CF_HALO * CF_ROWB;         // x part of a stage (21,120 B)
+// LDS pixel rows per image row: the 132 halo pixels padded to 136 (17 blocks of 8; the 4 pad rows
+// are staged as zeros and never read) so that the staging writes can pair rows j and j + 4
+constexpr int CF_HALOP = 136;
+constexpr int CF_XB = 2 * CF_HALOP * CF_ROWB;        // x part of a stage (21,760 B)
 constexpr int CF_WB = CW_K * CW_C * CF_ROWB;          // filter part (51,200 B)
 constexpr int CF_STAGE = CF_XB + CF_WB;               // 72,320 B
-constexpr int CF_XP = 2 * CF_HALO * 4;                // 16-byte x pieces per stage (1056)
+constexpr int CF_XP = 2 * CF_HALOP * 4;               // 16-byte x pieces per stage (1088)
 constexpr int CF_WP = CW_K * CW_C * 4;                // filter pieces (2560)
 constexpr int CF_NL = (CF_XP + CF_WP + 511) / 512;    // loads per thread per stage (8)
 
@@ -261,6 +276,14 @@ struct ConvFArgs {
 //             block input
 constexpr int EPI_PLAIN = 0, EPI_RELU = 1, EPI_RES = 2, EPI_RESFWD = 3;
 
+// LDS row of staging piece w (blocks of 32 pieces = 8 rows x 4 16-byte pieces): lanes 8 m .. 8 m + 7
+// of a ds_write_b128 lane group take rows m and m + 4 of the block, 80 dwords apart (see the staging
+// comment in conv_fwd_k5_kernel)
+DEV int cf_row(int w) {
+  const int t = (w >> 2) & 7;
+  return 8 * (w >> 5) + (t >> 1) + 4 * (t & 1);
+}
+
 template <int EPI>
 __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
   __shared__ __attribute__((aligned(16))) char smem_cf[2 * CF_STAGE];
@@ -277,9 +300,13 @@ __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  // stage s = (kh = s / 4, cc = s % 4). Piece q < CF_XP: x row r = q / (4 * CF_HALO) of the pair,
-  // halo pixel j = (q / 4) % CF_HALO, 16-byte channel piece q % 4; else filter piece
-  // q' = q - CF_XP: tap kw = q' / 512, out channel (q' / 4) % 128, piece q' % 4.
+  // stage s = (kh = s / 4, cc = s % 4). Pieces in blocks of 32 (8 LDS rows x 4 16-byte channel
+  // pieces); within a block, lanes 8 m .. 8 m + 7 take rows m and m + 4 (cf_row), whose 80-byte rows
+  // lie 80 dwords apart: the two 64-byte pieces fill the 32 banks of a ds_write_b128 lane group
+  // exactly once (rows m and m + 1 shared 4 banks: every staging write paid a 2-way conflict).
+  // Piece q < CF_XP: x row r = q / (4 CF_HALOP) of the pair, halo pixel j (zeros past the 132
+  // real ones), channel piece pc; else filter piece q' = q - CF_XP: tap kw = q' / 512, out
+  // channel co, piece pc.
   u32x4_t lv[2][CF_NL];
   const u32x4_t zero = {0u, 0u, 0u, 0u};
   auto load = [&](int s, auto set_c) {
@@ -290,12 +317,12 @@ __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
       const int q = tid + 512 * i;
       u32x4_t v = zero;
       if (q < CF_XP) {
-        const int r = q / (4 * CF_HALO), j = (q >> 2) % CF_HALO, pc = q & 3;
+        const int r = q / (4 * CF_HALOP), j = cf_row(q - r * 4 * CF_HALOP), pc = q & 3;
         const int xr = h0 + r + kh - CW_K / 2, w = j - CW_K / 2;
         if (xr >= 0 && xr < a.H && w >= 0 && w < CF_W)
           v = *(const u32x4_t*)(a.x + (((int64_t)n * a.H + xr) * CF_W + w) * CW_C + CF_CC * cc + 8 * pc);
       } else if (q < CF_XP + CF_WP) {
-        const int q2 = q - CF_XP, kw = q2 >> 9, co = (q2 >> 2) & 127, pc = q2 & 3;
+        const int q2 = q - CF_XP, kw = q2 >> 9, co = cf_row(q2 & 511), pc = q2 & 3;
         v = *(const u32x4_t*)(a.w + ((int64_t)(co * CW_K + kh) * CW_K + kw) * CW_C + CF_CC * cc + 8 * pc);
       }
       lv[set][i] = v;
@@ -308,10 +335,10 @@ __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
     for (int i = 0; i < CF_NL; ++i) {
       const int q = tid + 512 * i;
       if (q < CF_XP) {
-        const int r = q / (4 * CF_HALO), j = (q >> 2) % CF_HALO, pc = q & 3;
-        *(u32x4_t*)(base + (r * CF_HALO + j) * CF_ROWB + 16 * pc) = lv[set][i];
+        const int r = q / (4 * CF_HALOP), j = cf_row(q - r * 4 * CF_HALOP), pc = q & 3;
+        *(u32x4_t*)(base + (r * CF_HALOP + j) * CF_ROWB + 16 * pc) = lv[set][i];
       } else if (q < CF_XP + CF_WP) {
-        const int q2 = q - CF_XP, kw = q2 >> 9, co = (q2 >> 2) & 127, pc = q2 & 3;
+        const int q2 = q - CF_XP, kw = q2 >> 9, co = cf_row(q2 & 511), pc = q2 & 3;
         *(u32x4_t*)(base + CF_XB + (kw * CW_C + co) * CF_ROWB + 16 * pc) = lv[set][i];
       }
     }
@@ -327,7 +354,7 @@ __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int px = 64 * wp + 32 * j + l32;
-    boff[j] = ((px >> 7) * CF_HALO + (px & 127)) * CF_ROWB + 16 * kh2;
+    boff[j] = ((px >> 7) * CF_HALOP + (px & 127)) * CF_ROWB + 16 * kh2;
   }
   const uint32_t sbase = lds_addr(smem_cf);
 
@@ -562,10 +589,11 @@ DEV void tie(bf16x8& v) { asm volatile("" : "+v"(v)); }
 template <int KS, int CI, int COT>
 __global__ __launch_bounds__(512) void conv_fwd_gen_kernel(ConvGArgs a) {
   constexpr int HALO = CF_W + KS - 1;
-  constexpr int XB = 2 * HALO * CF_ROWB;
+  constexpr int HALOP = (HALO + 7) / 8 * 8;  // LDS rows per image row, padded (conv_fwd_k5_kernel's cf_row)
+  constexpr int XB = 2 * HALOP * CF_ROWB;
   constexpr int WB = KS * COT * CF_ROWB;
   constexpr int STAGE = XB + WB;
-  constexpr int XP = 2 * HALO * 4, WP = KS * COT * 4;
+  constexpr int XP = 2 * HALOP * 4, WP = KS * COT * 4;
   constexpr int NL = (XP + WP + 511) / 512;
   constexpr int NCC = CI / CF_CC;
   constexpr int NS = KS * NCC;
@@ -605,12 +633,12 @@ __global__ __launch_bounds__(512) void conv_fwd_gen_kernel(ConvGArgs a) {
       const int q = tid + 512 * i;
       u32x4_t v = zero;
       if (q < XP) {
-        const int r = q / (4 * HALO), j = (q >> 2) % HALO, pc = q & 3;
+        const int r = q / (4 * HALOP), j = cf_row(q - r * 4 * HALOP), pc = q & 3;
         const int xr = h0 + r + kh - KS / 2, w = j - KS / 2;
-        if (xr >= 0 && xr < a.H && w >= 0 && w < CF_W)
+        if (xr >= 0 && xr < a.H && w >= 0 && w < CF_W && j < HALO)
           v = *(const u32x4_t*)(a.x + (((int64_t)n * a.H + xr) * CF_W + w) * CI + CF_CC * cc + 8 * pc);
       } else if (q < XP + WP) {
-        const int q2 = q - XP, kw = q2 / (4 * COT), co = (q2 >> 2) % COT, pc = q2 & 3;
+        const int q2 = q - XP, kw = q2 / (4 * COT), co = cf_row(q2 % (4 * COT)), pc = q2 & 3;
         v = *(const u32x4_t*)(a.w + ((int64_t)((co0 + co) * KS + kh) * KS + kw) * CI + CF_CC * cc + 8 * pc);
       }
       lv[set][i] = v;
@@ -623,10 +651,10 @@ __global__ __launch_bounds__(512) void conv_fwd_gen_kernel(ConvGArgs a) {
     for (int i = 0; i < NL; ++i) {
       const int q = tid + 512 * i;
       if (q < XP) {
-        const int r = q / (4 * HALO), j = (q >> 2) % HALO, pc = q & 3;
-        *(u32x4_t*)(base + (r * HALO + j) * CF_ROWB + 16 * pc) = lv[set][i];
+        const int r = q / (4 * HALOP), j = cf_row(q - r * 4 * HALOP), pc = q & 3;
+        *(u32x4_t*)(base + (r * HALOP + j) * CF_ROWB + 16 * pc) = lv[set][i];
       } else if (q < XP + WP) {
-        const int q2 = q - XP, kw = q2 / (4 * COT), co = (q2 >> 2) % COT, pc = q2 & 3;
+        const int q2 = q - XP, kw = q2 / (4 * COT), co = cf_row(q2 % (4 * COT)), pc = q2 & 3;
         *(u32x4_t*)(base + XB + (kw * COT + co) * CF_ROWB + 16 * pc) = lv[set][i];
       }
     }
@@ -641,7 +669,7 @@ __global__ __launch_bounds__(512) void conv_fwd_gen_kernel(ConvGArgs a) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int px = 64 * wp + 32 * j + l32;
-    boff[j] = ((px >> 7) * HALO + (px & 127)) * CF_ROWB + 16 * kh2;
+    boff[j] = ((px >> 7) * HALOP + (px & 127)) * CF_ROWB + 16 * kh2;
   }
   const uint32_t sbase = lds_addr(smem_g);
 
