@@ -241,7 +241,7 @@ constexpr int CF_ROWB = 80;                  // bytes per LDS row (32 bf16 + 16 
 constexpr int CF_HALOP = 136;
 constexpr int CF_XB = 2 * CF_HALOP * CF_ROWB;        // x part of a stage (21,760 B)
 constexpr int CF_WB = CW_K * CW_C * CF_ROWB;          // filter part (51,200 B)
-constexpr int CF_STAGE = CF_XB + CF_WB;               // 72,320 B
+constexpr int CF_STAGE = CF_XB + CF_WB;               // 72,960 B
 constexpr int CF_XP = 2 * CF_HALOP * 4;               // 16-byte x pieces per stage (1088)
 constexpr int CF_WP = CW_K * CW_C * 4;                // filter pieces (2560)
 constexpr int CF_NL = (CF_XP + CF_WP + 511) / 512;    // loads per thread per stage (8)
@@ -284,9 +284,23 @@ DEV int cf_row(int w) {
   return 8 * (w >> 5) + (t >> 1) + 4 * (t & 1);
 }
 
-template <int EPI>
+// DMA: the stage image is filled by LDS-DMA (buffer_load ... lds: 1 KB per wave-instruction, no
+// VGPR staging, no LDS write transfer from the register file) one stage ahead, instead of global
+// loads two stages ahead into registers and ds_write_b128 staging. The image is the same
+// (pad slots and pixels outside the image arrive as zeros through out-of-range buffer offsets);
+// each stage is padded to a multiple of 1 KB (CF_STAGE_DMA) so the last instruction's tail stays
+// inside it.
+// In that image the x part is padded to whole 1 KB instructions (no instruction spans both parts:
+// an LDS-DMA instruction writes every lane's 16 bytes).
+constexpr int CF_DMA_XN = (CF_XB + 1023) / 1024;                  // x-part instructions (22)
+constexpr int CF_XB_DMA = CF_DMA_XN * 1024;                       // 22,528 B
+constexpr int CF_DMA_N = CF_DMA_XN + (CF_WB + 1023) / 1024;       // per stage (72)
+constexpr int CF_STAGE_DMA = CF_DMA_N * 1024;                     // 73,728 B
+constexpr int CF_DMA_PER_WAVE = (CF_DMA_N + 7) / 8;               // 9
+template <int EPI, bool DMA = false>
 __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem_cf[2 * CF_STAGE];
+  constexpr int STG = DMA ? CF_STAGE_DMA : CF_STAGE;
+  __shared__ __attribute__((aligned(16))) char smem_cf[2 * STG];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wc = wave & 1, wp = wave >> 1;
   const int hp = a.H / 2;  // row pairs per image (H even)
@@ -350,7 +364,7 @@ __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
   const int l32 = lane & 31, kh2 = lane >> 5;
   uint32_t aoff[2], boff[2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) aoff[i] = CF_XB + (64 * wc + 32 * i + l32) * CF_ROWB + 16 * kh2;
+  for (int i = 0; i < 2; ++i) aoff[i] = (DMA ? CF_XB_DMA : CF_XB) + (64 * wc + 32 * i + l32) * CF_ROWB + 16 * kh2;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int px = 64 * wp + 32 * j + l32;
@@ -361,17 +375,56 @@ __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
   constexpr int NS = CW_K * 4;
-  load(0, S0{});
-  stage(S0{}, 0);
-  load(1, S1{});
+  // DMA: wave w issues instructions g = w + 8 i (slots 64 g .. 64 g + 63 of the stage image)
+  const __amdgpu_buffer_rsrc_t rX = make_rsrc(a.x + (int64_t)n * a.H * CF_W * CW_C, (int64_t)a.H * CF_W * CW_C * 2);
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.w, (int64_t)CW_C * CW_K * CW_K * CW_C * 2);
+  auto dma = [&](int s, int buf) {
+    const int kh = s >> 2, cc = s & 3;
+    char* base = smem_cf + buf * STG;
+#pragma unroll
+    for (int i = 0; i < CF_DMA_PER_WAVE; ++i) {
+      const int g = wave + 8 * i;  // (wave-uniform: the branches below are too)
+      if (g < CF_DMA_XN) {
+        // x part: slots 64 g + lane of rows (r, j) x 5 (4 channel pieces + the pad slot)
+        const int slot = 64 * g + lane;
+        const int row = slot / 5, pc = slot - row * 5;
+        const int r = row >= CF_HALOP ? 1 : 0, j = row - r * CF_HALOP;
+        const int xr = h0 + r + kh - CW_K / 2, w = j - CW_K / 2;
+        uint32_t off = 0x7fffffffu;  // out of range: zeros
+        if (row < 2 * CF_HALOP && pc < 4 && xr >= 0 && xr < a.H && w >= 0 && w < CF_W)
+          off = (uint32_t)(((xr * CF_W + w) * CW_C + CF_CC * cc + 8 * pc) * 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)(base + 1024 * g), 16, off, 0, 0, 0);
+      } else if (g < CF_DMA_N) {
+        // filter part: rows (kw, co) x 5
+        const int slot = 64 * (g - CF_DMA_XN) + lane;
+        const int row = slot / 5, pc = slot - row * 5;
+        const int kw = row >> 7, co = row & 127;
+        uint32_t off = 0x7fffffffu;
+        if (pc < 4 && kw < CW_K) off = (uint32_t)((((co * CW_K + kh) * CW_K + kw) * CW_C + CF_CC * cc + 8 * pc) * 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(base + 1024 * g), 16, off, 0, 0, 0);
+      }
+    }
+  };
+  if constexpr (DMA) {
+    dma(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    load(0, S0{});
+    stage(S0{}, 0);
+    load(1, S1{});
+  }
   __syncthreads();
   auto iter = [&](int s, auto par_c) {
     constexpr int par = decltype(par_c)::value;
     using SN = std::integral_constant<int, par ^ 1>;
     using SC = std::integral_constant<int, par>;
-    if (s + 1 < NS) stage(SN{}, (s + 1) & 1);
-    if (s + 2 < NS) load(s + 2, SC{});
-    const uint32_t sb = sbase + (s & 1) * CF_STAGE;
+    if constexpr (DMA) {
+      if (s + 1 < NS) dma(s + 1, (s + 1) & 1);
+    } else {
+      if (s + 1 < NS) stage(SN{}, (s + 1) & 1);
+      if (s + 2 < NS) load(s + 2, SC{});
+    }
+    const uint32_t sb = sbase + (s & 1) * STG;
     // 10 K steps (kw, ks); the fragments of step i + 1 are read while step i's MFMAs run
     bf16x8 af[2][2], bfr[2][2];
 #define SIREN_CF_RD(I)                                                                                            \
@@ -398,6 +451,7 @@ __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
           acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[b][ii], bfr[b][j], acc[ii][j], 0, 0, 0);
     });
 #undef SIREN_CF_RD
+    if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of stage s + 1
     __syncthreads();
   };
   for (int s = 0; s < NS; s += 2) {

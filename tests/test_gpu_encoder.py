@@ -405,3 +405,32 @@ def test_fused_dgrad_epilogues_match_the_passes(blocks, k):
             assert orc.norm_rel(g1[n].cpu(), g1b[n].cpu()) < 1e-6, n
             assert orc.norm_rel(g1[n].cpu(), g0[n].cpu()) < 1e-6, n
 
+
+
+def test_dma_staged_convolutions_equal_register_staged():
+    """The 5x5 convolutions with their stages filled by LDS-DMA (option conv_dma) against the
+    register-staged kernel: the same LDS image and K order, so the encoder node's embedding and
+    every gradient are bit-identical (the 1x1's MIOpen weight gradient aside, 1e-4)."""
+    from siren_mri_amd import _native
+    enc = _encoder("bf16", blocks=2, k=7, seed=8)
+    g = torch.Generator().manual_seed(9)
+    I = torch.randn(2, 2, 128, 128, generator=g).to(DEV)
+    ge = torch.randn(2, 128, generator=g).to(DEV)
+    res = []
+    prev = _native.get_option("conv_dma")
+    for dma in (1, 0):
+        _native.set_option("conv_dma", dma)
+        try:
+            res.append(_run(enc, I, ge))
+        finally:
+            _native.set_option("conv_dma", prev)
+    (e1, g1), (e0, g0) = res
+    assert torch.equal(e1, e0)
+    shapes = dict((n, p.shape) for n, p in enc.named_parameters())
+    for n in g1:
+        if len(shapes[n]) == 4 and shapes[n][-1] == 1:
+            assert orc.norm_rel(g1[n].cpu(), g0[n].cpu()) < 1e-4, n
+        elif n.startswith("fc") or len(shapes[n]) == 4:
+            assert torch.equal(g1[n], g0[n]), n
+        else:
+            assert orc.norm_rel(g1[n].cpu(), g0[n].cpu()) < 1e-6, n

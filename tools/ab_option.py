@@ -1,6 +1,6 @@
 """A/B a runtime option on one box: bench steps alternating option values, per-kernel-class times.
 
-    python tools/ab_option.py NAME V1,V2 [--rounds 3] [--steps 100]
+    python tools/ab_option.py NAME V1,V2 [--rounds 3] [--steps 100] [--config m|c1|..|c4]
 """
 import argparse
 import os
@@ -23,8 +23,9 @@ def main():
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--kclass", type=int, default=0, help="also time this kernel class (bench.KCLASS_NAMES)")
+    p.add_argument("--config", default="m", help="bench workload (bench.py --config)")
     cli = p.parse_args()
-    sys.argv = [sys.argv[0], "--no-psnr", "--no-cpu-baseline"]
+    sys.argv = [sys.argv[0], "--no-psnr", "--no-cpu-baseline", "--config", cli.config]
     args = bench.parse()
     _native.load_library()
     dev = torch.device("cuda", 0)
