@@ -1,6 +1,6 @@
 """Benchmark: SIREN fitting throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config m|c1|c2|c3|c4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config m|c1|c2|c3|c4|c4_fp32|m_fp32|m_shard8]
                     [--scaling weak|strong] [--precision bf16|fp32] [--no-graph]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
@@ -16,6 +16,11 @@ Workloads (BASELINE.json configs); the default is M, the m
       of 128^2 per GPU per step, conv encoder (bf16 channels-last) -> hypernetwork -> SIREN
       16-256-256-256-256-2 with per-slice weights (bf16) -> data consistency, image_hypernetwork_loss,
       clip_grad_norm_(1.0), Adam(5.57e-5).
+  c4_fp32  the same step in the reference's arithmetic: fp32 encoder (MIOpen, immediate mode) and
+      fp32 SIREN (tests/test_gpu_c4_precision.py checks the two at equal steps).
+  m_fp32   the metric fit in fp32 (exact-fp32 MFMA), the reference's arithmetic.
+  m_shard8 rank 0's 1/8 row shard of the metric grid without the exchange (the compute-only bound of
+      the 8-GPU strong-scaling speed-up).
 One step = forward + loss + backward (+ N>1: the gradient all-reduce over RCCL) + Adam.
 
 Scaling: weak (default; every rank owns its own full-size problem: a 512^2 block of a 512 x 512N

@@ -832,10 +832,10 @@ __global__ __launch_bounds__(512) void conv_wrw_gen_kernel(ConvGArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cb = wave % CB, ib = wave / CB;
   const int nrows = a.N * a.H;
-  const int64_t r0 = (int64_t)split * a.rows_per_split;
-  const int64_t r1 = r0 + a.rows_per_split < nrows ? r0 + a.rows_per_split : nrows;
+  const int r0 = split * (int)a.rows_per_split;
+  const int r1 = r0 + (int)a.rows_per_split < nrows ? r0 + (int)a.rows_per_split : nrows;
   const int nch = a.W / CW_PX;
-  const int64_t T = r1 > r0 ? (r1 - r0) * nch : 0;
+  const int T = r1 > r0 ? (r1 - r0) * nch : 0;
   const int CO = a.CO;
 
   f32x16 acc[KS];
@@ -844,13 +844,21 @@ __global__ __launch_bounds__(512) void conv_wrw_gen_kernel(ConvGArgs a) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[k][e] = 0.f;
 
+  // loader cursor over the chunks, loaded in order (conv_wrw_k5_kernel: no per-chunk division)
+  int cn = r0 / a.H, crow = r0 - (r0 / a.H) * a.H, cpx = 0;
   u32x4_t dv[2][NDL], xv[2][NXL];
   const u32x4_t zero = {0u, 0u, 0u, 0u};
-  auto load = [&](int64_t t, auto set_c) {
+  auto load = [&](auto set_c) {
     constexpr int set = decltype(set_c)::value;
-    const int64_t r = r0 + t / nch;
-    const int px0 = (int)(t % nch) * CW_PX;
-    const int n = (int)(r / a.H), h = (int)(r % a.H);
+    const int n = cn, h = crow, px0 = cpx;
+    cpx += CW_PX;
+    if (cpx == a.W) {
+      cpx = 0;
+      if (++crow == a.H) {
+        crow = 0;
+        ++cn;
+      }
+    }
     const int xr = h + kh - KS / 2;
     const bool rowok = xr >= 0 && xr < a.H;
 #pragma unroll
@@ -896,18 +904,20 @@ __global__ __launch_bounds__(512) void conv_wrw_gen_kernel(ConvGArgs a) {
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
   if (T > 0) {
-    load(0, S0{});
+    load(S0{});
     stage(S0{}, 0);
   }
-  if (T > 1) load(1, S1{});
+  if (T > 1) load(S1{});
+  int bcur = 0;  // t % CW_NB
   __syncthreads();
-  auto iter = [&](int64_t t, auto par_c) {
+  auto iter = [&](int t, auto par_c) {
     constexpr int par = decltype(par_c)::value;
     using SN = std::integral_constant<int, par ^ 1>;
     using SC = std::integral_constant<int, par>;
-    if (t + 1 < T) stage(SN{}, (int)((t + 1) % CW_NB));
-    if (t + 2 < T) load(t + 2, SC{});
-    const int buf = (int)(t % CW_NB);
+    const int buf = bcur;
+    bcur = bcur == CW_NB - 1 ? 0 : bcur + 1;
+    if (t + 1 < T) stage(SN{}, bcur);
+    if (t + 2 < T) load(SC{});
     const uint32_t db = dbase + buf * DSTAGE, xb = xbase + buf * XSTAGE;
     TrFrag fa[2], fb[2][KS];
 #define SIREN_CWG_RD(KS_)                                                         \
@@ -940,7 +950,7 @@ __global__ __launch_bounds__(512) void conv_wrw_gen_kernel(ConvGArgs a) {
 #undef SIREN_CWG_RD
     __syncthreads();
   };
-  for (int64_t t = 0; t < T; t += 2) {
+  for (int t = 0; t < T; t += 2) {
     iter(t, S0{});
     if (t + 1 < T) iter(t + 1, S1{});
   }
