@@ -284,7 +284,8 @@ DEV int cf_row(int w) {
   return 8 * (w >> 5) + (t >> 1) + 4 * (t & 1);
 }
 
-// DMA: the stage image is filled by LDS-DMA (buffer_load ... lds: 1 KB per wave-instruction, no
+// DMA (option conv_dma, default on: C4 17.24 -> 17.01 ms/step in a three-round one-box A/B,
+// profiles/r6_ab_conv_dma.txt; bit-identical, tests/test_gpu_encoder.py): the stage image is filled by LDS-DMA (buffer_load ... lds: 1 KB per wave-instruction, no
 // VGPR staging, no LDS write transfer from the register file) one stage ahead, instead of global
 // loads two stages ahead into registers and ds_write_b128 staging. The image is the same
 // (pad slots and pixels outside the image arrive as zeros through out-of-range buffer offsets);

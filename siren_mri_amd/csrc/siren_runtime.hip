@@ -103,7 +103,7 @@ bool g_tail_reduce = true;  // a pair launch reduces the previous pair launch's 
 bool g_jvp_adj = true;
 bool g_jvp_tan = true;      // tangent streams of a hidden layer stacked by row (jvp_tan_kernel)
 bool g_f32_rows = true;     // fp32 hidden layers' forward / input gradient on the row-stacked tile
-bool g_conv_dma = false;    // the 5x5 encoder convolutions' stages filled by LDS-DMA (conv_fwd_k5_kernel DMA)
+bool g_conv_dma = true;     // the 5x5 encoder convolutions' stages filled by LDS-DMA (conv_fwd_k5_kernel DMA)
 bool g_jvp_tn2 = true;      // fp32 analytic-derivative weight gradients on jvp_tn2_kernel      // analytic-derivative backward: adjoint GEMM + combine in one launch (jvp_adj_kernel)
 // pair_ring role split, input-gradient workgroups per 32 of the grid, per pair kind (middle, top,
 // bottom); 16 = the paired mapping (npair + npair, same tiles on one XCD)
