@@ -298,7 +298,13 @@ constexpr int CF_XB_DMA = CF_DMA_XN * 1024;                       // 22,528 B
 constexpr int CF_DMA_N = CF_DMA_XN + (CF_WB + 1023) / 1024;       // per stage (72)
 constexpr int CF_STAGE_DMA = CF_DMA_N * 1024;                     // 73,728 B
 constexpr int CF_DMA_PER_WAVE = (CF_DMA_N + 7) / 8;               // 9
-template <int EPI, bool DMA = false>
+// DMA 2 (option conv_dma 2): the same stage image, with each lane's source offsets computed once
+// per workgroup instead of once per stage. A stage (kh, cc) moves every offset by a wave-uniform
+// amount (x: kh image rows + cc channel pieces; filter: kh filter rows + cc), and an x piece's row
+// test is one compare of (h0 + r - 2 + kh) against H; the per-stage address arithmetic of form 1
+// (a division by 5, the halo row split, four range tests: ~150 VALU per wave and stage, issued
+// while no wave runs MFMAs) becomes one add and a compare-select per instruction.
+template <int EPI, int DMA = 0>
 __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
   constexpr int STG = DMA ? CF_STAGE_DMA : CF_STAGE;
   __shared__ __attribute__((aligned(16))) char smem_cf[2 * STG];
@@ -379,9 +385,48 @@ __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
   // DMA: wave w issues instructions g = w + 8 i (slots 64 g .. 64 g + 63 of the stage image)
   const __amdgpu_buffer_rsrc_t rX = make_rsrc(a.x + (int64_t)n * a.H * CF_W * CW_C, (int64_t)a.H * CF_W * CW_C * 2);
   const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.w, (int64_t)CW_C * CW_K * CW_K * CW_C * 2);
+  // DMA 2: per instruction i, the lane's stage-(0, 0) offset and (x part) its row test value
+  int pbase[CF_DMA_PER_WAVE], prow[CF_DMA_PER_WAVE];
+  if constexpr (DMA == 2) {
+#pragma unroll
+    for (int i = 0; i < CF_DMA_PER_WAVE; ++i) {
+      const int g = wave + 8 * i;
+      if (g < CF_DMA_XN) {
+        const int slot = 64 * g + lane;
+        const int row = slot / 5, pc = slot - row * 5;
+        const int r = row >= CF_HALOP ? 1 : 0, j = row - r * CF_HALOP;
+        const int w = j - CW_K / 2;
+        const bool ok = row < 2 * CF_HALOP && pc < 4 && w >= 0 && w < CF_W;
+        prow[i] = ok ? h0 + r - CW_K / 2 : -(1 << 20);  // x row = prow + kh; never in range when !ok
+        pbase[i] = ((h0 + r - CW_K / 2) * CF_W + w) * CW_C * 2 + 16 * pc;
+      } else {
+        const int slot = 64 * (g - CF_DMA_XN) + lane;
+        const int row = slot / 5, pc = slot - row * 5;
+        const int kw = row >> 7, co = row & 127;
+        prow[i] = 0;
+        pbase[i] = (g < CF_DMA_N && pc < 4 && kw < CW_K) ? (co * CW_K * CW_K * CW_C + kw * CW_C + 8 * pc) * 2
+                                                          : 0x7fff0000;  // + a stage's 5,312 B: still out of range
+      }
+    }
+  }
   auto dma = [&](int s, int buf) {
     const int kh = s >> 2, cc = s & 3;
     char* base = smem_cf + buf * STG;
+    if constexpr (DMA == 2) {
+      const int xadd = kh * CF_W * CW_C * 2 + CF_CC * cc * 2, wadd = kh * CW_K * CW_C * 2 + CF_CC * cc * 2;
+#pragma unroll
+      for (int i = 0; i < CF_DMA_PER_WAVE; ++i) {
+        const int g = wave + 8 * i;  // wave-uniform
+        if (g < CF_DMA_XN) {
+          const uint32_t off = (uint32_t)(prow[i] + kh) < (uint32_t)a.H ? (uint32_t)(pbase[i] + xadd) : 0x7fffffffu;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)(base + 1024 * g), 16, off, 0, 0, 0);
+        } else if (g < CF_DMA_N) {
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(base + 1024 * g), 16, (uint32_t)(pbase[i] + wadd),
+                                                   0, 0, 0);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < CF_DMA_PER_WAVE; ++i) {
       const int g = wave + 8 * i;  // (wave-uniform: the branches below are too)

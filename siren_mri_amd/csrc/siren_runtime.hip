@@ -103,7 +103,8 @@ bool g_tail_reduce = true;  // a pair launch reduces the previous pair launch's 
 bool g_jvp_adj = true;
 bool g_jvp_tan = true;      // tangent streams of a hidden layer stacked by row (jvp_tan_kernel)
 bool g_f32_rows = true;     // fp32 hidden layers' forward / input gradient on the row-stacked tile
-bool g_conv_dma = true;     // the 5x5 encoder convolutions' stages filled by LDS-DMA (conv_fwd_k5_kernel DMA)
+int g_conv_dma = 1;         // the 5x5 encoder convolutions' stages: 0 register staging, 1 LDS-DMA, 2 LDS-DMA with
+                            // per-workgroup source offsets (conv_fwd_k5_kernel DMA)
 bool g_jvp_tn2 = true;      // fp32 analytic-derivative weight gradients on jvp_tn2_kernel      // analytic-derivative backward: adjoint GEMM + combine in one launch (jvp_adj_kernel)
 // pair_ring role split, input-gradient workgroups per 32 of the grid, per pair kind (middle, top,
 // bottom); 16 = the paired mapping (npair + npair, same tiles on one XCD)
@@ -2227,6 +2228,14 @@ int loss_path_fail(const siren_mlp_desc* d) {
   return fail(SIREN_EINVAL, "fused loss: shape not supported (bf16 fused shapes: the register forward's "
                             "forms with 3+ layers and 1 output for 1..4 inputs; per-layer path: <= 8 outputs)");
 }
+
+// conv_fwd_k5_kernel in the stage-fill form of option conv_dma
+template <int EPI>
+void launch_conv_fwd_k5(dim3 grid, hipStream_t st, const ConvFArgs& a) {
+  if (g_conv_dma == 2) hipLaunchKernelGGL((conv_fwd_k5_kernel<EPI, 2>), grid, dim3(512), 0, st, a);
+  else if (g_conv_dma == 1) hipLaunchKernelGGL((conv_fwd_k5_kernel<EPI, 1>), grid, dim3(512), 0, st, a);
+  else hipLaunchKernelGGL((conv_fwd_k5_kernel<EPI, 0>), grid, dim3(512), 0, st, a);
+}
 }  // namespace
 extern "C" {
 
@@ -2512,8 +2521,7 @@ int siren_conv_fwd_k5(const void* x, const void* w, const void* bias, int relu, 
   a.N = N;
   a.H = H;
   a.relu = relu ? 1 : 0;
-  if (g_conv_dma) hipLaunchKernelGGL((conv_fwd_k5_kernel<EPI_PLAIN, true>), dim3((unsigned)(N * (H / 2))), dim3(512), 0, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL((conv_fwd_k5_kernel<EPI_PLAIN, false>), dim3((unsigned)(N * (H / 2))), dim3(512), 0, (hipStream_t)stream, a);
+  launch_conv_fwd_k5<EPI_PLAIN>(dim3((unsigned)(N * (H / 2))), (hipStream_t)stream, a);
   return check_launch("conv_fwd_k5");
 }
 
@@ -2533,8 +2541,7 @@ int siren_conv_fwd_k5_res(const void* x, const void* w, const void* cb, const vo
   a.g2 = (const bf16*)t;
   a.cb = (const bf16*)cb;
   a.y2 = (bf16*)out;
-  if (g_conv_dma) hipLaunchKernelGGL((conv_fwd_k5_kernel<EPI_RESFWD, true>), dim3((unsigned)(N * (H / 2))), dim3(512), 0, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL((conv_fwd_k5_kernel<EPI_RESFWD, false>), dim3((unsigned)(N * (H / 2))), dim3(512), 0, (hipStream_t)stream, a);
+  launch_conv_fwd_k5<EPI_RESFWD>(dim3((unsigned)(N * (H / 2))), (hipStream_t)stream, a);
   return check_launch("conv_fwd_k5_res");
 }
 
@@ -2566,11 +2573,9 @@ int siren_conv_dgrad_k5_fused(int mode, const void* dy, const void* wf, const vo
   a.part = (float*)ws;
   hipStream_t st = (hipStream_t)stream;
   if (mode == 1) {
-    if (g_conv_dma) hipLaunchKernelGGL((conv_fwd_k5_kernel<EPI_RELU, true>), dim3((unsigned)nblk), dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((conv_fwd_k5_kernel<EPI_RELU, false>), dim3((unsigned)nblk), dim3(512), 0, st, a);
+    launch_conv_fwd_k5<EPI_RELU>(dim3((unsigned)nblk), st, a);
   } else {
-    if (g_conv_dma) hipLaunchKernelGGL((conv_fwd_k5_kernel<EPI_RES, true>), dim3((unsigned)nblk), dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((conv_fwd_k5_kernel<EPI_RES, false>), dim3((unsigned)nblk), dim3(512), 0, st, a);
+    launch_conv_fwd_k5<EPI_RES>(dim3((unsigned)nblk), st, a);
   }
   int rc = check_launch("conv_dgrad_k5_fused");
   if (rc) return rc;
@@ -3164,8 +3169,8 @@ int siren_config_set(const char* key, int64_t value) {
     g_jvp_adj = value != 0;
     return SIREN_OK;
   }
-  if (key && strcmp(key, "conv_dma") == 0 && (value == 0 || value == 1)) {
-    g_conv_dma = value != 0;
+  if (key && strcmp(key, "conv_dma") == 0 && value >= 0 && value <= 2) {
+    g_conv_dma = (int)value;
     return SIREN_OK;
   }
   if (key && strcmp(key, "f32_rows") == 0 && (value == 0 || value == 1)) {
@@ -3217,7 +3222,7 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "jvp_tn2") == 0) return g_jvp_tn2 ? 1 : 0;
   if (key && strcmp(key, "jvp_tan") == 0) return g_jvp_tan ? 1 : 0;
   if (key && strcmp(key, "f32_rows") == 0) return g_f32_rows ? 1 : 0;
-  if (key && strcmp(key, "conv_dma") == 0) return g_conv_dma ? 1 : 0;
+  if (key && strcmp(key, "conv_dma") == 0) return g_conv_dma;
   if (key && strcmp(key, "dx_stagger") == 0) return g_dx_stagger ? 1 : 0;
   if (key && strcmp(key, "pair_ring") == 0) return g_pair_ring ? 1 : 0;
   if (key && strcmp(key, "debug_keep_p0") == 0) return g_keep_p0 ? 1 : 0;
