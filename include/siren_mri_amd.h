@@ -496,6 +496,16 @@ int siren_sincos_f32(const float* x, float* s, float* c, int64_t n, int impl, vo
  *                    0: the 128x128-tile kernel.
  *   "debug_pair_roles"  3 (default); 1 / 2 run only the input- / weight-gradient role of
  *                    pair_ring_bf16_kernel (timing experiments only: the gradients are then wrong).
+ *   "jvp_tan"        1 (default): fp32 tangent streams of the 256-wide hidden layers on the
+ *                    row-stacked tile (jvp_tan_kernel); 0: the stream-stacked GEMMs.
+ *   "f32_rows"       1 (default): fp32 hidden layers' forward and input gradient on the
+ *                    row-stacked tile, per-layer weight gradients on the all-rows tile; 0: the
+ *                    128x128-tile kernels.
+ *   "conv_dma"       2 (default): the 5x5 encoder convolutions' stages filled by LDS-DMA with
+ *                    per-workgroup source offsets; 1: LDS-DMA with per-stage offsets; 0: register
+ *                    staging (all three bit-identical).
+ *   "wrw_dma"        0 (default), 1: the 5x5 weight-gradient convolution's chunks filled by
+ *                    LDS-DMA instead of register staging (bit-identical).
  *   "debug_fused_profile"  device address of an int64 buffer [grid][4] that receives per-
  *                    workgroup cycle counts of the fused forward's phases, or 0 (off).
  * Returns SIREN_OK, or SIREN_EINVAL for an unknown key / value. Not thread-safe.

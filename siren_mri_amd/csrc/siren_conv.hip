@@ -48,9 +48,22 @@ struct ConvWArgs {
 // Pipeline: chunk t + 2's global loads go to register set t % 2 while chunk t's MFMAs run; at the
 // top of iteration t + 1 that set is written to LDS stage (t + 2) % 3 (last read in iteration
 // t - 1, before the barrier that closed it); one barrier per chunk.
+// DMA (option wrw_dma): the same LDS image filled by LDS-DMA (buffer_load ... lds, 1 KB per
+// wave-instruction) straight into stage (t + 2) % 3 at the top of iteration t, no register sets and
+// no staging writes. A chunk is 12 dY instructions (64 rows x 12 slots: 8 channel pieces + 4 pad)
+// and 22 X instructions (68 halo rows x 20 slots: 16 + 4 pad; the X stage padded to 22 KB); a lane's
+// source offsets are fixed per workgroup: the chunk moves the buffer bases (scalar), and halo pixels
+// left or right of the image, pad slots and X rows outside the image (a zero-size buffer) are out of
+// range, so they arrive as zeros.
+constexpr int CW_DMA_D = CW_PX * 12 / 64;                   // dY instructions per chunk (12)
+constexpr int CW_DMA_X = (CW_XROWS * 20 + 63) / 64;        // X instructions per chunk (22)
+constexpr int CW_DMA_N = CW_DMA_D + CW_DMA_X;                // 34
+constexpr int CW_DMA_PER_WAVE = (CW_DMA_N + 7) / 8;          // 5 (waves 0, 1), 4 (waves 2..7)
+constexpr int CW_XSTAGE_DMA = CW_DMA_X * 1024;               // 22,528 B
+template <bool DMA>
 __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 sD[CW_NB][CW_PX * CW_DROW];
-  __shared__ __attribute__((aligned(16))) bf16 sX[CW_NB][CW_XROWS * CW_XROW];
+  __shared__ __attribute__((aligned(16))) bf16 sX[CW_NB][DMA ? CW_XSTAGE_DMA / 2 : CW_XROWS * CW_XROW];
   const int split = blockIdx.x, kh = blockIdx.y, ch = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cb = wave & 1, ib = wave >> 1;
@@ -119,28 +132,88 @@ __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
   const int r8 = 8 * (g >> 1) + tq;                  // row of K step 0
   const uint32_t dbase = lds_addr(&sD[0][0]) + (uint32_t)((r8 * CW_DROW + ca) * 2);
   const uint32_t xbase = lds_addr(&sX[0][0]) + (uint32_t)((r8 * CW_XROW + cx) * 2);
-  constexpr uint32_t DSTAGE = CW_PX * CW_DROW * 2, XSTAGE = CW_XROWS * CW_XROW * 2;
+  constexpr uint32_t DSTAGE = CW_PX * CW_DROW * 2, XSTAGE = DMA ? CW_XSTAGE_DMA : CW_XROWS * CW_XROW * 2;
   constexpr int DROWB = CW_DROW * 2, XROWB = CW_XROW * 2;
 
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
-  if (T > 0) {
-    load(S0{});
-    stage(S0{}, 0);
+  // DMA: lane source offsets of this wave's instructions g = wave + 8 i (dY: row * 256 + piece;
+  // X: (halo row - 2) * 256 + piece, plus 256 px0 per chunk; out of range for the pad slots)
+  int voff[CW_DMA_PER_WAVE];
+  if constexpr (DMA) {
+#pragma unroll
+    for (int i = 0; i < CW_DMA_PER_WAVE; ++i) {
+      const int g = wave + 8 * i;
+      if (g < CW_DMA_D) {
+        const int slot = 64 * g + lane, row = slot / 12, pc = slot - 12 * (slot / 12);
+        voff[i] = pc < 8 ? row * CW_C * 2 + 16 * pc : 0x7fffffff;
+      } else {
+        const int slot = 64 * (g - CW_DMA_D) + lane, row = slot / 20, pc = slot - 20 * (slot / 20);
+        voff[i] = (pc < 16 && row < CW_XROWS) ? (row - CW_K / 2) * CW_C * 2 + 16 * pc : 0x40000000;
+      }
+    }
   }
-  if (T > 1) load(S1{});
-  __syncthreads();
+  // DMA of the chunk at the cursor into stage buf, then the cursor advances one chunk
+  auto dma = [&](int buf) {
+    const int n = cn, h = ch_row, px0 = cpx;
+    cpx += CW_PX;
+    if (cpx == a.W) {
+      cpx = 0;
+      if (++ch_row == a.H) {
+        ch_row = 0;
+        ++cn;
+      }
+    }
+    const int xr = h + kh - CW_K / 2;
+    const bool rowok = xr >= 0 && xr < a.H;
+    const __amdgpu_buffer_rsrc_t rD =
+        make_rsrc(a.dy + (((int64_t)n * a.H + h) * a.W + px0) * CW_C + 64 * ch, (CW_PX * CW_C - 64) * 2);
+    const __amdgpu_buffer_rsrc_t rX =
+        make_rsrc(a.x + ((int64_t)n * a.H + (rowok ? xr : 0)) * a.W * CW_C, rowok ? (int64_t)a.W * CW_C * 2 : 0);
+#pragma unroll
+    for (int i = 0; i < CW_DMA_PER_WAVE; ++i) {
+      const int g = wave + 8 * i;  // wave-uniform
+      if (g < CW_DMA_D)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rD, (lds_void*)((char*)&sD[buf][0] + 1024 * g), 16, (uint32_t)voff[i],
+                                                 0, 0, 0);
+      else if (g < CW_DMA_N)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)((char*)&sX[buf][0] + 1024 * (g - CW_DMA_D)), 16,
+                                                 (uint32_t)(voff[i] + px0 * CW_C * 2), 0, 0, 0);
+    }
+  };
+  if constexpr (DMA) {
+    if (T > 0) dma(0);
+    if (T > 1) {
+      dma(1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // chunk 0 (the younger chunk 1 is 4 or 5)
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  } else {
+    if (T > 0) {
+      load(S0{});
+      stage(S0{}, 0);
+    }
+    if (T > 1) load(S1{});
+    __syncthreads();
+  }
   int bcur = 0;  // t % CW_NB
   // iteration t: chunk t + 1 (register set (t + 1) & 1) to LDS, chunk t + 2's loads into set t & 1,
-  // chunk t's MFMAs
+  // chunk t's MFMAs (DMA: chunk t + 2 into stage (t + 2) % 3, chunk t's MFMAs, wait for chunk t + 1)
   auto iter = [&](int t, auto par_c) {
     constexpr int par = decltype(par_c)::value;  // t & 1
     using SN = std::integral_constant<int, par ^ 1>;
     using SC = std::integral_constant<int, par>;
     const int buf = bcur;
     bcur = bcur == CW_NB - 1 ? 0 : bcur + 1;
-    if (t + 1 < T) stage(SN{}, bcur);
-    if (t + 2 < T) load(SC{});
+    if constexpr (DMA) {
+      if (t + 2 < T) dma(bcur == CW_NB - 1 ? 0 : bcur + 1);
+    } else {
+      if (t + 1 < T) stage(SN{}, bcur);
+      if (t + 2 < T) load(SC{});
+    }
     const uint32_t db = dbase + buf * DSTAGE, xb = xbase + buf * XSTAGE;
     // K step ks's 12 fragment reads are issued before step ks - 1's MFMAs (a wait for the older 12
     // then covers step ks - 1 exactly: lgkmcnt(12))
@@ -177,7 +250,17 @@ __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
       });
     });
 #undef SIREN_CW_RD
-    __syncthreads();
+    if constexpr (DMA) {
+      // this wave's part of chunk t + 1 landed (chunk t + 2's 4 or 5 are younger); a barrier without
+      // __syncthreads' fence, which would drain chunk t + 2's DMA too (vmcnt(0))
+      if (t + 2 < T) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      __syncthreads();
+    }
   };
   for (int t = 0; t < T; t += 2) {
     iter(t, S0{});
@@ -303,7 +386,8 @@ constexpr int CF_DMA_PER_WAVE = (CF_DMA_N + 7) / 8;               // 9
 // amount (x: kh image rows + cc channel pieces; filter: kh filter rows + cc), and an x piece's row
 // test is one compare of (h0 + r - 2 + kh) against H; the per-stage address arithmetic of form 1
 // (a division by 5, the halo row split, four range tests: ~150 VALU per wave and stage, issued
-// while no wave runs MFMAs) becomes one add and a compare-select per instruction.
+// while no wave runs MFMAs) becomes one add and a compare-select per instruction. Default: C4
+// 17.02 -> 16.67 ms/step over six interleaved one-box pairs (profiles/r6_ab_conv_dma2.txt), bit-identical.
 template <int EPI, int DMA = 0>
 __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
   constexpr int STG = DMA ? CF_STAGE_DMA : CF_STAGE;

@@ -103,8 +103,10 @@ bool g_tail_reduce = true;  // a pair launch reduces the previous pair launch's 
 bool g_jvp_adj = true;
 bool g_jvp_tan = true;      // tangent streams of a hidden layer stacked by row (jvp_tan_kernel)
 bool g_f32_rows = true;     // fp32 hidden layers' forward / input gradient on the row-stacked tile
-int g_conv_dma = 1;         // the 5x5 encoder convolutions' stages: 0 register staging, 1 LDS-DMA, 2 LDS-DMA with
-                            // per-workgroup source offsets (conv_fwd_k5_kernel DMA)
+bool g_wrw_dma = false;     // the 5x5 weight-gradient convolution's chunks filled by LDS-DMA (conv_wrw_k5_kernel DMA)
+int g_conv_dma = 2;         // the 5x5 encoder convolutions' stages: 0 register staging, 1 LDS-DMA, 2 LDS-DMA with
+                            // per-workgroup source offsets (conv_fwd_k5_kernel DMA; 2 is C4 -2 %,
+                            // profiles/r6_ab_conv_dma2.txt)
 bool g_jvp_tn2 = true;      // fp32 analytic-derivative weight gradients on jvp_tn2_kernel      // analytic-derivative backward: adjoint GEMM + combine in one launch (jvp_adj_kernel)
 // pair_ring role split, input-gradient workgroups per 32 of the grid, per pair kind (middle, top,
 // bottom); 16 = the paired mapping (npair + npair, same tiles on one XCD)
@@ -2499,7 +2501,8 @@ int siren_conv_wrw_k5(const void* x, const void* dy, int N, int H, int W, int C,
   a.nsplit = nsplit;
   a.rows_per_split = cdiv(rows, nsplit);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(conv_wrw_k5_kernel, dim3((unsigned)nsplit, CW_K, 2), dim3(512), 0, st, a);
+  if (g_wrw_dma) hipLaunchKernelGGL(conv_wrw_k5_kernel<true>, dim3((unsigned)nsplit, CW_K, 2), dim3(512), 0, st, a);
+  else hipLaunchKernelGGL(conv_wrw_k5_kernel<false>, dim3((unsigned)nsplit, CW_K, 2), dim3(512), 0, st, a);
   int rc = check_launch("conv_wrw_k5");
   if (rc) return rc;
   hipLaunchKernelGGL(conv_wrw_reduce_kernel, dim3((unsigned)cdiv(CW_SLAB, 256)), dim3(256), 0, st, a);
@@ -3169,6 +3172,10 @@ int siren_config_set(const char* key, int64_t value) {
     g_jvp_adj = value != 0;
     return SIREN_OK;
   }
+  if (key && strcmp(key, "wrw_dma") == 0 && (value == 0 || value == 1)) {
+    g_wrw_dma = value != 0;
+    return SIREN_OK;
+  }
   if (key && strcmp(key, "conv_dma") == 0 && value >= 0 && value <= 2) {
     g_conv_dma = (int)value;
     return SIREN_OK;
@@ -3223,6 +3230,7 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "jvp_tan") == 0) return g_jvp_tan ? 1 : 0;
   if (key && strcmp(key, "f32_rows") == 0) return g_f32_rows ? 1 : 0;
   if (key && strcmp(key, "conv_dma") == 0) return g_conv_dma;
+  if (key && strcmp(key, "wrw_dma") == 0) return g_wrw_dma ? 1 : 0;
   if (key && strcmp(key, "dx_stagger") == 0) return g_dx_stagger ? 1 : 0;
   if (key && strcmp(key, "pair_ring") == 0) return g_pair_ring ? 1 : 0;
   if (key && strcmp(key, "debug_keep_p0") == 0) return g_keep_p0 ? 1 : 0;

@@ -210,21 +210,41 @@ def test_conv_weight_gradient_kernel_against_fp32(N, H, W):
     ref = torch.nn.grad.conv2d_weight(x.double(), (128, 128, 5, 5), dy.double(), padding=2).float()
     xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
     dyd = dy.to(DEV).contiguous(memory_format=torch.channels_last)
-    dw = torch.empty(128, 128, 5, 5, device=DEV).contiguous(memory_format=torch.channels_last)
     ws = torch.empty(int(lib.siren_conv_wrw_workspace_bytes(N, H, W)), dtype=torch.uint8, device=DEV)
-    _native.check(lib.siren_conv_wrw_k5(xd.data_ptr(), dyd.data_ptr(), N, H, W, 128, dw.data_ptr(), ws.data_ptr(),
-                                        ws.numel(), _native.stream_handle(DEV)), "conv_wrw")
-    assert orc.norm_rel(dw.cpu(), ref) < 1e-6
-    dw2 = torch.empty_like(dw)
-    _native.check(lib.siren_conv_wrw_k5(xd.data_ptr(), dyd.data_ptr(), N, H, W, 128, dw2.data_ptr(), ws.data_ptr(),
-                                        ws.numel(), _native.stream_handle(DEV)), "conv_wrw")
-    assert torch.equal(dw, dw2)
+    prev = _native.get_option("wrw_dma")
+    outs = {}
+    try:
+        for dma in (0, 1, 1):  # register staging; LDS-DMA (option wrw_dma) twice: run-to-run equality
+            _native.set_option("wrw_dma", dma)
+            dw = torch.empty(128, 128, 5, 5, device=DEV).contiguous(memory_format=torch.channels_last)
+            _native.check(lib.siren_conv_wrw_k5(xd.data_ptr(), dyd.data_ptr(), N, H, W, 128, dw.data_ptr(),
+                                                ws.data_ptr(), ws.numel(), _native.stream_handle(DEV)), "conv_wrw")
+            outs.setdefault(dma, []).append(dw)
+    finally:
+        _native.set_option("wrw_dma", prev)
+    assert orc.norm_rel(outs[0][0].cpu(), ref) < 1e-6
+    # the LDS-DMA form stages the same image: bit-identical, and deterministic
+    assert torch.equal(outs[1][0], outs[0][0])
+    assert torch.equal(outs[1][0], outs[1][1])
 
 
+@pytest.mark.parametrize("dma", [0, 1, 2])
 @pytest.mark.parametrize("bias,relu", [(False, False), (True, False), (True, True)])
-def test_conv_forward_kernel_against_fp32(bias, relu):
+def test_conv_forward_kernel_against_fp32(bias, relu, dma):
     """siren_conv_fwd_k5 (128 -> 128, 5x5, W = 128) against the fp32 convolution of the same bf16
-    operands (then the conv + bias-add chain's bf16 roundings), and bit-equal on a rerun."""
+    operands (then the conv + bias-add chain's bf16 roundings), and bit-equal on a rerun; in each
+    stage-fill form (option conv_dma: registers, LDS-DMA, LDS-DMA with per-workgroup offsets) on a
+    6-row image, where most stages hold rows outside the image."""
+    from siren_mri_amd import _native
+    prev = _native.get_option("conv_dma")
+    _native.set_option("conv_dma", dma)
+    try:
+        _conv_forward_case(bias, relu)
+    finally:
+        _native.set_option("conv_dma", prev)
+
+
+def _conv_forward_case(bias, relu):
     from siren_mri_amd import _native
     import torch.nn.functional as F
     lib = _native.lib()
@@ -408,29 +428,33 @@ def test_fused_dgrad_epilogues_match_the_passes(blocks, k):
 
 
 def test_dma_staged_convolutions_equal_register_staged():
-    """The 5x5 convolutions with their stages filled by LDS-DMA (option conv_dma) against the
-    register-staged kernel: the same LDS image and K order, so the encoder node's embedding and
+    """The 5x5 convolutions with their stages filled by LDS-DMA (options conv_dma, wrw_dma) against
+    the register-staged kernels: the same LDS image and K order, so the encoder node's embedding and
     every gradient are bit-identical (the 1x1's MIOpen weight gradient aside, 1e-4)."""
     from siren_mri_amd import _native
     enc = _encoder("bf16", blocks=2, k=7, seed=8)
     g = torch.Generator().manual_seed(9)
     I = torch.randn(2, 2, 128, 128, generator=g).to(DEV)
     ge = torch.randn(2, 128, generator=g).to(DEV)
-    res = []
-    prev = _native.get_option("conv_dma")
-    for dma in (1, 0):
+    res = {}
+    prev, prev_w = _native.get_option("conv_dma"), _native.get_option("wrw_dma")
+    for dma in (0, 1, 2):  # 2: the DMA source offsets computed once per workgroup
         _native.set_option("conv_dma", dma)
+        _native.set_option("wrw_dma", 1 if dma else 0)  # the weight gradient's LDS-DMA form beside them
         try:
-            res.append(_run(enc, I, ge))
+            res[dma] = _run(enc, I, ge)
         finally:
             _native.set_option("conv_dma", prev)
-    (e1, g1), (e0, g0) = res
-    assert torch.equal(e1, e0)
+            _native.set_option("wrw_dma", prev_w)
+    e0, g0 = res[0]
     shapes = dict((n, p.shape) for n, p in enc.named_parameters())
-    for n in g1:
-        if len(shapes[n]) == 4 and shapes[n][-1] == 1:
-            assert orc.norm_rel(g1[n].cpu(), g0[n].cpu()) < 1e-4, n
-        elif n.startswith("fc") or len(shapes[n]) == 4:
-            assert torch.equal(g1[n], g0[n]), n
-        else:
-            assert orc.norm_rel(g1[n].cpu(), g0[n].cpu()) < 1e-6, n
+    for dma in (1, 2):
+        e1, g1 = res[dma]
+        assert torch.equal(e1, e0), dma
+        for n in g1:
+            if len(shapes[n]) == 4 and shapes[n][-1] == 1:
+                assert orc.norm_rel(g1[n].cpu(), g0[n].cpu()) < 1e-4, (dma, n)
+            elif n.startswith("fc") or len(shapes[n]) == 4:
+                assert torch.equal(g1[n], g0[n]), (dma, n)
+            else:
+                assert orc.norm_rel(g1[n].cpu(), g0[n].cpu()) < 1e-6, (dma, n)
