@@ -504,8 +504,8 @@ int siren_sincos_f32(const float* x, float* s, float* c, int64_t n, int impl, vo
  *   "conv_dma"       2 (default): the 5x5 encoder convolutions' stages filled by LDS-DMA with
  *                    per-workgroup source offsets; 1: LDS-DMA with per-stage offsets; 0: register
  *                    staging (all three bit-identical).
- *   "wrw_dma"        0 (default), 1: the 5x5 weight-gradient convolution's chunks filled by
- *                    LDS-DMA instead of register staging (bit-identical).
+ *   "wrw_dma"        1 (default): the 5x5 weight-gradient convolution's chunks filled by
+ *                    LDS-DMA; 0: register staging (bit-identical).
  *   "debug_fused_profile"  device address of an int64 buffer [grid][4] that receives per-
  *                    workgroup cycle counts of the fused forward's phases, or 0 (off).
  * Returns SIREN_OK, or SIREN_EINVAL for an unknown key / value. Not thread-safe.

@@ -32,6 +32,7 @@ constexpr int ENC_MAXC = 256;
 // the ticket
 constexpr int64_t ENC_WS_FLOATS = (int64_t)ENC_MAX_BLOCKS * ENC_MAXC;
 constexpr int ENC_U = 4;  // pixels per thread per iteration in the gradient passes
+constexpr int ENC_UB = 8;  // images per thread per iteration in enc_pixfc_bwd_kernel
 
 struct EncArgs {
   const bf16* g1;     // incoming gradient (or a / x operands, see each kernel)
@@ -102,12 +103,20 @@ DEV void enc_block_sum(const EncArgs& a, const float (&acc)[8], int c0, int pix,
   if (tid == 0) last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
   __syncthreads();
   if (!last) return;
-  // The rows are read eight loads at a time before any is added (a chain of single sc1 loads made
-  // this tail 0.2-0.5 ms), in a fixed order: deterministic.
+  // The rows are read 32 loads at a time before any is added (a chain of single sc1 loads made
+  // this tail 0.2-0.5 ms; 8 at a time still left 64 load latencies in a row for 1,024 blocks), in a
+  // fixed order: deterministic.
   auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   auto sum_rows = [&](const float* src, unsigned b0, unsigned b1, int64_t stride) {
     float s = 0.f;
     unsigned b = b0;
+    for (; b + 32 <= b1; b += 32) {
+      float v[32];
+#pragma unroll
+      for (int k = 0; k < 32; ++k) v[k] = ld(src + (int64_t)(b + k) * stride);
+#pragma unroll
+      for (int k = 0; k < 32; ++k) s += v[k];
+    }
     for (; b + 8 <= b1; b += 8) {
       float v[8];
 #pragma unroll
@@ -289,13 +298,26 @@ __global__ __launch_bounds__(256) void enc_pixfc_fwd_kernel(EncArgs a) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] = 0.f;
   load_bias8(a.cb, c0, bb);
-  for (int64_t p = p0 + pix; p < p1; p += ppi) {
-    float v[8];
-    load_bf16x8(src + p * a.C + c0, v);
-    add_bias8(v, bb, a.cb != nullptr);
-    const float wp = a.w[p];
+  // ENC_U pixels' loads in flight before the first is used (one at a time ran at ~1.9 TB/s); the
+  // sums keep the pixel order
+  for (int64_t p = p0 + pix; p < p1; p += ENC_U * ppi) {
+    float v[ENC_U][8], wp[ENC_U];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = fmaf(fmaxf(v[e], 0.f), wp, acc[e]);
+    for (int u = 0; u < ENC_U; ++u) {
+      const int64_t q = p + u * ppi;
+      if (q < p1) {
+        load_bf16x8(src + q * a.C + c0, v[u]);
+        wp[u] = a.w[q];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < ENC_U; ++u) {
+      if (p + u * ppi < p1) {
+        add_bias8(v[u], bb, a.cb != nullptr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = fmaf(fmaxf(v[u][e], 0.f), wp[u], acc[e]);
+      }
+    }
   }
   enc_block_sum(a, acc, c0, pix, ppi, a.B * a.C, a.e, a.bias);
 }
@@ -314,22 +336,37 @@ __global__ __launch_bounds__(256) void enc_pixfc_bwd_kernel(EncArgs a) {
   for (int64_t p = p0 + pix; p < p1; p += ppi) {
     const float wp = a.w[p];
     float gw = 0.f;
-    for (int b = 0; b < a.B; ++b) {
-      const int64_t off = ((int64_t)b * a.P + p) * a.C + c0;
-      float v[8];
-      load_bf16x8(a.a + off, v);
-      add_bias8(v, bb, a.cb != nullptr);
-      const f32x4 g0 = *(const f32x4*)(a.gin + (int64_t)b * a.C + c0);
-      const f32x4 g1 = *(const f32x4*)(a.gin + (int64_t)b * a.C + c0 + 4);
-      bf16x8 o;
+    // ENC_UB images' loads issued before the first store (a store to out may alias the next load
+    // for the compiler: one image at a time left every load's latency exposed, ~1.2 TB/s); the
+    // sums keep the image order
+    for (int b0 = 0; b0 < a.B; b0 += ENC_UB) {
+      float v[ENC_UB][8];
+      f32x4 g0[ENC_UB], g1[ENC_UB];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float g = e < 4 ? g0[e] : g1[e - 4];
-        o[e] = (bf16)(v[e] > 0.f ? g * wp : 0.f);
-        acc[e] += (float)o[e];
-        gw = fmaf(g, fmaxf(v[e], 0.f), gw);
+      for (int u = 0; u < ENC_UB; ++u) {
+        const int b = b0 + u;
+        if (b < a.B) {
+          load_bf16x8(a.a + ((int64_t)b * a.P + p) * a.C + c0, v[u]);
+          g0[u] = *(const f32x4*)(a.gin + (int64_t)b * a.C + c0);
+          g1[u] = *(const f32x4*)(a.gin + (int64_t)b * a.C + c0 + 4);
+        }
       }
-      *(bf16x8*)(a.out + off) = o;
+#pragma unroll
+      for (int u = 0; u < ENC_UB; ++u) {
+        const int b = b0 + u;
+        if (b < a.B) {
+          add_bias8(v[u], bb, a.cb != nullptr);
+          bf16x8 o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float g = e < 4 ? g0[u][e] : g1[u][e - 4];
+            o[e] = (bf16)(v[u][e] > 0.f ? g * wp : 0.f);
+            acc[e] += (float)o[e];
+            gw = fmaf(g, fmaxf(v[u][e], 0.f), gw);
+          }
+          *(bf16x8*)(a.out + ((int64_t)b * a.P + p) * a.C + c0) = o;
+        }
+      }
     }
     // the pixel's tpp lanes (consecutive) add their channel groups
     for (int off = tpp / 2; off >= 1; off >>= 1) gw += __shfl_xor(gw, off, tpp);
