@@ -501,9 +501,10 @@ int siren_sincos_f32(const float* x, float* s, float* c, int64_t n, int impl, vo
  *   "f32_rows"       1 (default): fp32 hidden layers' forward and input gradient on the
  *                    row-stacked tile, per-layer weight gradients on the all-rows tile; 0: the
  *                    128x128-tile kernels.
- *   "conv_dma"       2 (default): the 5x5 encoder convolutions' stages filled by LDS-DMA with
- *                    per-workgroup source offsets; 1: LDS-DMA with per-stage offsets; 0: register
- *                    staging (all three bit-identical).
+ *   "conv_dma"       2 (default): the encoder's forward / input-gradient convolutions (5x5 and
+ *                    the other shapes) fill their stages by LDS-DMA with per-workgroup source
+ *                    offsets; 1: LDS-DMA with per-stage offsets for the 5x5 ones, register staging
+ *                    for the others; 0: register staging (all forms bit-identical).
  *   "wrw_dma"        1 (default): the 5x5 weight-gradient convolution's chunks filled by
  *                    LDS-DMA; 0: register staging (bit-identical).
  *   "debug_fused_profile"  device address of an int64 buffer [grid][4] that receives per-

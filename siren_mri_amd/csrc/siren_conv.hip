@@ -770,13 +770,19 @@ DEV void lgkm_wait() {
 DEV void tie(TrFrag& f) { asm volatile("" : "+v"(f.lo), "+v"(f.hi)); }
 DEV void tie(bf16x8& v) { asm volatile("" : "+v"(v)); }
 
-template <int KS, int CI, int COT>
+// DMA (option conv_dma 2, as conv_fwd_k5_kernel's form 2): the stage image filled by LDS-DMA
+// one stage ahead, each lane's source offsets computed once per workgroup; the x part padded to
+// whole 1 KB instructions (the filter part is KS x COT rows of 80 bytes: a multiple of 1 KB).
+template <int KS, int CI, int COT, bool DMA = false>
 __global__ __launch_bounds__(512) void conv_fwd_gen_kernel(ConvGArgs a) {
   constexpr int HALO = CF_W + KS - 1;
   constexpr int HALOP = (HALO + 7) / 8 * 8;  // LDS rows per image row, padded (conv_fwd_k5_kernel's cf_row)
-  constexpr int XB = 2 * HALOP * CF_ROWB;
+  constexpr int XB0 = 2 * HALOP * CF_ROWB;
+  constexpr int XB = DMA ? (XB0 + 1023) / 1024 * 1024 : XB0;
   constexpr int WB = KS * COT * CF_ROWB;
+  static_assert(!DMA || WB % 1024 == 0, "filter part in whole DMA instructions");
   constexpr int STAGE = XB + WB;
+  constexpr int DXN = XB / 1024, DN = DXN + WB / 1024, DPW = (DN + 7) / 8;  // DMA instructions
   constexpr int XP = 2 * HALOP * 4, WP = KS * COT * 4;
   constexpr int NL = (XP + WP + 511) / 512;
   constexpr int NCC = CI / CF_CC;
@@ -859,16 +865,64 @@ __global__ __launch_bounds__(512) void conv_fwd_gen_kernel(ConvGArgs a) {
 
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
-  load(0, S0{});
-  stage(S0{}, 0);
-  if (NS > 1) load(1, S1{});
+  // DMA: instruction g = wave + 8 i fills slots 64 g .. 64 g + 63 of the stage (rows of 5 slots: 4
+  // channel pieces + the pad); per lane the stage-(0, 0) source offset and (x part) the row test
+  int pbase[DPW], prow[DPW];
+  const __amdgpu_buffer_rsrc_t rX = make_rsrc(a.x + (int64_t)n * a.H * CF_W * CI, (int64_t)a.H * CF_W * CI * 2);
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.w, (int64_t)CO * KS * KS * CI * 2);
+  if constexpr (DMA) {
+#pragma unroll
+    for (int i = 0; i < DPW; ++i) {
+      const int g = wave + 8 * i;
+      if (g < DXN) {
+        const int slot = 64 * g + lane, row = slot / 5, pc = slot - 5 * (slot / 5);
+        const int r = row >= HALOP ? 1 : 0, j = row - r * HALOP, w = j - KS / 2;
+        const bool ok = row < 2 * HALOP && pc < 4 && j < HALO && w >= 0 && w < CF_W;
+        prow[i] = ok ? h0 + r - KS / 2 : -(1 << 20);
+        pbase[i] = ((h0 + r - KS / 2) * CF_W + w) * CI * 2 + 16 * pc;
+      } else {
+        const int slot = 64 * (g - DXN) + lane, row = slot / 5, pc = slot - 5 * (slot / 5);
+        const int kw = row / COT, co = row - COT * (row / COT);
+        prow[i] = 0;
+        pbase[i] = (g < DN && pc < 4 && kw < KS) ? ((co0 + co) * KS * KS * CI + kw * CI + 8 * pc) * 2 : 0x7fff0000;
+      }
+    }
+  }
+  auto dma = [&](int s, int buf) {
+    const int kh = s / NCC, cc = s % NCC;
+    char* base = smem_g + buf * STAGE;
+    const int xadd = kh * CF_W * CI * 2 + CF_CC * cc * 2, wadd = kh * KS * CI * 2 + CF_CC * cc * 2;
+#pragma unroll
+    for (int i = 0; i < DPW; ++i) {
+      const int g = wave + 8 * i;  // wave-uniform
+      if (g < DXN) {
+        const uint32_t off = (uint32_t)(prow[i] + kh) < (uint32_t)a.H ? (uint32_t)(pbase[i] + xadd) : 0x7fffffffu;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)(base + 1024 * g), 16, off, 0, 0, 0);
+      } else if (g < DN) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(base + 1024 * g), 16, (uint32_t)(pbase[i] + wadd), 0,
+                                                 0, 0);
+      }
+    }
+  };
+  if constexpr (DMA) {
+    dma(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    load(0, S0{});
+    stage(S0{}, 0);
+    if (NS > 1) load(1, S1{});
+  }
   __syncthreads();
   auto iter = [&](int s, auto par_c) {
     constexpr int par = decltype(par_c)::value;
     using SN = std::integral_constant<int, par ^ 1>;
     using SC = std::integral_constant<int, par>;
-    if (s + 1 < NS) stage(SN{}, (s + 1) & 1);
-    if (s + 2 < NS) load(s + 2, SC{});
+    if constexpr (DMA) {
+      if (s + 1 < NS) dma(s + 1, (s + 1) & 1);
+    } else {
+      if (s + 1 < NS) stage(SN{}, (s + 1) & 1);
+      if (s + 2 < NS) load(s + 2, SC{});
+    }
     const uint32_t sb = sbase + (s & 1) * STAGE;
     // 2 KS K steps (kw, ks); step i + 1's fragments are read while step i's MFMAs run
     bf16x8 af[2][NI], bfr[2][2];
@@ -902,6 +956,7 @@ __global__ __launch_bounds__(512) void conv_fwd_gen_kernel(ConvGArgs a) {
           acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[b][ii], bfr[b][j], acc[ii][j], 0, 0, 0);
     });
 #undef SIREN_CG_RD
+    if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of stage s + 1
     __syncthreads();
   };
   for (int s = 0; s < NS; s += 2) {

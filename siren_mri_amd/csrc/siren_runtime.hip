@@ -2674,7 +2674,11 @@ int siren_conv_fwd(const void* x, const void* w, const void* bias, int relu, voi
   }
   const bool big = KS <= 5 && CO % 128 == 0;  // 128-channel tiles (the 7x7 stages need 64 to fit in LDS)
   const dim3 grid((unsigned)(N * (H / 2)), (unsigned)(CO / (big ? 128 : 64)));
-#define SIREN_CF(K, C, T) hipLaunchKernelGGL((conv_fwd_gen_kernel<K, C, T>), grid, dim3(512), 0, st, a)
+#define SIREN_CF(K, C, T)                                                                           \
+  do {                                                                                              \
+    if (g_conv_dma == 2) hipLaunchKernelGGL((conv_fwd_gen_kernel<K, C, T, true>), grid, dim3(512), 0, st, a); \
+    else hipLaunchKernelGGL((conv_fwd_gen_kernel<K, C, T, false>), grid, dim3(512), 0, st, a);      \
+  } while (0)
   if (KS == 3) {
     if (CI == 64) { if (big) SIREN_CF(3, 64, 128); else SIREN_CF(3, 64, 64); }
     else { if (big) SIREN_CF(3, 128, 128); else SIREN_CF(3, 128, 64); }
@@ -2920,7 +2924,9 @@ int siren_enc_res_bwd(const void* g1, const void* g2, const void* out, const voi
 int siren_enc_pixfc_fwd(const void* a_pre, const void* cb, const float* w, const float* bias, float* e, int B,
                         int64_t P, int C, void* ws, int64_t ws_bytes, void* stream) {
   EncArgs a;
-  int rc = enc_setup(a, P, C, ws, ws_bytes, true, 1024, "enc_pixfc_fwd");
+  // chunks of >= 512 pixels, at most ENC_MAX_BLOCKS blocks over the B images (32 x 32 at C4's 128^2)
+  const int64_t min_rows = std::max<int64_t>(512, cdiv(std::max<int64_t>(P, 1), std::max<int64_t>(1, ENC_MAX_BLOCKS / std::max(B, 1))));
+  int rc = enc_setup(a, P, C, ws, ws_bytes, true, min_rows, "enc_pixfc_fwd");
   if (rc) return rc;
   if (!a_pre || !w || !bias || !e || B < 1) return fail(SIREN_EINVAL, "enc_pixfc_fwd: null pointer or B < 1");
   const int64_t nchunk = cdiv(P, a.chunk);
@@ -2940,7 +2946,7 @@ int siren_enc_pixfc_fwd(const void* a_pre, const void* cb, const float* w, const
 int siren_enc_pixfc_bwd(const float* g, const void* a_pre, const void* cb, const float* w, void* ga, float* db,
                         float* gw, int B, int64_t P, int C, void* ws, int64_t ws_bytes, void* stream) {
   EncArgs a;
-  int rc = enc_setup(a, P, C, ws, ws_bytes, true, 128, "enc_pixfc_bwd");
+  int rc = enc_setup(a, P, C, ws, ws_bytes, true, 32, "enc_pixfc_bwd");  // 512 blocks at 128^2 (128: 177 us, C4)
   if (rc) return rc;
   if (!g || !a_pre || !w || !ga || !db || !gw || B < 1) return fail(SIREN_EINVAL, "enc_pixfc_bwd: null pointer or B < 1");
   if (P == 0) return fail(SIREN_EINVAL, "enc_pixfc_bwd: no pixels");

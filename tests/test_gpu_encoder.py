@@ -281,7 +281,8 @@ def test_generic_conv_forward_kernel_against_fp32(k, ci, co, bias, relu):
     """siren_conv_fwd (round 5: the encoder's other shapes — cnn[0]'s 64 -> 128 7x7, its input
     gradient 128 -> 64, the 3x3 forms; conv_theta's 2 input channels, with a ragged last
     workgroup of image rows) against the fp64 convolution of the same bf16 operands (then the
-    conv + bias-add chain's bf16 roundings), bit-equal on a rerun."""
+    conv + bias-add chain's bf16 roundings), bit-equal on a rerun and between the stage fills
+    (option conv_dma)."""
     from siren_mri_amd import _native
     import torch.nn.functional as F
     lib = _native.lib()
@@ -300,12 +301,18 @@ def test_generic_conv_forward_kernel_against_fp32(k, ci, co, bias, relu):
     wd = w.to(DEV).contiguous(memory_format=torch.channels_last)
     bd = b.to(DEV)
     outs = []
-    for _ in range(2):
-        y = torch.empty(N, co, H, 128, dtype=torch.bfloat16, device=DEV).contiguous(memory_format=torch.channels_last)
-        _native.check(lib.siren_conv_fwd(xd.data_ptr(), wd.data_ptr(), bd.data_ptr() if bias else None, int(relu),
-                                         y.data_ptr(), N, H, 128, ci, co, k, _native.stream_handle(DEV)), "conv_fwd")
-        outs.append(y)
+    prev = _native.get_option("conv_dma")
+    try:
+        for dma in (2, 2, 0):  # the LDS-DMA stage fill twice (run-to-run), then register staging
+            _native.set_option("conv_dma", dma)
+            y = torch.empty(N, co, H, 128, dtype=torch.bfloat16, device=DEV).contiguous(memory_format=torch.channels_last)
+            _native.check(lib.siren_conv_fwd(xd.data_ptr(), wd.data_ptr(), bd.data_ptr() if bias else None, int(relu),
+                                             y.data_ptr(), N, H, 128, ci, co, k, _native.stream_handle(DEV)), "conv_fwd")
+            outs.append(y)
+    finally:
+        _native.set_option("conv_dma", prev)
     assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[2])  # the same stage image either way
     d = (outs[0].float().cpu() - ref.float())
     assert orc.norm_rel(outs[0].float().cpu(), ref.float()) < 4e-3
     assert (d.abs() <= ref.float().abs() * 2 ** -7 + 1e-6).float().mean() > 0.999
