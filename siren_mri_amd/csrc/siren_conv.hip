@@ -55,22 +55,28 @@ struct ConvWArgs {
 // source offsets are fixed per workgroup: the chunk moves the buffer bases (scalar), and halo pixels
 // left or right of the image, pad slots and X rows outside the image (a zero-size buffer) are out of
 // range, so they arrive as zeros.
-constexpr int CW_DMA_D = CW_PX * 12 / 64;                   // dY instructions per chunk (12)
-constexpr int CW_DMA_X = (CW_XROWS * 20 + 63) / 64;        // X instructions per chunk (22)
-constexpr int CW_DMA_N = CW_DMA_D + CW_DMA_X;                // 34
-constexpr int CW_DMA_PER_WAVE = (CW_DMA_N + 7) / 8;          // 5 (waves 0, 1), 4 (waves 2..7)
-constexpr int CW_XSTAGE_DMA = CW_DMA_X * 1024;               // 22,528 B
-template <bool DMA>
+// PX = 128 (option wrw_dma 2, DMA only, W a multiple of 128): 128-pixel chunks in two LDS stages
+// (135 KB), the chunk after next's DMA one chunk ahead; twice the MFMAs per barrier, DMA issue and
+// fragment-read ramp-up of a 64-pixel chunk.
+template <bool DMA, int PX = CW_PX>
 __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16 sD[CW_NB][CW_PX * CW_DROW];
-  __shared__ __attribute__((aligned(16))) bf16 sX[CW_NB][DMA ? CW_XSTAGE_DMA / 2 : CW_XROWS * CW_XROW];
+  static_assert(PX == CW_PX || (DMA && PX == 2 * CW_PX), "64-pixel chunks, or 128 with the DMA fill");
+  constexpr int NB = PX == CW_PX ? CW_NB : 2;                // LDS stages
+  constexpr int XROWS = PX + CW_K - 1;                       // halo rows
+  constexpr int DMA_D = PX * 12 / 64;                        // dY instructions per chunk (12 / 24)
+  constexpr int DMA_X = (XROWS * 20 + 63) / 64;              // X instructions per chunk (22 / 42)
+  constexpr int DMA_N = DMA_D + DMA_X;
+  constexpr int DMA_PER_WAVE = (DMA_N + 7) / 8;
+  constexpr int XSTAGE_DMA = DMA_X * 1024;
+  __shared__ __attribute__((aligned(16))) bf16 sD[NB][PX * CW_DROW];
+  __shared__ __attribute__((aligned(16))) bf16 sX[NB][DMA ? XSTAGE_DMA / 2 : CW_XROWS * CW_XROW];
   const int split = blockIdx.x, kh = blockIdx.y, ch = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cb = wave & 1, ib = wave >> 1;
   const int nrows = a.N * a.H;
   const int r0 = split * (int)a.rows_per_split;
   const int r1 = r0 + (int)a.rows_per_split < nrows ? r0 + (int)a.rows_per_split : nrows;
-  const int nch = a.W / CW_PX;
+  const int nch = a.W / PX;
   const int T = r1 > r0 ? (r1 - r0) * nch : 0;
 
   f32x16 acc[CW_K];
@@ -132,31 +138,31 @@ __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
   const int r8 = 8 * (g >> 1) + tq;                  // row of K step 0
   const uint32_t dbase = lds_addr(&sD[0][0]) + (uint32_t)((r8 * CW_DROW + ca) * 2);
   const uint32_t xbase = lds_addr(&sX[0][0]) + (uint32_t)((r8 * CW_XROW + cx) * 2);
-  constexpr uint32_t DSTAGE = CW_PX * CW_DROW * 2, XSTAGE = DMA ? CW_XSTAGE_DMA : CW_XROWS * CW_XROW * 2;
+  constexpr uint32_t DSTAGE = PX * CW_DROW * 2, XSTAGE = DMA ? XSTAGE_DMA : CW_XROWS * CW_XROW * 2;
   constexpr int DROWB = CW_DROW * 2, XROWB = CW_XROW * 2;
 
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
   // DMA: lane source offsets of this wave's instructions g = wave + 8 i (dY: row * 256 + piece;
   // X: (halo row - 2) * 256 + piece, plus 256 px0 per chunk; out of range for the pad slots)
-  int voff[CW_DMA_PER_WAVE];
+  int voff[DMA_PER_WAVE];
   if constexpr (DMA) {
 #pragma unroll
-    for (int i = 0; i < CW_DMA_PER_WAVE; ++i) {
+    for (int i = 0; i < DMA_PER_WAVE; ++i) {
       const int g = wave + 8 * i;
-      if (g < CW_DMA_D) {
+      if (g < DMA_D) {
         const int slot = 64 * g + lane, row = slot / 12, pc = slot - 12 * (slot / 12);
         voff[i] = pc < 8 ? row * CW_C * 2 + 16 * pc : 0x7fffffff;
       } else {
-        const int slot = 64 * (g - CW_DMA_D) + lane, row = slot / 20, pc = slot - 20 * (slot / 20);
-        voff[i] = (pc < 16 && row < CW_XROWS) ? (row - CW_K / 2) * CW_C * 2 + 16 * pc : 0x40000000;
+        const int slot = 64 * (g - DMA_D) + lane, row = slot / 20, pc = slot - 20 * (slot / 20);
+        voff[i] = (pc < 16 && row < XROWS) ? (row - CW_K / 2) * CW_C * 2 + 16 * pc : 0x40000000;
       }
     }
   }
   // DMA of the chunk at the cursor into stage buf, then the cursor advances one chunk
   auto dma = [&](int buf) {
     const int n = cn, h = ch_row, px0 = cpx;
-    cpx += CW_PX;
+    cpx += PX;
     if (cpx == a.W) {
       cpx = 0;
       if (++ch_row == a.H) {
@@ -167,21 +173,26 @@ __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
     const int xr = h + kh - CW_K / 2;
     const bool rowok = xr >= 0 && xr < a.H;
     const __amdgpu_buffer_rsrc_t rD =
-        make_rsrc(a.dy + (((int64_t)n * a.H + h) * a.W + px0) * CW_C + 64 * ch, (CW_PX * CW_C - 64) * 2);
+        make_rsrc(a.dy + (((int64_t)n * a.H + h) * a.W + px0) * CW_C + 64 * ch, (PX * CW_C - 64) * 2);
     const __amdgpu_buffer_rsrc_t rX =
         make_rsrc(a.x + ((int64_t)n * a.H + (rowok ? xr : 0)) * a.W * CW_C, rowok ? (int64_t)a.W * CW_C * 2 : 0);
 #pragma unroll
-    for (int i = 0; i < CW_DMA_PER_WAVE; ++i) {
+    for (int i = 0; i < DMA_PER_WAVE; ++i) {
       const int g = wave + 8 * i;  // wave-uniform
-      if (g < CW_DMA_D)
+      if (g < DMA_D)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rD, (lds_void*)((char*)&sD[buf][0] + 1024 * g), 16, (uint32_t)voff[i],
                                                  0, 0, 0);
-      else if (g < CW_DMA_N)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)((char*)&sX[buf][0] + 1024 * (g - CW_DMA_D)), 16,
+      else if (g < DMA_N)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)((char*)&sX[buf][0] + 1024 * (g - DMA_D)), 16,
                                                  (uint32_t)(voff[i] + px0 * CW_C * 2), 0, 0, 0);
     }
   };
-  if constexpr (DMA) {
+  if constexpr (NB == 2) {
+    if (T > 0) dma(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  } else if constexpr (DMA) {
     if (T > 0) dma(0);
     if (T > 1) {
       dma(1);
@@ -206,10 +217,12 @@ __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
     constexpr int par = decltype(par_c)::value;  // t & 1
     using SN = std::integral_constant<int, par ^ 1>;
     using SC = std::integral_constant<int, par>;
-    const int buf = bcur;
-    bcur = bcur == CW_NB - 1 ? 0 : bcur + 1;
-    if constexpr (DMA) {
-      if (t + 2 < T) dma(bcur == CW_NB - 1 ? 0 : bcur + 1);
+    const int buf = NB == 2 ? par : bcur;
+    bcur = bcur == NB - 1 ? 0 : bcur + 1;
+    if constexpr (NB == 2) {
+      if (t + 1 < T) dma(par ^ 1);  // stage (t + 1) & 1: last read by chunk t - 1
+    } else if constexpr (DMA) {
+      if (t + 2 < T) dma(bcur == NB - 1 ? 0 : bcur + 1);
     } else {
       if (t + 1 < T) stage(SN{}, bcur);
       if (t + 2 < T) load(SC{});
@@ -230,9 +243,9 @@ __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
     });                                                                                  \
   }
     SIREN_CW_RD(0)
-    static_for<0, CW_PX / 16>([&](auto ks_c) {
+    static_for<0, PX / 16>([&](auto ks_c) {
       constexpr int ks = decltype(ks_c)::value, b = ks & 1;
-      if constexpr (ks + 1 < CW_PX / 16) {
+      if constexpr (ks + 1 < PX / 16) {
         SIREN_CW_RD(ks + 1)
         asm volatile("s_waitcnt lgkmcnt(12)"
                      : "+v"(fa[b].lo), "+v"(fa[b].hi), "+v"(fb[b][0].lo), "+v"(fb[b][0].hi), "+v"(fb[b][1].lo),
@@ -252,8 +265,9 @@ __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
 #undef SIREN_CW_RD
     if constexpr (DMA) {
       // this wave's part of chunk t + 1 landed (chunk t + 2's 4 or 5 are younger); a barrier without
-      // __syncthreads' fence, which would drain chunk t + 2's DMA too (vmcnt(0))
-      if (t + 2 < T) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      // __syncthreads' fence, which would drain chunk t + 2's DMA too (vmcnt(0)); two stages: chunk
+      // t + 1 is the youngest
+      if (NB == 3 && t + 2 < T) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();

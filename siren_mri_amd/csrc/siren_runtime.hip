@@ -103,7 +103,8 @@ bool g_tail_reduce = true;  // a pair launch reduces the previous pair launch's 
 bool g_jvp_adj = true;
 bool g_jvp_tan = true;      // tangent streams of a hidden layer stacked by row (jvp_tan_kernel)
 bool g_f32_rows = true;     // fp32 hidden layers' forward / input gradient on the row-stacked tile
-bool g_wrw_dma = true;      // the 5x5 weight-gradient convolution's chunks filled by LDS-DMA (conv_wrw_k5_kernel DMA;
+int g_wrw_dma = 1;          // the 5x5 weight-gradient convolution's chunks filled by LDS-DMA (conv_wrw_k5_kernel DMA;
+                            // 2: 128-pixel chunks where W allows;
                             // C4 -0.05 ms/step, 5 of 6 one-box pairs: profiles/r6_ab_wrw_dma.txt)
 int g_conv_dma = 2;         // the 5x5 encoder convolutions' stages: 0 register staging, 1 LDS-DMA, 2 LDS-DMA with
                             // per-workgroup source offsets (conv_fwd_k5_kernel DMA; 2 is C4 -2 %,
@@ -2502,8 +2503,10 @@ int siren_conv_wrw_k5(const void* x, const void* dy, int N, int H, int W, int C,
   a.nsplit = nsplit;
   a.rows_per_split = cdiv(rows, nsplit);
   hipStream_t st = (hipStream_t)stream;
-  if (g_wrw_dma) hipLaunchKernelGGL(conv_wrw_k5_kernel<true>, dim3((unsigned)nsplit, CW_K, 2), dim3(512), 0, st, a);
-  else hipLaunchKernelGGL(conv_wrw_k5_kernel<false>, dim3((unsigned)nsplit, CW_K, 2), dim3(512), 0, st, a);
+  const dim3 wg((unsigned)nsplit, CW_K, 2);
+  if (g_wrw_dma == 2 && W % (2 * CW_PX) == 0) hipLaunchKernelGGL((conv_wrw_k5_kernel<true, 2 * CW_PX>), wg, dim3(512), 0, st, a);
+  else if (g_wrw_dma) hipLaunchKernelGGL((conv_wrw_k5_kernel<true>), wg, dim3(512), 0, st, a);
+  else hipLaunchKernelGGL((conv_wrw_k5_kernel<false>), wg, dim3(512), 0, st, a);
   int rc = check_launch("conv_wrw_k5");
   if (rc) return rc;
   hipLaunchKernelGGL(conv_wrw_reduce_kernel, dim3((unsigned)cdiv(CW_SLAB, 256)), dim3(256), 0, st, a);
@@ -3179,8 +3182,8 @@ int siren_config_set(const char* key, int64_t value) {
     g_jvp_adj = value != 0;
     return SIREN_OK;
   }
-  if (key && strcmp(key, "wrw_dma") == 0 && (value == 0 || value == 1)) {
-    g_wrw_dma = value != 0;
+  if (key && strcmp(key, "wrw_dma") == 0 && value >= 0 && value <= 2) {
+    g_wrw_dma = (int)value;
     return SIREN_OK;
   }
   if (key && strcmp(key, "conv_dma") == 0 && value >= 0 && value <= 2) {
@@ -3237,7 +3240,7 @@ int64_t siren_config_get(const char* key) {
   if (key && strcmp(key, "jvp_tan") == 0) return g_jvp_tan ? 1 : 0;
   if (key && strcmp(key, "f32_rows") == 0) return g_f32_rows ? 1 : 0;
   if (key && strcmp(key, "conv_dma") == 0) return g_conv_dma;
-  if (key && strcmp(key, "wrw_dma") == 0) return g_wrw_dma ? 1 : 0;
+  if (key && strcmp(key, "wrw_dma") == 0) return g_wrw_dma;
   if (key && strcmp(key, "dx_stagger") == 0) return g_dx_stagger ? 1 : 0;
   if (key && strcmp(key, "pair_ring") == 0) return g_pair_ring ? 1 : 0;
   if (key && strcmp(key, "debug_keep_p0") == 0) return g_keep_p0 ? 1 : 0;
