@@ -103,8 +103,8 @@ bool g_tail_reduce = true;  // a pair launch reduces the previous pair launch's 
 bool g_jvp_adj = true;
 bool g_jvp_tan = true;      // tangent streams of a hidden layer stacked by row (jvp_tan_kernel)
 bool g_f32_rows = true;     // fp32 hidden layers' forward / input gradient on the row-stacked tile
-int g_wrw_dma = 1;          // the 5x5 weight-gradient convolution's chunks filled by LDS-DMA (conv_wrw_k5_kernel DMA;
-                            // 2: 128-pixel chunks where W allows;
+int g_wrw_dma = 2;          // the 5x5 weight-gradient convolution's chunks filled by LDS-DMA (conv_wrw_k5_kernel DMA;
+                            // 2: 128-pixel chunks where W allows, C4 -0.33..-0.52 ms/step: profiles/r6_ab_wrw_128px.txt;
                             // C4 -0.05 ms/step, 5 of 6 one-box pairs: profiles/r6_ab_wrw_dma.txt)
 int g_conv_dma = 2;         // the 5x5 encoder convolutions' stages: 0 register staging, 1 LDS-DMA, 2 LDS-DMA with
                             // per-workgroup source offsets (conv_fwd_k5_kernel DMA; 2 is C4 -2 %,
