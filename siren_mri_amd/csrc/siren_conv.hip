@@ -58,10 +58,9 @@ struct ConvWArgs {
 // PX = 128 (option wrw_dma 2, DMA only, W a multiple of 128): 128-pixel chunks in two LDS stages
 // (135 KB), the chunk after next's DMA one chunk ahead; twice the MFMAs per barrier, DMA issue and
 // fragment-read ramp-up of a 64-pixel chunk.
-template <bool DMA, int PX = CW_PX, bool ILV = false>
+template <bool DMA, int PX = CW_PX>
 __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
   static_assert(PX == CW_PX || (DMA && PX == 2 * CW_PX), "64-pixel chunks, or 128 with the DMA fill");
-  static_assert(!ILV || PX == 2 * CW_PX, "the interleaved DMA issue: 128-pixel chunks (two stages)");
   constexpr int NB = PX == CW_PX ? CW_NB : 2;                // LDS stages
   constexpr int XROWS = PX + CW_K - 1;                       // halo rows
   constexpr int DMA_D = PX * 12 / 64;                        // dY instructions per chunk (12 / 24)
@@ -160,17 +159,9 @@ __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
       }
     }
   }
-  // DMA of the chunk at the cursor into stage buf, then the cursor advances one chunk: the buffer
-  // bases (setup, scalar) and the wave's instructions (issue i; ILV: one per K step of the chunk
-  // before, after that step's MFMAs, instead of all of them at the top of the iteration)
-  // (the chunk's state as plain scalars captured by reference: a kernel-local struct type broke the
-  // host-side stub of these instantiations)
-  int64_t c_drow = 0, c_xrow = 0;  // element offsets of the chunk's dY rows and of its X row
-  int c_px0 = 0, c_buf = 0, c_xbytes = 0;
-  auto dma_setup = [&](int buf) {
-    const int n = cn, h = ch_row;
-    c_px0 = cpx;
-    c_buf = buf;
+  // DMA of the chunk at the cursor into stage buf, then the cursor advances one chunk
+  auto dma = [&](int buf) {
+    const int n = cn, h = ch_row, px0 = cpx;
     cpx += PX;
     if (cpx == a.W) {
       cpx = 0;
@@ -181,25 +172,20 @@ __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
     }
     const int xr = h + kh - CW_K / 2;
     const bool rowok = xr >= 0 && xr < a.H;
-    c_drow = (((int64_t)n * a.H + h) * a.W + c_px0) * CW_C + 64 * ch;
-    c_xrow = ((int64_t)n * a.H + (rowok ? xr : 0)) * a.W * CW_C;
-    c_xbytes = rowok ? a.W * CW_C * 2 : 0;  // X row outside the image: every piece out of range
-  };
-  auto dma_issue = [&](int i) {
-    const int g = wave + 8 * i;  // wave-uniform
-    if (g < DMA_D)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(a.dy + c_drow, (PX * CW_C - 64) * 2),
-                                               (lds_void*)((char*)&sD[c_buf][0] + 1024 * g), 16, (uint32_t)voff[i], 0,
-                                               0, 0);
-    else if (g < DMA_N)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(a.x + c_xrow, c_xbytes),
-                                               (lds_void*)((char*)&sX[c_buf][0] + 1024 * (g - DMA_D)), 16,
-                                               (uint32_t)(voff[i] + c_px0 * CW_C * 2), 0, 0, 0);
-  };
-  auto dma = [&](int buf) {
-    dma_setup(buf);
+    const __amdgpu_buffer_rsrc_t rD =
+        make_rsrc(a.dy + (((int64_t)n * a.H + h) * a.W + px0) * CW_C + 64 * ch, (PX * CW_C - 64) * 2);
+    const __amdgpu_buffer_rsrc_t rX =
+        make_rsrc(a.x + ((int64_t)n * a.H + (rowok ? xr : 0)) * a.W * CW_C, rowok ? (int64_t)a.W * CW_C * 2 : 0);
 #pragma unroll
-    for (int i = 0; i < DMA_PER_WAVE; ++i) dma_issue(i);
+    for (int i = 0; i < DMA_PER_WAVE; ++i) {
+      const int g = wave + 8 * i;  // wave-uniform
+      if (g < DMA_D)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rD, (lds_void*)((char*)&sD[buf][0] + 1024 * g), 16, (uint32_t)voff[i],
+                                                 0, 0, 0);
+      else if (g < DMA_N)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)((char*)&sX[buf][0] + 1024 * (g - DMA_D)), 16,
+                                                 (uint32_t)(voff[i] + px0 * CW_C * 2), 0, 0, 0);
+    }
   };
   if constexpr (NB == 2) {
     if (T > 0) dma(0);
@@ -233,11 +219,8 @@ __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
     using SC = std::integral_constant<int, par>;
     const int buf = NB == 2 ? par : bcur;
     bcur = bcur == NB - 1 ? 0 : bcur + 1;
-    const bool more = t + 1 < T;
-    if constexpr (ILV) {
-      if (more) dma_setup(par ^ 1);  // issued in the K loop below
-    } else if constexpr (NB == 2) {
-      if (more) dma(par ^ 1);  // stage (t + 1) & 1: last read by chunk t - 1
+    if constexpr (NB == 2) {
+      if (t + 1 < T) dma(par ^ 1);  // stage (t + 1) & 1: last read by chunk t - 1
     } else if constexpr (DMA) {
       if (t + 2 < T) dma(bcur == NB - 1 ? 0 : bcur + 1);
     } else {
@@ -278,16 +261,6 @@ __global__ __launch_bounds__(512) void conv_wrw_k5_kernel(ConvWArgs a) {
         constexpr int kw = decltype(kw_c)::value;
         acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr16_value(fa[b]), tr16_value(fb[b][kw]), acc[kw], 0, 0, 0);
       });
-      if constexpr (ILV) {
-        // instructions ks (and, at the last K step, the rest) of the next chunk's DMA
-        if (more) {
-          if constexpr (ks + 1 < PX / 16) {
-            if constexpr (ks < DMA_PER_WAVE) dma_issue(ks);
-          } else {
-            static_for<ks, DMA_PER_WAVE>([&](auto i_c) { dma_issue(decltype(i_c)::value); });
-          }
-        }
-      }
     });
 #undef SIREN_CW_RD
     if constexpr (DMA) {

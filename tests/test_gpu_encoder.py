@@ -214,9 +214,8 @@ def test_conv_weight_gradient_kernel_against_fp32(N, H, W):
     prev = _native.get_option("wrw_dma")
     outs = {}
     try:
-        for dma in (0, 1, 1, 2, 3):  # register staging; LDS-DMA (option wrw_dma) twice: run-to-run equality;
-            # 2: 128-pixel chunks (W a multiple of 128; else the 64-pixel form runs); 3: 2 with its DMA
-            # issued in the K loop
+        for dma in (0, 1, 1, 2):  # register staging; LDS-DMA (option wrw_dma) twice: run-to-run equality;
+            # 2: 128-pixel chunks (W a multiple of 128; else the 64-pixel form runs)
             _native.set_option("wrw_dma", dma)
             dw = torch.empty(128, 128, 5, 5, device=DEV).contiguous(memory_format=torch.channels_last)
             _native.check(lib.siren_conv_wrw_k5(xd.data_ptr(), dyd.data_ptr(), N, H, W, 128, dw.data_ptr(),
@@ -230,7 +229,6 @@ def test_conv_weight_gradient_kernel_against_fp32(N, H, W):
     assert torch.equal(outs[1][0], outs[1][1])
     # 128-pixel chunks: the same K steps in the same pixel order, so bit-identical too
     assert torch.equal(outs[2][0], outs[0][0])
-    assert torch.equal(outs[3][0], outs[0][0])
 
 
 @pytest.mark.parametrize("dma", [0, 1, 2, 3])
