@@ -485,7 +485,7 @@ __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
   const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.w, (int64_t)CW_C * CW_K * CW_K * CW_C * 2);
   // DMA 2: per instruction i, the lane's stage-(0, 0) offset and (x part) its row test value
   int pbase[CF_DMA_PER_WAVE], prow[CF_DMA_PER_WAVE];
-  if constexpr (DMA >= 2) {
+  if constexpr (DMA == 2) {
 #pragma unroll
     for (int i = 0; i < CF_DMA_PER_WAVE; ++i) {
       const int g = wave + 8 * i;
@@ -507,26 +507,22 @@ __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
       }
     }
   }
-  // forms 2, 3: this wave's DMA instruction i of stage s into buffer buf
-  auto dma1 = [&](int s, int buf, int i) {
-    const int kh = s >> 2, cc = s & 3;
-    char* base = smem_cf + buf * STG;
-    const int xadd = kh * CF_W * CW_C * 2 + CF_CC * cc * 2, wadd = kh * CW_K * CW_C * 2 + CF_CC * cc * 2;
-    const int g = wave + 8 * i;  // wave-uniform
-    if (g < CF_DMA_XN) {
-      const uint32_t off = (uint32_t)(prow[i] + kh) < (uint32_t)a.H ? (uint32_t)(pbase[i] + xadd) : 0x7fffffffu;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)(base + 1024 * g), 16, off, 0, 0, 0);
-    } else if (g < CF_DMA_N) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(base + 1024 * g), 16, (uint32_t)(pbase[i] + wadd), 0, 0,
-                                               0);
-    }
-  };
   auto dma = [&](int s, int buf) {
     const int kh = s >> 2, cc = s & 3;
     char* base = smem_cf + buf * STG;
-    if constexpr (DMA >= 2) {
+    if constexpr (DMA == 2) {
+      const int xadd = kh * CF_W * CW_C * 2 + CF_CC * cc * 2, wadd = kh * CW_K * CW_C * 2 + CF_CC * cc * 2;
 #pragma unroll
-      for (int i = 0; i < CF_DMA_PER_WAVE; ++i) dma1(s, buf, i);
+      for (int i = 0; i < CF_DMA_PER_WAVE; ++i) {
+        const int g = wave + 8 * i;  // wave-uniform
+        if (g < CF_DMA_XN) {
+          const uint32_t off = (uint32_t)(prow[i] + kh) < (uint32_t)a.H ? (uint32_t)(pbase[i] + xadd) : 0x7fffffffu;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)(base + 1024 * g), 16, off, 0, 0, 0);
+        } else if (g < CF_DMA_N) {
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(base + 1024 * g), 16, (uint32_t)(pbase[i] + wadd),
+                                                   0, 0, 0);
+        }
+      }
       return;
     }
 #pragma unroll
@@ -566,9 +562,7 @@ __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
     constexpr int par = decltype(par_c)::value;
     using SN = std::integral_constant<int, par ^ 1>;
     using SC = std::integral_constant<int, par>;
-    if constexpr (DMA == 3) {
-      // the next stage's DMA is issued one instruction per K step, after that step's MFMAs
-    } else if constexpr (DMA) {
+    if constexpr (DMA) {
       if (s + 1 < NS) dma(s + 1, (s + 1) & 1);
     } else {
       if (s + 1 < NS) stage(SN{}, (s + 1) & 1);
@@ -599,10 +593,6 @@ __global__ __launch_bounds__(512) void conv_fwd_k5_kernel(ConvFArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[b][ii], bfr[b][j], acc[ii][j], 0, 0, 0);
-      if constexpr (DMA == 3 && i < CF_DMA_PER_WAVE) {
-        static_assert(CF_DMA_PER_WAVE <= 2 * CW_K, "one DMA instruction per K step");
-        if (s + 1 < NS) dma1(s + 1, (s + 1) & 1, i);
-      }
     });
 #undef SIREN_CF_RD
     if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of stage s + 1

@@ -2236,8 +2236,7 @@ int loss_path_fail(const siren_mlp_desc* d) {
 // conv_fwd_k5_kernel in the stage-fill form of option conv_dma
 template <int EPI>
 void launch_conv_fwd_k5(dim3 grid, hipStream_t st, const ConvFArgs& a) {
-  if (g_conv_dma == 3) hipLaunchKernelGGL((conv_fwd_k5_kernel<EPI, 3>), grid, dim3(512), 0, st, a);
-  else if (g_conv_dma == 2) hipLaunchKernelGGL((conv_fwd_k5_kernel<EPI, 2>), grid, dim3(512), 0, st, a);
+  if (g_conv_dma == 2) hipLaunchKernelGGL((conv_fwd_k5_kernel<EPI, 2>), grid, dim3(512), 0, st, a);
   else if (g_conv_dma == 1) hipLaunchKernelGGL((conv_fwd_k5_kernel<EPI, 1>), grid, dim3(512), 0, st, a);
   else hipLaunchKernelGGL((conv_fwd_k5_kernel<EPI, 0>), grid, dim3(512), 0, st, a);
 }
@@ -2680,7 +2679,7 @@ int siren_conv_fwd(const void* x, const void* w, const void* bias, int relu, voi
   const dim3 grid((unsigned)(N * (H / 2)), (unsigned)(CO / (big ? 128 : 64)));
 #define SIREN_CF(K, C, T)                                                                           \
   do {                                                                                              \
-    if (g_conv_dma >= 2) hipLaunchKernelGGL((conv_fwd_gen_kernel<K, C, T, true>), grid, dim3(512), 0, st, a); \
+    if (g_conv_dma == 2) hipLaunchKernelGGL((conv_fwd_gen_kernel<K, C, T, true>), grid, dim3(512), 0, st, a); \
     else hipLaunchKernelGGL((conv_fwd_gen_kernel<K, C, T, false>), grid, dim3(512), 0, st, a);      \
   } while (0)
   if (KS == 3) {
@@ -3187,7 +3186,7 @@ int siren_config_set(const char* key, int64_t value) {
     g_wrw_dma = (int)value;
     return SIREN_OK;
   }
-  if (key && strcmp(key, "conv_dma") == 0 && value >= 0 && value <= 3) {
+  if (key && strcmp(key, "conv_dma") == 0 && value >= 0 && value <= 2) {
     g_conv_dma = (int)value;
     return SIREN_OK;
   }
