@@ -42,14 +42,59 @@ struct HyArgs {
 
 enum { HY_BIAS_RELU = 0, HY_BIAS = 1, HY_DWDB = 2, HY_PART = 3, HY_MASK = 4, HY_PLAIN = 5 };
 
+// One operand tile (R rows of the M or N extent x BK k) into LDS dst[k][r] in 16-byte quads along
+// the operand's contiguous dimension: T 0 reads X[r ld + k] (k contiguous), T 1 reads X[k ld + r]
+// (r contiguous). A quad in range of an aligned operand (ld % 4 == 0, 16-byte base) is one 16-byte
+// load, any other quad four bounds-checked single loads (zeros outside); the values are the same.
+template <int T, int R, int BK, int RS>
+DEV void hy_stage(const float* X, int ld, bool vec, int r0, int rlim, int kb, int k1, float (*dst)[RS], int tid) {
+  constexpr int NQ = R * BK / 4;
+#pragma unroll
+  for (int q = 0; q < (NQ + 255) / 256; ++q) {
+    const int e = tid + 256 * q;
+    if (NQ % 256 != 0 && e >= NQ) break;
+    if (T == 0) {
+      const int r = e / (BK / 4), kq = 4 * (e % (BK / 4));
+      const int gr = r0 + r, gk = kb + kq;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (vec && gr < rlim && gk + 3 < k1) {
+        v = *(const f32x4*)(X + (int64_t)gr * ld + gk);
+      } else if (gr < rlim) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (gk + c < k1) v[c] = X[(int64_t)gr * ld + gk + c];
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dst[kq + c][r] = v[c];
+    } else {
+      const int rq = 4 * (e % (R / 4)), k = e / (R / 4);
+      const int gr = r0 + rq, gk = kb + k;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (vec && gk < k1 && gr + 3 < rlim) {
+        v = *(const f32x4*)(X + (int64_t)gk * ld + gr);
+      } else if (gk < k1) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (gr + c < rlim) v[c] = X[(int64_t)gk * ld + gr + c];
+      }
+      *(f32x4*)&dst[k][rq] = v;
+    }
+  }
+}
+
 // BM x BN tile (BM 64: 64 x 64; BM 32: 32 x 128, the heads' 32-row latent batches), 4 x 4 outputs
-// per thread: rows tm + (BM / 4) i, columns tn + (BN / 4) j
+// per thread: rows 4 tm + i, columns 4 tn + j, so a thread's four A and four B values of a K step
+// are one 16-byte LDS read each (round 6: with rows tm + (BM / 4) i the 8 single-dword LDS reads per
+// 16 FMAs were the bound — ds_read_b32 moves 128 B/clk/CU, ds_read_b128 256); the same products
+// in the same K order per output.
 template <int TA, int TB, int EPI, int BM>
 __global__ __launch_bounds__(256) void hy_gemm_kernel(HyArgs a) {
-  constexpr int BN = 4096 / BM, BK = 16, SM = BM / 4, SN = BN / 4;
+  constexpr int BN = 4096 / BM, BK = 16, SM = BM / 4;
   static_assert(BM == 32 || BM == 64, "tile");
-  __shared__ float As[BK][BM + 1];
-  __shared__ float Bs[BK][BN + 1];
+  // rows padded by 4 floats: the 16-byte reads stay aligned, and the k-major staging stores of
+  // 16 k x 4 m (or n) per wave land on 64 distinct banks
+  __shared__ __attribute__((aligned(16))) float As[BK][BM + 4];
+  __shared__ __attribute__((aligned(16))) float Bs[BK][BN + 4];
   const int tid = threadIdx.x;
   const int tm = tid % SM, tn = tid / SM;
   int gi = 0;
@@ -76,37 +121,18 @@ __global__ __launch_bounds__(256) void hy_gemm_kernel(HyArgs a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
   }
 
+  // 16-byte staging loads where the operand allows (uniform per group)
+  // (k-contiguous operands also need the split's first k on a quad boundary)
+  const bool veca = G.lda % 4 == 0 && ((uintptr_t)G.A & 15) == 0 && (TA == 1 || k0 % 4 == 0);
+  const bool vecb = G.ldb % 4 == 0 && ((uintptr_t)G.B & 15) == 0 && (TB == 1 || k0 % 4 == 0);
   for (int kb = k0; kb < k1; kb += BK) {
-#pragma unroll
-    for (int q = 0; q < BM * BK / 256; ++q) {
-      const int e = tid + 256 * q;
-      int mm, kk;
-      if (TA == 0) { kk = e % BK; mm = e / BK; }
-      else { mm = e % BM; kk = e / BM; }
-      const int m = m0 + mm, k = kb + kk;
-      float v = 0.f;
-      if (m < G.M && k < k1) v = TA == 0 ? G.A[(int64_t)m * G.lda + k] : G.A[(int64_t)k * G.lda + m];
-      As[kk][mm] = v;
-    }
-#pragma unroll
-    for (int q = 0; q < BN * BK / 256; ++q) {
-      const int e = tid + 256 * q;
-      int nn, kk;
-      if (TB == 0) { kk = e % BK; nn = e / BK; }
-      else { nn = e % BN; kk = e / BN; }
-      const int n = n0 + nn, k = kb + kk;
-      float v = 0.f;
-      if (k < k1 && n < NB) v = TB == 0 ? G.B[(int64_t)n * G.ldb + k] : G.B[(int64_t)k * G.ldb + n];
-      Bs[kk][nn] = v;
-    }
+    hy_stage<TA, BM, BK, BM + 4>(G.A, G.lda, veca, m0, G.M, kb, k1, As, tid);
+    hy_stage<TB, BN, BK, BN + 4>(G.B, G.ldb, vecb, n0, NB, kb, k1, Bs, tid);
     __syncthreads();
 #pragma unroll
     for (int kk = 0; kk < BK; ++kk) {
-      float av[4], bv[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) av[i] = As[kk][tm + SM * i];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bv[j] = Bs[kk][tn + SN * j];
+      const f32x4 av = *(const f32x4*)&As[kk][4 * tm];
+      const f32x4 bv = *(const f32x4*)&Bs[kk][4 * tn];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if (EPI == HY_DWDB) rs[i] += av[i];
@@ -119,12 +145,12 @@ __global__ __launch_bounds__(256) void hy_gemm_kernel(HyArgs a) {
 
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int m = m0 + tm + SM * i;
+    const int m = m0 + 4 * tm + i;
     if (m >= G.M) continue;
     if (EPI == HY_DWDB && n0 == 0 && tn == 0) G.db[m] = rs[i];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int n = n0 + tn + SN * j;
+      const int n = n0 + 4 * tn + j;
       if (n >= NB) continue;
       float v = acc[i][j];
       if (EPI == HY_BIAS_RELU) {
