@@ -507,7 +507,9 @@ int siren_sincos_f32(const float* x, float* s, float* c, int64_t n, int impl, vo
  *                    for the others; 0: register staging (all forms bit-identical).
  *   "wrw_dma"        2 (default): the 5x5 weight-gradient convolution's 128-pixel chunks (W a
  *                    multiple of 128, else 64) filled by LDS-DMA; 1: 64-pixel chunks by LDS-DMA;
- *                    0: 64-pixel chunks by register staging (all bit-identical).
+ *                    0: 64-pixel chunks by register staging; 3: 2, and the other shapes' weight
+ *                    gradients (cnn[0]'s 7x7, the 3x3 forms) in 128-pixel LDS-DMA chunks too
+ *                    (all bit-identical).
  *   "debug_fused_profile"  device address of an int64 buffer [grid][4] that receives per-
  *                    workgroup cycle counts of the fused forward's phases, or 0 (off).
  * Returns SIREN_OK, or SIREN_EINVAL for an unknown key / value. Not thread-safe.

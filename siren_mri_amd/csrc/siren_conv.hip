@@ -1016,24 +1016,33 @@ __global__ __launch_bounds__(512) void conv_fwd_gen_kernel(ConvGArgs a) {
   }
 }
 
-template <int KS, int CI, int CB>
+// DMA (option wrw_dma 3, W a multiple of 128): conv_wrw_k5_kernel's 128-pixel LDS-DMA form for
+// these shapes — two stages, the next chunk's DMA one chunk ahead, lane offsets fixed per
+// workgroup (rows of COW / 8 + 4 and CI / 8 + 4 16-byte slots, the pads and pixels outside the
+// image out of range); the same K steps in the same pixel order as the 64-pixel form.
+template <int KS, int CI, int CB, bool DMA = false>
 __global__ __launch_bounds__(512) void conv_wrw_gen_kernel(ConvGArgs a) {
   constexpr int IB = CI / 32;
   static_assert(CB * IB == 8, "8 waves: CB co blocks x IB ci blocks");
+  constexpr int PX = DMA ? 2 * CW_PX : CW_PX;  // pixels per chunk
+  constexpr int NB = DMA ? 2 : CW_NB;          // LDS stages
   constexpr int COW = 32 * CB;                 // output channels per workgroup
-  constexpr int XR = CW_PX + KS - 1;           // halo rows
+  constexpr int XR = PX + KS - 1;              // halo rows
   constexpr int DROW = COW + 32, XROW = CI + 32;  // bf16 per staged row (+64-byte pad)
-  constexpr int DP = CW_PX * COW / 8, XPC = XR * CI / 8;  // 16-byte pieces
+  constexpr int DP = CW_PX * COW / 8, XPC = (CW_PX + KS - 1) * CI / 8;  // 16-byte pieces (64-pixel form)
   constexpr int NDL = (DP + 511) / 512, NXL = (XPC + 511) / 512;
-  __shared__ __attribute__((aligned(16))) bf16 sD[CW_NB][CW_PX * DROW];
-  __shared__ __attribute__((aligned(16))) bf16 sX[CW_NB][XR * XROW];
+  constexpr int DSL = COW / 8 + 4, XSL = CI / 8 + 4;  // 16-byte slots per staged row
+  constexpr int DMA_D = PX * DSL / 64, DMA_X = (XR * XSL + 63) / 64, DMA_N = DMA_D + DMA_X;
+  constexpr int DMA_PER_WAVE = (DMA_N + 7) / 8;
+  __shared__ __attribute__((aligned(16))) bf16 sD[NB][PX * DROW];
+  __shared__ __attribute__((aligned(16))) bf16 sX[NB][DMA ? DMA_X * 512 : XR * XROW];
   const int split = blockIdx.x, kh = blockIdx.y, ch = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cb = wave % CB, ib = wave / CB;
   const int nrows = a.N * a.H;
   const int r0 = split * (int)a.rows_per_split;
   const int r1 = r0 + (int)a.rows_per_split < nrows ? r0 + (int)a.rows_per_split : nrows;
-  const int nch = a.W / CW_PX;
+  const int nch = a.W / PX;
   const int T = r1 > r0 ? (r1 - r0) * nch : 0;
   const int CO = a.CO;
 
@@ -1096,27 +1105,79 @@ __global__ __launch_bounds__(512) void conv_wrw_gen_kernel(ConvGArgs a) {
   const int r8 = 8 * (g >> 1) + tq;
   const uint32_t dbase = lds_addr(&sD[0][0]) + (uint32_t)((r8 * DROW + ca) * 2);
   const uint32_t xbase = lds_addr(&sX[0][0]) + (uint32_t)((r8 * XROW + cx) * 2);
-  constexpr uint32_t DSTAGE = CW_PX * DROW * 2, XSTAGE = XR * XROW * 2;
+  constexpr uint32_t DSTAGE = PX * DROW * 2, XSTAGE = DMA ? DMA_X * 1024 : XR * XROW * 2;
   constexpr int DROWB = DROW * 2, XROWB = XROW * 2;
   constexpr int NRD = 2 + 2 * KS;  // fragment reads per K step
 
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
-  if (T > 0) {
-    load(S0{});
-    stage(S0{}, 0);
+  int voff[DMA_PER_WAVE];
+  if constexpr (DMA) {
+#pragma unroll
+    for (int i = 0; i < DMA_PER_WAVE; ++i) {
+      const int gi = wave + 8 * i;
+      if (gi < DMA_D) {
+        const int slot = 64 * gi + lane, row = slot / DSL, pc = slot - DSL * (slot / DSL);
+        voff[i] = pc < COW / 8 ? row * CO * 2 + 16 * pc : 0x7fffffff;
+      } else {
+        const int slot = 64 * (gi - DMA_D) + lane, row = slot / XSL, pc = slot - XSL * (slot / XSL);
+        voff[i] = (pc < CI / 8 && row < XR) ? (row - KS / 2) * CI * 2 + 16 * pc : 0x40000000;
+      }
+    }
   }
-  if (T > 1) load(S1{});
+  auto dma = [&](int buf) {
+    const int n = cn, h = crow, px0 = cpx;
+    cpx += PX;
+    if (cpx == a.W) {
+      cpx = 0;
+      if (++crow == a.H) {
+        crow = 0;
+        ++cn;
+      }
+    }
+    const int xr = h + kh - KS / 2;
+    const bool rowok = xr >= 0 && xr < a.H;
+    const __amdgpu_buffer_rsrc_t rD = make_rsrc(a.dy + (((int64_t)n * a.H + h) * a.W + px0) * CO + COW * ch,
+                                                ((int64_t)(PX - 1) * CO + COW) * 2);
+    const __amdgpu_buffer_rsrc_t rX =
+        make_rsrc(a.x + ((int64_t)n * a.H + (rowok ? xr : 0)) * a.W * CI, rowok ? (int64_t)a.W * CI * 2 : 0);
+#pragma unroll
+    for (int i = 0; i < DMA_PER_WAVE; ++i) {
+      const int gi = wave + 8 * i;  // wave-uniform
+      if (gi < DMA_D)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rD, (lds_void*)((char*)&sD[buf][0] + 1024 * gi), 16,
+                                                 (uint32_t)voff[i], 0, 0, 0);
+      else if (gi < DMA_N)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)((char*)&sX[buf][0] + 1024 * (gi - DMA_D)), 16,
+                                                 (uint32_t)(voff[i] + px0 * CI * 2), 0, 0, 0);
+    }
+  };
+  if constexpr (DMA) {
+    if (T > 0) dma(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  } else {
+    if (T > 0) {
+      load(S0{});
+      stage(S0{}, 0);
+    }
+    if (T > 1) load(S1{});
+  }
   int bcur = 0;  // t % CW_NB
   __syncthreads();
   auto iter = [&](int t, auto par_c) {
     constexpr int par = decltype(par_c)::value;
     using SN = std::integral_constant<int, par ^ 1>;
     using SC = std::integral_constant<int, par>;
-    const int buf = bcur;
+    const int buf = DMA ? par : bcur;
     bcur = bcur == CW_NB - 1 ? 0 : bcur + 1;
-    if (t + 1 < T) stage(SN{}, bcur);
-    if (t + 2 < T) load(SC{});
+    if constexpr (DMA) {
+      if (t + 1 < T) dma(par ^ 1);  // stage (t + 1) & 1: last read by chunk t - 1
+    } else {
+      if (t + 1 < T) stage(SN{}, bcur);
+      if (t + 2 < T) load(SC{});
+    }
     const uint32_t db = dbase + buf * DSTAGE, xb = xbase + buf * XSTAGE;
     TrFrag fa[2], fb[2][KS];
 #define SIREN_CWG_RD(KS_)                                                         \
@@ -1131,9 +1192,9 @@ __global__ __launch_bounds__(512) void conv_wrw_gen_kernel(ConvGArgs a) {
     });                                                                           \
   }
     SIREN_CWG_RD(0)
-    static_for<0, CW_PX / 16>([&](auto ks_c) {
+    static_for<0, PX / 16>([&](auto ks_c) {
       constexpr int ks = decltype(ks_c)::value, b = ks & 1;
-      if constexpr (ks + 1 < CW_PX / 16) {
+      if constexpr (ks + 1 < PX / 16) {
         SIREN_CWG_RD(ks + 1)
         lgkm_wait<NRD>();
       } else {
@@ -1147,7 +1208,15 @@ __global__ __launch_bounds__(512) void conv_wrw_gen_kernel(ConvGArgs a) {
       });
     });
 #undef SIREN_CWG_RD
-    __syncthreads();
+    if constexpr (DMA) {
+      // this wave's part of chunk t + 1 landed; a barrier without __syncthreads' fence
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      __syncthreads();
+    }
   };
   for (int t = 0; t < T; t += 2) {
     iter(t, S0{});

@@ -2504,7 +2504,7 @@ int siren_conv_wrw_k5(const void* x, const void* dy, int N, int H, int W, int C,
   a.rows_per_split = cdiv(rows, nsplit);
   hipStream_t st = (hipStream_t)stream;
   const dim3 wg((unsigned)nsplit, CW_K, 2);
-  if (g_wrw_dma == 2 && W % (2 * CW_PX) == 0) hipLaunchKernelGGL((conv_wrw_k5_kernel<true, 2 * CW_PX>), wg, dim3(512), 0, st, a);
+  if (g_wrw_dma >= 2 && W % (2 * CW_PX) == 0) hipLaunchKernelGGL((conv_wrw_k5_kernel<true, 2 * CW_PX>), wg, dim3(512), 0, st, a);
   else if (g_wrw_dma) hipLaunchKernelGGL((conv_wrw_k5_kernel<true>), wg, dim3(512), 0, st, a);
   else hipLaunchKernelGGL((conv_wrw_k5_kernel<false>), wg, dim3(512), 0, st, a);
   int rc = check_launch("conv_wrw_k5");
@@ -2764,7 +2764,10 @@ int siren_conv_wrw(const void* x, const void* dy, int N, int H, int W, int CI, i
   const dim3 rgrid((unsigned)cdiv(slab, 256));
 #define SIREN_CW(K, C, B)                                                               \
   {                                                                                      \
-    hipLaunchKernelGGL((conv_wrw_gen_kernel<K, C, B>), grid, dim3(512), 0, st, a);        \
+    if (g_wrw_dma == 3 && W % 128 == 0)                                                  \
+      hipLaunchKernelGGL((conv_wrw_gen_kernel<K, C, B, true>), grid, dim3(512), 0, st, a); \
+    else                                                                                 \
+      hipLaunchKernelGGL((conv_wrw_gen_kernel<K, C, B>), grid, dim3(512), 0, st, a);      \
     if ((rc = check_launch("conv_wrw_gen"))) return rc;                                  \
     hipLaunchKernelGGL((conv_wrw_gen_reduce_kernel<K, C>), rgrid, dim3(256), 0, st, a);   \
   }
@@ -3182,7 +3185,7 @@ int siren_config_set(const char* key, int64_t value) {
     g_jvp_adj = value != 0;
     return SIREN_OK;
   }
-  if (key && strcmp(key, "wrw_dma") == 0 && value >= 0 && value <= 2) {
+  if (key && strcmp(key, "wrw_dma") == 0 && value >= 0 && value <= 3) {
     g_wrw_dma = (int)value;
     return SIREN_OK;
   }

@@ -336,12 +336,18 @@ def test_generic_conv_weight_gradient_kernel_against_fp32(k, ci, co, N, H, W):
     dyd = dy.to(DEV).contiguous(memory_format=torch.channels_last)
     ws = torch.empty(int(lib.siren_conv_wrw_ws_bytes(N, H, W, ci, co, k)), dtype=torch.uint8, device=DEV)
     outs = []
-    for _ in range(2):
-        dw = torch.empty(co, ci, k, k, device=DEV).contiguous(memory_format=torch.channels_last)
-        _native.check(lib.siren_conv_wrw(xd.data_ptr(), dyd.data_ptr(), N, H, W, ci, co, k, dw.data_ptr(), ws.data_ptr(),
-                                         ws.numel(), _native.stream_handle(DEV)), "conv_wrw")
-        outs.append(dw)
+    prev = _native.get_option("wrw_dma")
+    try:
+        for dma in (prev, prev, 3):  # the default twice (run-to-run), then the 128-pixel LDS-DMA form
+            _native.set_option("wrw_dma", dma)
+            dw = torch.empty(co, ci, k, k, device=DEV).contiguous(memory_format=torch.channels_last)
+            _native.check(lib.siren_conv_wrw(xd.data_ptr(), dyd.data_ptr(), N, H, W, ci, co, k, dw.data_ptr(),
+                                             ws.data_ptr(), ws.numel(), _native.stream_handle(DEV)), "conv_wrw")
+            outs.append(dw)
+    finally:
+        _native.set_option("wrw_dma", prev)
     assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[2])  # the same K steps in the same pixel order
     assert orc.norm_rel(outs[0].cpu(), ref) < 1e-6
 
 
